@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X INA aggregation path.
+
+Metric (BASELINE.json): aggregated-gradient GB/s (device-resident), 8-worker x
+100 MB int32 sum-reduce.  One "step" = one W-way sum-reduce launch over one
+bucket of BASELINE config 3: W = 8 worker buffers of 26,214,400 int32 (100 MiB
+each, V = 256 packet slots -> 102,400 slots), resident in HBM, reduced into one
+aggregate -- the work the Tofino's Processor registers do per slot
+(processor.p4:14-24).  value = W * n * 4 bytes * steps * ranks / max-rank time.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU; each rank
+      aggregates its own bucket: slot ranges shard with no data-path collective,
+      "scaling": "weak")
+
+Extra rows (not the headline): --extra writes per-kernel timings of the other
+configs (fused quantise+reduce C2, int16 C4, pack/unpack, PS combine, end-to-end
+with pinned H2D/D2H) to gpurun_out/bench_extra.json.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
+sys.path.insert(0, REPO)
+
+METRIC = "aggregated-gradient GB/s (device-resident), 8-worker×100 MB int32 sum-reduce"
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+W_WORKERS = 8
+N_VALUES = 26_214_400        # 100 MiB of int32 per worker (config 3)
+V_SLOT = 256
+ROTATE = 2                   # input sets alternated per step (943 MB each > 256 MB MALL)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workers", type=int, default=W_WORKERS)
+    ap.add_argument("--values", type=int, default=N_VALUES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 22,
+                    help="values per worker in the bounded CPU-baseline sample")
+    ap.add_argument("--extra", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_sum_reduce_c3.json"))
+    return ap.parse_args()
+
+
+def init_dist(args):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_inputs(W, n, seed_base, dev):
+    g = torch.Generator(device=dev)
+    bufs = []
+    for w in range(W):
+        g.manual_seed(seed_base + w)   # seed = 1000 + w, offset per rank/set
+        bufs.append(torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev,
+                                  generator=g))
+    return bufs
+
+
+def load_traffic(path, W, n):
+    try:
+        t = json.load(open(path))
+        if t.get("workers") == W and t.get("values") == n:
+            return t.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(args, bufs_host, gpu_out_sample):
+    from oracle import oracle as orc
+    n = bufs_host[0].size
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(cores, 16))
+    res = {}
+    for P in sorted({1, threads}):
+        ts = []
+        out = None
+        for _ in range(3):
+            out, secs = orc.cpu_packetise_aggregate(bufs_host, V_SLOT, P)
+            ts.append(secs)
+        res[P] = (statistics.median(ts), out)
+    tP, outP = res[threads]
+    t1, _ = res[1]
+    W = len(bufs_host)
+    ok = bool(np.array_equal(outP, gpu_out_sample))
+    return {
+        "value": round(W * n * 4 / tP / 1e9, 3), "unit": "GB/s", "cores": threads,
+        "kind": "port",
+        "sample": (f"{W} workers x {n} int32 (first {n * 4 // (1 << 20)} MiB of each config-3 "
+                   f"bucket): NGA-{V_SLOT} packetise (header + memcpy + htonl per packet, "
+                   f"communicator.cc:51-63) -> P4 aggregator restatement (count/frag/Processor "
+                   f"registers, ngaa.p4:120-196) -> PS ack, median of 3, {threads} threads split "
+                   f"as communicator.py:133-157"),
+        "value_1core": round(W * n * 4 / t1 / 1e9, 3),
+        "affinity_cores": cores,
+        "matches_gpu": ok,
+    }
+
+
+def main():
+    args = parse()
+    rank, world, local = init_dist(args)
+    dev = torch.device(f"cuda:{local}")
+    from ina_amd import ops
+
+    W, n = args.workers, args.values
+    sets = [make_inputs(W, n, 1000 + 100 * (rank * ROTATE + r), dev) for r in range(ROTATE)]
+    outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(ROTATE)]
+    torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        ops.sum_reduce(sets[i % ROTATE], out=outs[i % ROTATE])
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        ops.sum_reduce(sets[i % ROTATE], out=outs[i % ROTATE])
+        ev[i][1].record(stream)
+    barrier(world)
+    t1 = time.perf_counter()
+    elapsed = max_over_ranks(t1 - t0, world)
+    launch_ms = [a.elapsed_time(b) for a, b in ev]
+    avg_launch_s = statistics.mean(launch_ms) / 1e3
+    avg_launch_s = max_over_ranks(avg_launch_s, world)
+
+    # correctness spot check of the measured output (first slots) against the oracle
+    check_n = min(n, 1 << 16)
+    from oracle import oracle as orc
+    last = (args.steps - 1) % ROTATE
+    want = orc.sum_reduce_i32([b[:check_n].cpu().numpy() for b in sets[last]])
+    parity = bool(np.array_equal(outs[last][:check_n].cpu().numpy(), want))
+
+    worker_bytes = W * n * 4
+    algo_bytes = (W + 1) * n * 4
+    value = worker_bytes * args.steps * world / elapsed / 1e9
+    achieved = algo_bytes / avg_launch_s / 1e9
+    traffic = load_traffic(args.traffic_file, W, n)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (int32 uniform in [-2^20, 2^20), torch generator seed 1000+w per worker)",
+        "config": {"workload": "C3: 8 workers x 100 MiB int32 (26,214,400 values), V=256 slots",
+                   "workers": W, "values_per_worker": n, "slot_values": V_SLOT,
+                   "slots": (n + V_SLOT - 1) // V_SLOT,
+                   "parallelism": f"slot-range shards, one bucket per rank x {world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "kernel": "k_sum_reduce_i32_vec<8,2,nt>",
+                     "algorithmic_bytes_per_launch": algo_bytes,
+                     "avg_launch_us": round(avg_launch_s * 1e6, 2)},
+        "parity_spot_check": parity,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        s = min(args.cpu_sample, n)
+        host = [b[:s].cpu().numpy() for b in sets[last]]
+        line["cpu_baseline"] = cpu_baseline(args, host, outs[last][:s].cpu().numpy())
+    if rank == 0 and args.extra:
+        from bench_extra import run_extra
+        extra = run_extra(dev)
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        json.dump(extra, open(os.path.join(REPO, "gpurun_out", "bench_extra.json"), "w"), indent=1)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+"""bench_extra.py -- secondary per-kernel timings for DESIGN.md (not the headline line).
+
+Each row: median device time of one launch (HIP events on the launch stream,
+20 launches after 3 warm-ups) and the algorithmic HBM bytes of that launch
+(SURVEY.md 8d), so GB/s = bytes / time and frac = GB/s / 8000.
+"""
+from __future__ import annotations
+
+import statistics
+
+import torch
+
+HBM = 8000.0
+
+
+def _time(fn, reps=20, warm=3):
+    s = torch.cuda.current_stream()
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        ts.append((a, b))
+    torch.cuda.synchronize()
+    return statistics.median([a.elapsed_time(b) for a, b in ts]) / 1e3
+
+
+def _row(name, secs, nbytes, **kw):
+    gbs = nbytes / secs / 1e9
+    r = {"kernel": name, "us": round(secs * 1e6, 2), "bytes": int(nbytes),
+         "GB/s": round(gbs, 1), "frac": round(gbs / HBM, 4)}
+    r.update(kw)
+    return r
+
+
+def run_extra(dev):
+    from ina_amd import ops
+    rows = []
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+
+    def rnd_i32(n):
+        return torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=gen)
+
+    def rnd_f32(n, scale=1e-2):
+        return torch.randn(n, device=dev, generator=gen) * scale
+
+    # --- sum-reduce tuning sweep, config 3 ---------------------------------------------
+    n3, W3 = 26_214_400, 8
+    b3 = [rnd_i32(n3) for _ in range(W3)]
+    o3 = torch.empty(n3, dtype=torch.int32, device=dev)
+    sweep = []
+    for nt in (True, False):
+        for unroll in (1, 2, 4):
+            for blocks in (512, 1024, 2048, 4096, 8192, 1 << 20):
+                ops.set_tuning(max_blocks=blocks, unroll=unroll, nontemporal=nt)
+                t = _time(lambda: ops.sum_reduce(b3, out=o3))
+                sweep.append(_row("sum_reduce_i32 W=8", t, (W3 + 1) * n3 * 4, nt=nt, unroll=unroll,
+                                  max_blocks=blocks))
+    ops.set_tuning(max_blocks=2048, unroll=2, nontemporal=True)
+    rows.append(max(sweep, key=lambda r: r["GB/s"]) | {"note": "best of sweep"})
+    for W in (2, 4, 16):
+        bw = [rnd_i32(n3) for _ in range(W)] if W != 16 else b3 + [rnd_i32(n3) for _ in range(8)]
+        t = _time(lambda: ops.sum_reduce(bw, out=o3))
+        rows.append(_row(f"sum_reduce_i32 W={W}", t, (W + 1) * n3 * 4))
+        del bw
+
+    # --- quantise / dequantise ------------------------------------------------------------
+    x = rnd_f32(n3)
+    q = torch.empty(n3, dtype=torch.int32, device=dev)
+    rows.append(_row("quantize_f32_i32", _time(lambda: ops.quantize(x, 16, out=q)), 8 * n3))
+    y = torch.empty(n3, dtype=torch.float32, device=dev)
+    rows.append(_row("dequantize_i32_f32", _time(lambda: ops.dequantize(q, 16, out=y)), 8 * n3))
+
+    # --- config 2: fused quantise + reduce, 4 x ResNet-50 fp32 -----------------------------
+    n2 = 25_557_032
+    b2 = [rnd_f32(n2) for _ in range(4)]
+    o2 = torch.empty(n2, dtype=torch.int32, device=dev)
+    rows.append(_row("quantize_reduce_f32_i32 W=4 (C2)",
+                     _time(lambda: ops.quantize_reduce(b2, 16, out=o2)), (4 * 4 + 4) * n2))
+    # --- config 4: int16 saturating, 16 workers --------------------------------------------
+    b4 = b2 + [rnd_f32(n2) for _ in range(12)]
+    o4 = torch.empty(n2, dtype=torch.int16, device=dev)
+    f4 = torch.empty((n2 + 255) // 256, dtype=torch.uint8, device=dev)
+    rows.append(_row("quantize_reduce_f32_i16 W=16 V=256 (C4)",
+                     _time(lambda: ops.quantize_reduce_i16(b4, 12, 256, out=o4, overflow=f4)),
+                     (16 * 4 + 2) * n2 + f4.numel()))
+    # --- PS combine (launch.py:42-52), W=4 ---------------------------------------------------
+    local = rnd_f32(n2, 1.0)
+    oc = torch.empty_like(local)
+    rows.append(_row("ps_combine_f32 W=4", _time(lambda: ops.ps_combine(local, b2[:4], 0.2, out=oc)),
+                     (4 + 2) * 4 * n2))
+    del b4, b2, local, oc, o4
+
+    # --- packets, V = 256 over the C3 aggregate ------------------------------------------------
+    V = 256
+    stride = ops.nga_stride(V)
+    npk = (n3 + V - 1) // V
+    pk = torch.empty((npk, stride), dtype=torch.uint8, device=dev)
+    rows.append(_row("pack_nga V=256", _time(lambda: ops.pack_nga(o3, V, 1, 8, 1, 1, out=pk)),
+                     4 * n3 + npk * stride))
+    rows.append(_row("unpack_nga V=256", _time(lambda: ops.unpack_nga(pk, V)),
+                     npk * stride + 4 * n3 + npk * 15))
+    npc = 199_665   # ResNet-50 in C-128 packets (communicator.py:10)
+    g = rnd_i32(npc * 128)
+    pc = torch.empty((npc, 524), dtype=torch.uint8, device=dev)
+    rows.append(_row("pack_c128 ResNet-50", _time(lambda: ops.pack_c128(g, npc, 1, 0, 0, out=pc)),
+                     npc * (512 + 524)))
+
+    # --- packet-stream switch: 8 workers x 100 MiB as NGA-256 packets ------------------------
+    Ws = 8
+    stream = torch.cat([ops.pack_nga(b3[w], V, w + 1, Ws, 1, 1, num_slots=1 << 17) for w in range(Ws)])
+    sw = ops.Switch(V, num_slots=1 << 17, switch_id=1, device=dev)
+    acts = torch.empty(stream.shape[0], dtype=torch.uint8, device=dev)
+
+    def sw_round():
+        sw.count.zero_()
+        sw.frag.zero_()
+        sw.process(stream, acts)
+    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts)", _time(sw_round, reps=5, warm=1),
+                     2 * stream.numel() + 4 * (1 << 17) * V * 2))
+    del stream
+
+    # --- end to end: pinned host -> HBM -> reduce -> pinned host -------------------------------
+    hosts = [b.cpu().pin_memory() for b in b3]
+    hout = torch.empty(n3, dtype=torch.int32).pin_memory()
+    dbuf = [torch.empty(n3, dtype=torch.int32, device=dev) for _ in range(W3)]
+
+    def e2e():
+        for h, d in zip(hosts, dbuf):
+            d.copy_(h, non_blocking=True)
+        ops.sum_reduce(dbuf, out=o3)
+        hout.copy_(o3, non_blocking=True)
+    t = _time(e2e, reps=5, warm=1)
+    rows.append(_row("end-to-end pinned H2D(8x100MiB)+reduce+D2H", t, (W3 + 1) * n3 * 4,
+                     aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2)))
+    return {"rows": rows, "sweep": sweep}

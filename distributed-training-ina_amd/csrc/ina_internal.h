@@ -1,0 +1,20 @@
+// ina_internal.h -- shared between the libina.so translation units (not installed).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+#include "ina.h"
+
+namespace ina {
+
+// W device pointers passed by value in the kernel arguments (512 B at W_max = 64)
+template <typename T>
+struct PtrPack {
+    const T* p[INA_MAX_WORKERS];
+};
+
+int set_error(int code, const char* fmt, const char* detail);
+
+}  // namespace ina
+
+extern "C" int ina_set_tuning(int key, int value);

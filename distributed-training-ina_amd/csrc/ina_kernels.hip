@@ -1,0 +1,1000 @@
+// ina_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the INA aggregation path
+// and the extern "C" entry points declared in include/ina.h.
+//
+// Reference behaviour each kernel reproduces (Fangjin98/distributed-training-INA):
+//   k_sum_reduce_*      processor.p4:14-24 (x32, ngaa.p4:87-168): per-slot bit<32> add
+//   k_quantize_*        float_to_int (absent; DataManager.py:9,37) -- build-defined
+//   k_dequantize_*      int_to_float (absent; NGAPacket.py:5,118) -- build-defined
+//   k_ps_combine_f32    aggregate(), launch.py:42-52 / launch_async.py:42-57
+//   k_pack_nga_*        DataManager._send_data, DataManager.py:111-165 + headers.p4:27-80
+//   k_unpack_nga_*      NGAHeader/NGAPayload, NGAPacket.py:62-118 (layout of headers.p4)
+//   k_pack_c128         send_gradients packet loop, communicator.cc:23-37
+//
+// All of these are HBM-streaming kernels (no contraction -> no MFMA): 16 B per lane
+// per access (global_load_dwordx4), 256-thread workgroups, grid-stride loops over
+// a grid capped near 8 workgroups per CU, non-temporal loads/stores for data that is
+// touched exactly once.  Integer sums use uint32 arithmetic (defined wraparound).
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+
+#include "ina.h"
+#include "ina_internal.h"
+
+namespace ina {
+
+using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+using f32x4 = float __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------
+// error reporting
+// ---------------------------------------------------------------------------
+static thread_local char g_err[256] = "";
+
+int set_error(int code, const char* fmt, const char* detail) {
+    snprintf(g_err, sizeof g_err, fmt, detail ? detail : "");
+    return code;
+}
+
+static int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+        return INA_EHIP;
+    }
+    return INA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// tuning (grid cap / unroll), overridable for sweeps through ina_set_tuning()
+// ---------------------------------------------------------------------------
+static std::atomic<int> g_max_blocks{2048};   // 8 workgroups x 256 CUs
+static std::atomic<int> g_unroll{2};
+static std::atomic<int> g_nontemporal{1};
+
+static inline unsigned grid_for(size_t work_items, int per_thread) {
+    size_t per_block = (size_t)kBlock * (size_t)per_thread;
+    size_t blocks = (work_items + per_block - 1) / per_block;
+    size_t cap = (size_t)g_max_blocks.load();
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    return (unsigned)blocks;
+}
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ---------------------------------------------------------------------------
+// memory helpers
+// ---------------------------------------------------------------------------
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// ---------------------------------------------------------------------------
+// quantiser (build-defined, see include/ina.h): sat(rne(x * 2^k)), NaN -> 0
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t q32(float x, float s) {
+    float y = __builtin_rintf(x * s);
+    int32_t r = (int32_t)y;                         // in-range lanes only are selected
+    r = (y >= 2147483648.0f) ? INT32_MAX : r;
+    r = (y < -2147483648.0f) ? INT32_MIN : r;
+    return (y != y) ? 0 : r;
+}
+
+// returns the int16 value widened to int32; *sat |= clamped-or-NaN
+__device__ __forceinline__ int32_t q16(float x, float s, bool& sat) {
+    float y = __builtin_rintf(x * s);
+    bool in = (y <= 32767.0f) && (y >= -32768.0f);  // false for NaN
+    sat |= !in;
+    int32_t r = in ? (int32_t)y : 0;
+    r = (y > 32767.0f) ? 32767 : r;
+    r = (y < -32768.0f) ? -32768 : r;
+    return r;
+}
+
+__device__ __forceinline__ int32_t sat16(int32_t a, bool& sat) {
+    bool hi = a > 32767, lo = a < -32768;
+    sat |= hi | lo;
+    return hi ? 32767 : (lo ? -32768 : a);
+}
+
+// ---------------------------------------------------------------------------
+// per-slot overflow flags: thread t owns 8 consecutive values; a slot of V values
+// (V % 8 == 0, V/8 a power of two <= 64) is V/8 adjacent lanes of one wave.  The
+// group's first lane writes the slot flag from a wave ballot -- one writer per slot,
+// no atomics, no pre-zeroing.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void write_slot_flags8(unsigned long long m, bool active, size_t elem0,
+                                                  int V, int lanes_per_slot,
+                                                  uint8_t* __restrict__ ovf) {
+    int lane = threadIdx.x & 63;
+    int g0 = lane & ~(lanes_per_slot - 1);
+    unsigned long long gm = (lanes_per_slot == 64) ? ~0ull : (((1ull << lanes_per_slot) - 1ull) << g0);
+    if (active && (lane & (lanes_per_slot - 1)) == 0) ovf[elem0 / (size_t)V] = (m & gm) ? 1 : 0;
+}
+
+static inline bool slot_ballot_ok(int V) {
+    if (V % 8) return false;
+    int l = V / 8;
+    return l >= 1 && l <= 64 && (l & (l - 1)) == 0;
+}
+
+// ===========================================================================
+// 1. W-way int32 sum-reduce (the headline kernel)
+// ===========================================================================
+template <int W, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_vec(PtrPack<int32_t> in,
+                                                               int32_t* __restrict__ out,
+                                                               size_t n4, size_t n) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    size_t i = tid;
+    // full iterations: U independent 16-byte chunks per thread, all W*U loads in flight
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        u32x4 acc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc[u] = ld<NT>(reinterpret_cast<const u32x4*>(in.p[0]) + i + u * stride);
+#pragma unroll
+        for (int w = 1; w < W; ++w) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                acc[u] += ld<NT>(reinterpret_cast<const u32x4*>(in.p[w]) + i + u * stride);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            st<NT>(reinterpret_cast<u32x4*>(out) + i + u * stride, acc[u]);
+    }
+    for (; i < n4; i += stride) {
+        u32x4 acc = ld<NT>(reinterpret_cast<const u32x4*>(in.p[0]) + i);
+#pragma unroll
+        for (int w = 1; w < W; ++w) acc += ld<NT>(reinterpret_cast<const u32x4*>(in.p[w]) + i);
+        st<NT>(reinterpret_cast<u32x4*>(out) + i, acc);
+    }
+    // scalar tail (n % 4 values)
+    size_t t = 4 * n4 + tid;
+    if (t < n) {
+        uint32_t a = (uint32_t)in.p[0][t];
+#pragma unroll
+        for (int w = 1; w < W; ++w) a += (uint32_t)in.p[w][t];
+        out[t] = (int32_t)a;
+    }
+}
+
+// runtime-W vector kernel (W not in the specialised set)
+__global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_vec_dyn(PtrPack<int32_t> in, int W,
+                                                                   int32_t* __restrict__ out,
+                                                                   size_t n4, size_t n) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = tid; i < n4; i += stride) {
+        u32x4 acc = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[0]) + i);
+        int w = 1;
+        for (; w + 3 < W; w += 4) {
+            u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[w]) + i);
+            u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[w + 1]) + i);
+            u32x4 c = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[w + 2]) + i);
+            u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[w + 3]) + i);
+            acc += (a + b) + (c + d);
+        }
+        for (; w < W; ++w) acc += __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[w]) + i);
+        __builtin_nontemporal_store(acc, reinterpret_cast<u32x4*>(out) + i);
+    }
+    size_t t = 4 * n4 + tid;
+    if (t < n) {
+        uint32_t a = 0;
+        for (int w = 0; w < W; ++w) a += (uint32_t)in.p[w][t];
+        out[t] = (int32_t)a;
+    }
+}
+
+// unaligned fallback: one element per thread
+__global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_scalar(PtrPack<int32_t> in, int W,
+                                                                  int32_t* __restrict__ out,
+                                                                  size_t n) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        uint32_t a = 0;
+        for (int w = 0; w < W; ++w) a += (uint32_t)in.p[w][i];
+        out[i] = (int32_t)a;
+    }
+}
+
+template <int W, int U>
+static void launch_reduce_w(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
+                            hipStream_t s) {
+    unsigned g = grid_for(n4, U);
+    if (g_nontemporal.load())
+        hipLaunchKernelGGL((k_sum_reduce_i32_vec<W, U, true>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
+    else
+        hipLaunchKernelGGL((k_sum_reduce_i32_vec<W, U, false>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
+}
+
+template <int W>
+static void launch_reduce_u(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
+                            hipStream_t s) {
+    switch (g_unroll.load()) {
+        case 1: launch_reduce_w<W, 1>(pk, out, n4, n, s); break;
+        case 4: launch_reduce_w<W, 4>(pk, out, n4, n, s); break;
+        default: launch_reduce_w<W, 2>(pk, out, n4, n, s); break;
+    }
+}
+
+// ===========================================================================
+// 2. quantise / dequantise
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_quantize_i32(const float* __restrict__ x,
+                                                         int32_t* __restrict__ q, size_t n,
+                                                         float s, int vec) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    size_t n4 = vec ? n / 4 : 0;
+    for (size_t i = tid; i < n4; i += stride) {
+        f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x) + i);
+        u32x4 r;
+        r.x = (uint32_t)q32(v.x, s); r.y = (uint32_t)q32(v.y, s);
+        r.z = (uint32_t)q32(v.z, s); r.w = (uint32_t)q32(v.w, s);
+        __builtin_nontemporal_store(r, reinterpret_cast<u32x4*>(q) + i);
+    }
+    for (size_t i = 4 * n4 + tid; i < n; i += stride) q[i] = q32(x[i], s);
+}
+
+// int16: thread owns 8 values (two float4 loads, one 16-byte store)
+__global__ __launch_bounds__(kBlock) void k_quantize_i16_vec(const float* __restrict__ x,
+                                                             int16_t* __restrict__ q, size_t n,
+                                                             float s, int V, int lanes_per_slot,
+                                                             uint8_t* __restrict__ ovf) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const size_t n8 = (n + 7) / 8;
+    // uniform trip count per wave so every lane reaches the ballot together
+    const size_t wave0 = tid & ~(size_t)63;
+    for (size_t base = wave0; base < n8; base += stride) {
+        size_t i = base + (tid & 63);
+        bool sat = false;
+        if (i < n8) {
+            size_t e = 8 * i;
+            int32_t r[8];
+            if (e + 8 <= n) {
+                f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + e));
+                f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + e) + 1);
+                r[0] = q16(a.x, s, sat); r[1] = q16(a.y, s, sat); r[2] = q16(a.z, s, sat); r[3] = q16(a.w, s, sat);
+                r[4] = q16(b.x, s, sat); r[5] = q16(b.y, s, sat); r[6] = q16(b.z, s, sat); r[7] = q16(b.w, s, sat);
+                u32x4 o;
+                o.x = (uint32_t)(uint16_t)r[0] | ((uint32_t)r[1] << 16);
+                o.y = (uint32_t)(uint16_t)r[2] | ((uint32_t)r[3] << 16);
+                o.z = (uint32_t)(uint16_t)r[4] | ((uint32_t)r[5] << 16);
+                o.w = (uint32_t)(uint16_t)r[6] | ((uint32_t)r[7] << 16);
+                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(q + e));
+            } else {
+                for (size_t j = e; j < n; ++j) q[j] = (int16_t)q16(x[j], s, sat);
+            }
+        }
+        unsigned long long m = __ballot(sat);   // wave-convergent: uniform trip count
+        if (ovf) write_slot_flags8(m, i < n8, 8 * i, V, lanes_per_slot, ovf);
+    }
+}
+
+// generic int16 path (unaligned or V without a ballot layout): byte flags via a
+// pre-zeroed array and benign same-value stores
+__global__ __launch_bounds__(kBlock) void k_quantize_i16_scalar(const float* __restrict__ x,
+                                                                int16_t* __restrict__ q, size_t n,
+                                                                float s, int V,
+                                                                uint8_t* __restrict__ ovf) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        bool sat = false;
+        q[i] = (int16_t)q16(x[i], s, sat);
+        if (sat && ovf) ovf[i / (size_t)V] = 1;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequantize_i32(const int32_t* __restrict__ sv,
+                                                           float* __restrict__ y, size_t n,
+                                                           float inv, int vec) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    size_t n4 = vec ? n / 4 : 0;
+    for (size_t i = tid; i < n4; i += stride) {
+        u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sv) + i);
+        f32x4 r;
+        r.x = (float)(int32_t)v.x * inv; r.y = (float)(int32_t)v.y * inv;
+        r.z = (float)(int32_t)v.z * inv; r.w = (float)(int32_t)v.w * inv;
+        __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(y) + i);
+    }
+    for (size_t i = 4 * n4 + tid; i < n; i += stride) y[i] = (float)sv[i] * inv;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequantize_i16(const int16_t* __restrict__ sv,
+                                                           float* __restrict__ y, size_t n,
+                                                           float inv) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        y[i] = (float)sv[i] * inv;
+}
+
+// ===========================================================================
+// 3. fused quantise + reduce (configs 2 and 4) and the int16 narrow reduce
+// ===========================================================================
+template <int W>
+__device__ __forceinline__ u32x4 quant_sum4(const PtrPack<float>& in, int Wd, size_t i, float s) {
+    constexpr int UNR = W > 0 ? W : 1;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const int nw = W > 0 ? W : Wd;
+#pragma unroll UNR
+    for (int w = 0; w < nw; ++w) {
+        f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w]) + i);
+        acc.x += (uint32_t)q32(v.x, s); acc.y += (uint32_t)q32(v.y, s);
+        acc.z += (uint32_t)q32(v.z, s); acc.w += (uint32_t)q32(v.w, s);
+    }
+    return acc;
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_quant_reduce_i32(PtrPack<float> in, int Wd,
+                                                             int32_t* __restrict__ out,
+                                                             size_t n, float s, int vec) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const int nw = W > 0 ? W : Wd;
+    size_t n4 = vec ? n / 4 : 0;
+    for (size_t i = tid; i < n4; i += stride)
+        __builtin_nontemporal_store(quant_sum4<W>(in, Wd, i, s), reinterpret_cast<u32x4*>(out) + i);
+    for (size_t i = 4 * n4 + tid; i < n; i += stride) {
+        uint32_t a = 0;
+        for (int w = 0; w < nw; ++w) a += (uint32_t)q32(in.p[w][i], s);
+        out[i] = (int32_t)a;
+    }
+}
+
+// int16: thread owns 8 values; each worker value saturates at quantisation (wire
+// width), exact int32 sum, one final saturation; per-slot flag = any saturation.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_quant_reduce_i16(PtrPack<float> in, int Wd,
+                                                             int16_t* __restrict__ out, size_t n,
+                                                             float s, int V, int lanes_per_slot,
+                                                             uint8_t* __restrict__ ovf) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const int nw = W > 0 ? W : Wd;
+    constexpr int UNR = W > 0 ? W : 1;
+    const size_t n8 = (n + 7) / 8;
+    const size_t wave0 = tid & ~(size_t)63;
+    for (size_t base = wave0; base < n8; base += stride) {
+        size_t i = base + (tid & 63);
+        bool sat = false;
+        if (i < n8) {
+            size_t e = 8 * i;
+            if (e + 8 <= n) {
+                int32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll UNR
+                for (int w = 0; w < nw; ++w) {
+                    f32x4 u = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w] + e));
+                    f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w] + e) + 1);
+                    a[0] += q16(u.x, s, sat); a[1] += q16(u.y, s, sat);
+                    a[2] += q16(u.z, s, sat); a[3] += q16(u.w, s, sat);
+                    a[4] += q16(v.x, s, sat); a[5] += q16(v.y, s, sat);
+                    a[6] += q16(v.z, s, sat); a[7] += q16(v.w, s, sat);
+                }
+                u32x4 o;
+                o.x = (uint32_t)(uint16_t)sat16(a[0], sat) | ((uint32_t)sat16(a[1], sat) << 16);
+                o.y = (uint32_t)(uint16_t)sat16(a[2], sat) | ((uint32_t)sat16(a[3], sat) << 16);
+                o.z = (uint32_t)(uint16_t)sat16(a[4], sat) | ((uint32_t)sat16(a[5], sat) << 16);
+                o.w = (uint32_t)(uint16_t)sat16(a[6], sat) | ((uint32_t)sat16(a[7], sat) << 16);
+                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + e));
+            } else {
+                for (size_t j = e; j < n; ++j) {
+                    int32_t a = 0;
+                    for (int w = 0; w < nw; ++w) a += q16(in.p[w][j], s, sat);
+                    out[j] = (int16_t)sat16(a, sat);
+                }
+            }
+        }
+        unsigned long long m = __ballot(sat);   // wave-convergent: uniform trip count
+        if (ovf) write_slot_flags8(m, i < n8, 8 * i, V, lanes_per_slot, ovf);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_quant_reduce_i16_scalar(PtrPack<float> in, int W,
+                                                                    int16_t* __restrict__ out,
+                                                                    size_t n, float s, int V,
+                                                                    uint8_t* __restrict__ ovf) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        bool sat = false;
+        int32_t a = 0;
+        for (int w = 0; w < W; ++w) a += q16(in.p[w][i], s, sat);
+        out[i] = (int16_t)sat16(a, sat);
+        if (sat && ovf) ovf[i / (size_t)V] = 1;
+    }
+}
+
+// int16 narrow reduce of already-quantised int16 buffers
+__global__ __launch_bounds__(kBlock) void k_sum_reduce_i16(PtrPack<int16_t> in, int W,
+                                                           int16_t* __restrict__ out, size_t n,
+                                                           int V, int lanes_per_slot,
+                                                           uint8_t* __restrict__ ovf) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const size_t n8 = (n + 7) / 8;
+    const size_t wave0 = tid & ~(size_t)63;
+    for (size_t base = wave0; base < n8; base += stride) {
+        size_t i = base + (tid & 63);
+        bool sat = false;
+        if (i < n8) {
+            size_t e = 8 * i;
+            if (e + 8 <= n) {
+                int32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                for (int w = 0; w < W; ++w) {
+                    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[w] + e));
+                    a[0] += (int16_t)(v.x & 0xFFFF); a[1] += (int16_t)(v.x >> 16);
+                    a[2] += (int16_t)(v.y & 0xFFFF); a[3] += (int16_t)(v.y >> 16);
+                    a[4] += (int16_t)(v.z & 0xFFFF); a[5] += (int16_t)(v.z >> 16);
+                    a[6] += (int16_t)(v.w & 0xFFFF); a[7] += (int16_t)(v.w >> 16);
+                }
+                u32x4 o;
+                o.x = (uint32_t)(uint16_t)sat16(a[0], sat) | ((uint32_t)sat16(a[1], sat) << 16);
+                o.y = (uint32_t)(uint16_t)sat16(a[2], sat) | ((uint32_t)sat16(a[3], sat) << 16);
+                o.z = (uint32_t)(uint16_t)sat16(a[4], sat) | ((uint32_t)sat16(a[5], sat) << 16);
+                o.w = (uint32_t)(uint16_t)sat16(a[6], sat) | ((uint32_t)sat16(a[7], sat) << 16);
+                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + e));
+            } else {
+                for (size_t j = e; j < n; ++j) {
+                    int32_t a = 0;
+                    for (int w = 0; w < W; ++w) a += in.p[w][j];
+                    out[j] = (int16_t)sat16(a, sat);
+                }
+            }
+        }
+        unsigned long long m = __ballot(sat);   // wave-convergent: uniform trip count
+        if (ovf) write_slot_flags8(m, i < n8, 8 * i, V, lanes_per_slot, ovf);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sum_reduce_i16_scalar(PtrPack<int16_t> in, int W,
+                                                                  int16_t* __restrict__ out,
+                                                                  size_t n, int V,
+                                                                  uint8_t* __restrict__ ovf) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        bool sat = false;
+        int32_t a = 0;
+        for (int w = 0; w < W; ++w) a += in.p[w][i];
+        out[i] = (int16_t)sat16(a, sat);
+        if (sat && ovf) ovf[i / (size_t)V] = 1;
+    }
+}
+
+// ===========================================================================
+// 4. PS combine (launch.py:42-52), bit-exact fp32 op sequence; built with
+//    -ffp-contract=off so no FMA fuses the sub/add/mul.
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_ps_combine_f32(const float* __restrict__ local,
+                                                           PtrPack<float> paras, int W, float ws,
+                                                           float* __restrict__ out, size_t n) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        float l = local[i];
+        float acc = 0.0f;                      // python sum() starts at int 0
+        for (int w = 0; w < W; ++w) acc = __fadd_rn(acc, __fsub_rn(paras.p[w][i], l));
+        out[i] = __fadd_rn(l, __fmul_rn(acc, ws));
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ps_apply_i32(const float* __restrict__ local,
+                                                         const int32_t* __restrict__ sum,
+                                                         float inv, float ws,
+                                                         float* __restrict__ out, size_t n) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        float d = __fmul_rn((float)sum[i], inv);
+        out[i] = __fadd_rn(local[i], __fmul_rn(d, ws));
+    }
+}
+
+// ===========================================================================
+// 5. NGA-V packets (15-byte BE header, V BE words, zero tail)
+// ===========================================================================
+struct NgaHdr {
+    uint32_t bitmap, seq0, num_slots;
+    uint32_t flags_count_sw;   // count | flags << 8 | switch_id << 16
+    int V;
+};
+
+__device__ __forceinline__ uint32_t nga_val(const int32_t* __restrict__ vals, size_t n, size_t p,
+                                            int V, long j) {
+    // payload word j of packet p (0 outside [0, V) and past n: zero tail pad)
+    if (j < 0 || j >= V) return 0u;
+    size_t e = p * (size_t)V + (size_t)j;
+    return e < n ? (uint32_t)vals[e] : 0u;
+}
+
+// vector path: stride % 16 == 0, V % 4 == 0, 16-byte aligned buffers.
+// Thread per 16-byte chunk of the packet buffer.
+__global__ __launch_bounds__(kBlock) void k_pack_nga_vec(const int32_t* __restrict__ vals, size_t n,
+                                                         NgaHdr h, const uint8_t* __restrict__ ovf,
+                                                         uint8_t* __restrict__ pkts,
+                                                         uint32_t chunks_per_pkt, size_t nchunks) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const int V = h.V;
+    for (size_t g = (size_t)blockIdx.x * kBlock + threadIdx.x; g < nchunks; g += stride) {
+        size_t p = g / chunks_per_pkt;
+        uint32_t c = (uint32_t)(g - p * chunks_per_pkt);
+        u32x4 o;
+        if (c == 0) {
+            uint32_t seq = h.seq0 + (uint32_t)p;
+            uint32_t idx = seq % h.num_slots;
+            uint32_t flags = (h.flags_count_sw >> 8) & 0xFFu;
+            if (ovf && ovf[p]) flags |= INA_FLAG_OVERFLOW;
+            uint32_t count = h.flags_count_sw & 0xFFu, sw = (h.flags_count_sw >> 16) & 0xFFu;
+            uint32_t bi = bswap(idx), bf = bswap(seq);
+            o.x = bswap(h.bitmap);
+            o.y = count | (flags << 8) | (bi << 16);
+            o.z = (bi >> 16) | (sw << 16) | (bf << 24);
+            o.w = (bf >> 8) | (bswap(nga_val(vals, n, p, V, 0)) << 24);
+        } else {
+            long j0 = 4 * (long)c - 4;   // out word m=4c+t takes payload words m-4, m-3
+            uint32_t v[5];
+            size_t e0 = p * (size_t)V + (size_t)j0;
+            if (j0 + 4 < V && e0 + 5 <= n) {
+                u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + e0));
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+                v[4] = (uint32_t)vals[e0 + 4];
+            } else {
+#pragma unroll
+                for (int t = 0; t < 5; ++t) v[t] = nga_val(vals, n, p, V, j0 + t);
+            }
+            o.x = (bswap(v[0]) >> 8) | (v[1] & 0xFF000000u);
+            o.y = (bswap(v[1]) >> 8) | (v[2] & 0xFF000000u);
+            o.z = (bswap(v[2]) >> 8) | (v[3] & 0xFF000000u);
+            o.w = (bswap(v[3]) >> 8) | (v[4] & 0xFF000000u);
+        }
+        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(pkts) + g);
+    }
+}
+
+// generic path: any stride / alignment, thread per output byte
+__global__ __launch_bounds__(kBlock) void k_pack_nga_bytes(const int32_t* __restrict__ vals, size_t n,
+                                                           NgaHdr h, const uint8_t* __restrict__ ovf,
+                                                           uint8_t* __restrict__ pkts, size_t pstride,
+                                                           size_t nbytes) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const int V = h.V;
+    for (size_t g = (size_t)blockIdx.x * kBlock + threadIdx.x; g < nbytes; g += gs) {
+        size_t p = g / pstride;
+        size_t b = g - p * pstride;
+        uint32_t seq = h.seq0 + (uint32_t)p;
+        uint8_t out = 0;
+        if (b < 4) out = (uint8_t)(h.bitmap >> (24 - 8 * b));
+        else if (b == 4) out = (uint8_t)(h.flags_count_sw & 0xFF);
+        else if (b == 5) out = (uint8_t)(((h.flags_count_sw >> 8) & 0xFF) | ((ovf && ovf[p]) ? INA_FLAG_OVERFLOW : 0));
+        else if (b < 10) out = (uint8_t)((seq % h.num_slots) >> (24 - 8 * (b - 6)));
+        else if (b == 10) out = (uint8_t)((h.flags_count_sw >> 16) & 0xFF);
+        else if (b < 15) out = (uint8_t)(seq >> (24 - 8 * (b - 11)));
+        else if (b < 15 + 4 * (size_t)V) {
+            size_t q = b - 15;
+            out = (uint8_t)(nga_val(vals, n, p, V, (long)(q / 4)) >> (24 - 8 * (q % 4)));
+        }
+        pkts[g] = out;
+    }
+}
+
+struct NgaFieldsDev {
+    uint32_t* bitmap; uint8_t* count; uint8_t* flags; uint32_t* index; uint8_t* switch_id; uint32_t* frag_id;
+};
+
+__device__ __forceinline__ void nga_store_header(const NgaFieldsDev& f, size_t p, uint32_t w0,
+                                                 uint32_t w1, uint32_t w2, uint32_t w3) {
+    if (f.bitmap) f.bitmap[p] = bswap(w0);
+    if (f.count) f.count[p] = (uint8_t)(w1 & 0xFF);
+    if (f.flags) f.flags[p] = (uint8_t)((w1 >> 8) & 0xFF);
+    if (f.index) f.index[p] = bswap((w1 >> 16) | (w2 << 16));
+    if (f.switch_id) f.switch_id[p] = (uint8_t)((w2 >> 16) & 0xFF);
+    if (f.frag_id) f.frag_id[p] = bswap((w2 >> 24) | (w3 << 8));
+}
+
+// vector unpack: thread per (packet, 4 values); reads two aligned 16-byte chunks
+__global__ __launch_bounds__(kBlock) void k_unpack_nga_vec(const uint8_t* __restrict__ pkts,
+                                                           size_t npk, int V, size_t pstride,
+                                                           NgaFieldsDev f, int32_t* __restrict__ vals) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const uint32_t groups = (uint32_t)(V / 4);
+    const size_t total = npk * groups;
+    for (size_t g = (size_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += gs) {
+        size_t p = g / groups;
+        uint32_t j4 = (uint32_t)(g - p * groups);
+        const u32x4* src = reinterpret_cast<const u32x4*>(pkts + p * pstride + 16 * (size_t)j4);
+        u32x4 a = __builtin_nontemporal_load(src);
+        u32x4 b = __builtin_nontemporal_load(src + 1);
+        if (j4 == 0) nga_store_header(f, p, a.x, a.y, a.z, a.w);
+        if (vals) {
+            // value t starts at byte 15+4t of the 32 loaded bytes: words (3+t, 4+t)
+            u32x4 o;
+            o.x = bswap(__builtin_amdgcn_alignbyte(b.x, a.w, 3));
+            o.y = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
+            o.z = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
+            o.w = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
+            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(vals + p * (size_t)V) + j4);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t be32_at(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_nga_scalar(const uint8_t* __restrict__ pkts,
+                                                              size_t npk, int V, size_t pstride,
+                                                              NgaFieldsDev f, int32_t* __restrict__ vals) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const size_t per = (size_t)V + 1;   // slot 0: header, 1..V: values
+    for (size_t g = (size_t)blockIdx.x * kBlock + threadIdx.x; g < npk * per; g += gs) {
+        size_t p = g / per, j = g - p * per;
+        const uint8_t* pk = pkts + p * pstride;
+        if (j == 0) {
+            if (f.bitmap) f.bitmap[p] = be32_at(pk);
+            if (f.count) f.count[p] = pk[4];
+            if (f.flags) f.flags[p] = pk[5];
+            if (f.index) f.index[p] = be32_at(pk + 6);
+            if (f.switch_id) f.switch_id[p] = pk[10];
+            if (f.frag_id) f.frag_id[p] = be32_at(pk + 11);
+        } else if (vals) {
+            vals[p * (size_t)V + j - 1] = (int32_t)be32_at(pk + 15 + 4 * (j - 1));
+        }
+    }
+}
+
+// ===========================================================================
+// 6. C-128 packets: 131 BE words per packet (communicator.cc:23-37)
+// ===========================================================================
+__global__ __launch_bounds__(kBlock) void k_pack_c128(const uint32_t* __restrict__ g, size_t npk,
+                                                      uint32_t bitmap, uint32_t agg, int tensor_index,
+                                                      uint32_t* __restrict__ out) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const size_t total = npk * 131;
+    for (size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += gs) {
+        size_t p = t / 131;
+        uint32_t w = (uint32_t)(t - p * 131);
+        uint32_t v;
+        if (w == 0) v = bitmap;
+        else if (w == 1) v = agg;
+        else if (w == 2) v = (uint32_t)(tensor_index + (int)p);
+        else v = g[p * 128 + (w - 3)];
+        out[t] = bswap(v);
+    }
+}
+
+// ===========================================================================
+// 7. checksum: sum_i x[i]*(2i+1) mod 2^32 -- wave shuffle + LDS block reduce
+// ===========================================================================
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_checksum_i32(const int32_t* __restrict__ x, size_t n,
+                                                         int vec, uint32_t* __restrict__ out) {
+    __shared__ uint32_t part[kBlock / 64];
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    uint32_t acc = 0;
+    size_t n4 = vec ? n / 4 : 0;
+    for (size_t i = tid; i < n4; i += stride) {
+        u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(x) + i);
+        uint32_t c = (uint32_t)(8 * i + 1);
+        acc += v.x * c + v.y * (c + 2) + v.z * (c + 4) + v.w * (c + 6);
+    }
+    for (size_t i = 4 * n4 + tid; i < n; i += stride) acc += (uint32_t)x[i] * (uint32_t)(2 * i + 1);
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (int w = 0; w < kBlock / 64; ++w) s += part[w];
+        atomicAdd(out, s);
+    }
+}
+
+}  // namespace ina
+
+// ===========================================================================
+// extern "C" entry points
+// ===========================================================================
+using namespace ina;
+
+static inline hipStream_t hs(ina_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static int check_k(int k) {
+    if (k < -126 || k > 127) return set_error(INA_EINVAL, "k out of range [-126,127]%s", "");
+    return INA_OK;
+}
+
+template <typename T>
+static int fill_pack(PtrPack<T>& pk, const T* const* bufs, int W, bool& all_aligned) {
+    if (!bufs || W < 1 || W > INA_MAX_WORKERS)
+        return set_error(INA_EINVAL, "W must be in [1, %s]", "64");
+    all_aligned = true;
+    for (int w = 0; w < W; ++w) {
+        if (!bufs[w]) return set_error(INA_EINVAL, "null worker buffer%s", "");
+        pk.p[w] = bufs[w];
+        all_aligned &= aligned16(bufs[w]);
+    }
+    for (int w = W; w < INA_MAX_WORKERS; ++w) pk.p[w] = nullptr;
+    return INA_OK;
+}
+
+extern "C" {
+
+const char* ina_version(void) { return "ina-mi355x 0.1 (gfx950)"; }
+const char* ina_last_error_string(void) { return g_err; }
+
+int ina_set_tuning(int key, int value) {
+    switch (key) {
+        case 0: if (value < 1) return INA_EINVAL; g_max_blocks = value; return INA_OK;
+        case 1: if (value != 1 && value != 2 && value != 4) return INA_EINVAL; g_unroll = value; return INA_OK;
+        case 2: g_nontemporal = value ? 1 : 0; return INA_OK;
+        default: return INA_EINVAL;
+    }
+}
+
+int ina_sum_reduce_i32(const int32_t* const* bufs, int W, int32_t* out, size_t n,
+                       ina_stream_t stream) {
+    if (n == 0) return INA_OK;
+    PtrPack<int32_t> pk;
+    bool al;
+    if (int rc = fill_pack(pk, bufs, W, al)) return rc;
+    if (!out) return set_error(INA_EINVAL, "null out%s", "");
+    hipStream_t s = hs(stream);
+    if (!(al && aligned16(out))) {
+        hipLaunchKernelGGL(k_sum_reduce_i32_scalar, dim3(grid_for(n, 1)), dim3(kBlock), 0, s, pk, W, out, n);
+        return check_launch("sum_reduce_i32 scalar");
+    }
+    size_t n4 = n / 4;
+    switch (W) {
+        case 1: launch_reduce_u<1>(pk, out, n4, n, s); break;
+        case 2: launch_reduce_u<2>(pk, out, n4, n, s); break;
+        case 3: launch_reduce_u<3>(pk, out, n4, n, s); break;
+        case 4: launch_reduce_u<4>(pk, out, n4, n, s); break;
+        case 8: launch_reduce_u<8>(pk, out, n4, n, s); break;
+        case 16: launch_reduce_u<16>(pk, out, n4, n, s); break;
+        default:
+            hipLaunchKernelGGL(k_sum_reduce_i32_vec_dyn, dim3(grid_for(n4, 1)), dim3(kBlock), 0, s,
+                               pk, W, out, n4, n);
+    }
+    return check_launch("sum_reduce_i32");
+}
+
+int ina_quantize_f32_i32(const float* x, int32_t* q, size_t n, int k, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n == 0) return INA_OK;
+    if (!x || !q) return set_error(INA_EINVAL, "null pointer%s", "");
+    int vec = aligned16(x) && aligned16(q);
+    hipLaunchKernelGGL(k_quantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 1)), dim3(kBlock), 0,
+                       hs(stream), x, q, n, ldexpf(1.0f, k), vec);
+    return check_launch("quantize_i32");
+}
+
+int ina_quantize_f32_i16_sat(const float* x, int16_t* q, size_t n, int k, int V,
+                             uint8_t* ovf, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (V <= 0) return set_error(INA_EINVAL, "V must be > 0%s", "");
+    if (n == 0) return INA_OK;
+    if (!x || !q) return set_error(INA_EINVAL, "null pointer%s", "");
+    hipStream_t s = hs(stream);
+    float sc = ldexpf(1.0f, k);
+    if (aligned16(x) && aligned16(q) && (!ovf || slot_ballot_ok(V))) {
+        int lps = slot_ballot_ok(V) ? V / 8 : 1;
+        hipLaunchKernelGGL(k_quantize_i16_vec, dim3(grid_for((n + 7) / 8, 1)), dim3(kBlock), 0, s,
+                           x, q, n, sc, V, lps, ovf);
+    } else {
+        if (ovf && hipMemsetAsync(ovf, 0, (n + V - 1) / V, s) != hipSuccess)
+            return set_error(INA_EHIP, "memset overflow flags%s", "");
+        hipLaunchKernelGGL(k_quantize_i16_scalar, dim3(grid_for(n, 1)), dim3(kBlock), 0, s, x, q, n,
+                           sc, V, ovf);
+    }
+    return check_launch("quantize_i16");
+}
+
+int ina_dequantize_i32_f32(const int32_t* sv, float* y, size_t n, int k, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n == 0) return INA_OK;
+    if (!sv || !y) return set_error(INA_EINVAL, "null pointer%s", "");
+    int vec = aligned16(sv) && aligned16(y);
+    hipLaunchKernelGGL(k_dequantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 1)), dim3(kBlock), 0,
+                       hs(stream), sv, y, n, ldexpf(1.0f, -k), vec);
+    return check_launch("dequantize_i32");
+}
+
+int ina_dequantize_i16_f32(const int16_t* sv, float* y, size_t n, int k, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n == 0) return INA_OK;
+    if (!sv || !y) return set_error(INA_EINVAL, "null pointer%s", "");
+    hipLaunchKernelGGL(k_dequantize_i16, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), sv, y, n,
+                       ldexpf(1.0f, -k));
+    return check_launch("dequantize_i16");
+}
+
+int ina_sum_reduce_i16_sat(const int16_t* const* bufs, int W, int16_t* out, size_t n, int V,
+                           uint8_t* ovf, ina_stream_t stream) {
+    if (V <= 0) return set_error(INA_EINVAL, "V must be > 0%s", "");
+    if (n == 0) return INA_OK;
+    PtrPack<int16_t> pk;
+    bool al;
+    if (int rc = fill_pack(pk, bufs, W, al)) return rc;
+    if (!out) return set_error(INA_EINVAL, "null out%s", "");
+    hipStream_t s = hs(stream);
+    if (al && aligned16(out) && (!ovf || slot_ballot_ok(V))) {
+        int lps = slot_ballot_ok(V) ? V / 8 : 1;
+        hipLaunchKernelGGL(k_sum_reduce_i16, dim3(grid_for((n + 7) / 8, 1)), dim3(kBlock), 0, s, pk, W,
+                           out, n, V, lps, ovf);
+    } else {
+        if (ovf && hipMemsetAsync(ovf, 0, (n + V - 1) / V, s) != hipSuccess)
+            return set_error(INA_EHIP, "memset overflow flags%s", "");
+        hipLaunchKernelGGL(k_sum_reduce_i16_scalar, dim3(grid_for(n, 1)), dim3(kBlock), 0, s, pk, W,
+                           out, n, V, ovf);
+    }
+    return check_launch("sum_reduce_i16");
+}
+
+int ina_quantize_reduce_f32_i32(const float* const* bufs, int W, int32_t* out, size_t n, int k,
+                                ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n == 0) return INA_OK;
+    PtrPack<float> pk;
+    bool al;
+    if (int rc = fill_pack(pk, bufs, W, al)) return rc;
+    if (!out) return set_error(INA_EINVAL, "null out%s", "");
+    int vec = al && aligned16(out);
+    float sc = ldexpf(1.0f, k);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, 1);
+    hipStream_t s = hs(stream);
+    switch (W) {
+        case 2: hipLaunchKernelGGL(k_quant_reduce_i32<2>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec); break;
+        case 4: hipLaunchKernelGGL(k_quant_reduce_i32<4>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec); break;
+        case 8: hipLaunchKernelGGL(k_quant_reduce_i32<8>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec); break;
+        case 16: hipLaunchKernelGGL(k_quant_reduce_i32<16>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec); break;
+        default: hipLaunchKernelGGL(k_quant_reduce_i32<0>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec);
+    }
+    return check_launch("quantize_reduce_i32");
+}
+
+int ina_quantize_reduce_f32_i16_sat(const float* const* bufs, int W, int16_t* out, size_t n, int k,
+                                    int V, uint8_t* ovf, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (V <= 0) return set_error(INA_EINVAL, "V must be > 0%s", "");
+    if (n == 0) return INA_OK;
+    PtrPack<float> pk;
+    bool al;
+    if (int rc = fill_pack(pk, bufs, W, al)) return rc;
+    if (!out) return set_error(INA_EINVAL, "null out%s", "");
+    hipStream_t s = hs(stream);
+    float sc = ldexpf(1.0f, k);
+    if (al && aligned16(out) && (!ovf || slot_ballot_ok(V))) {
+        int lps = slot_ballot_ok(V) ? V / 8 : 1;
+        unsigned g = grid_for((n + 7) / 8, 1);
+        switch (W) {
+            case 4: hipLaunchKernelGGL(k_quant_reduce_i16<4>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, V, lps, ovf); break;
+            case 8: hipLaunchKernelGGL(k_quant_reduce_i16<8>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, V, lps, ovf); break;
+            case 16: hipLaunchKernelGGL(k_quant_reduce_i16<16>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, V, lps, ovf); break;
+            default: hipLaunchKernelGGL(k_quant_reduce_i16<0>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, V, lps, ovf);
+        }
+    } else {
+        if (ovf && hipMemsetAsync(ovf, 0, (n + V - 1) / V, s) != hipSuccess)
+            return set_error(INA_EHIP, "memset overflow flags%s", "");
+        hipLaunchKernelGGL(k_quant_reduce_i16_scalar, dim3(grid_for(n, 1)), dim3(kBlock), 0, s, pk, W,
+                           out, n, sc, V, ovf);
+    }
+    return check_launch("quantize_reduce_i16");
+}
+
+int ina_ps_combine_f32(const float* local, const float* const* paras, int W, double weight_step,
+                       float* out, size_t n, ina_stream_t stream) {
+    if (n == 0) return INA_OK;
+    PtrPack<float> pk;
+    bool al;
+    if (int rc = fill_pack(pk, paras, W, al)) return rc;
+    if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
+    hipLaunchKernelGGL(k_ps_combine_f32, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), local, pk,
+                       W, (float)weight_step, out, n);
+    return check_launch("ps_combine_f32");
+}
+
+int ina_ps_apply_i32(const float* local, const int32_t* sum_int, int k, double weight_step,
+                     float* out, size_t n, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n == 0) return INA_OK;
+    if (!local || !sum_int || !out) return set_error(INA_EINVAL, "null pointer%s", "");
+    hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), local,
+                       sum_int, ldexpf(1.0f, -k), (float)weight_step, out, n);
+    return check_launch("ps_apply_i32");
+}
+
+int ina_pack_nga(const int32_t* vals, size_t n, const ina_nga_params_t* prm, const uint8_t* ovf,
+                 uint8_t* pkts, size_t pstride, ina_stream_t stream) {
+    if (!prm || prm->V <= 0 || prm->num_slots == 0)
+        return set_error(INA_EINVAL, "bad nga params%s", "");
+    const int V = prm->V;
+    if (pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V)
+        return set_error(INA_EINVAL, "stride < 15 + 4V%s", "");
+    size_t npk = (n + (size_t)V - 1) / (size_t)V;
+    if (npk == 0) return INA_OK;
+    if (!vals || !pkts) return set_error(INA_EINVAL, "null pointer%s", "");
+    NgaHdr h{prm->bitmap, prm->seq0, prm->num_slots,
+             (uint32_t)prm->count | ((uint32_t)prm->flags << 8) | ((uint32_t)prm->switch_id << 16), V};
+    hipStream_t s = hs(stream);
+    if (pstride % 16 == 0 && V % 4 == 0 && aligned16(vals) && aligned16(pkts)) {
+        uint32_t cpp = (uint32_t)(pstride / 16);
+        size_t nchunks = npk * cpp;
+        hipLaunchKernelGGL(k_pack_nga_vec, dim3(grid_for(nchunks, 1)), dim3(kBlock), 0, s, vals, n, h,
+                           ovf, pkts, cpp, nchunks);
+    } else {
+        size_t nbytes = npk * pstride;
+        hipLaunchKernelGGL(k_pack_nga_bytes, dim3(grid_for(nbytes, 1)), dim3(kBlock), 0, s, vals, n, h,
+                           ovf, pkts, pstride, nbytes);
+    }
+    return check_launch("pack_nga");
+}
+
+int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
+                   const ina_nga_fields_t* fields, int32_t* vals, ina_stream_t stream) {
+    if (V <= 0 || pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V)
+        return set_error(INA_EINVAL, "bad V/stride%s", "");
+    if (npk == 0) return INA_OK;
+    if (!pkts) return set_error(INA_EINVAL, "null packets%s", "");
+    NgaFieldsDev f{};
+    if (fields) f = NgaFieldsDev{fields->bitmap, fields->count, fields->flags, fields->index,
+                                 fields->switch_id, fields->frag_id};
+    hipStream_t s = hs(stream);
+    if (pstride % 16 == 0 && V % 4 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
+        hipLaunchKernelGGL(k_unpack_nga_vec, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
+                           s, pkts, npk, V, pstride, f, vals);
+    } else {
+        hipLaunchKernelGGL(k_unpack_nga_scalar, dim3(grid_for(npk * ((size_t)V + 1), 1)), dim3(kBlock),
+                           0, s, pkts, npk, V, pstride, f, vals);
+    }
+    return check_launch("unpack_nga");
+}
+
+int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id, uint32_t aggregator_index,
+                  int tensor_index, uint8_t* pkts, ina_stream_t stream) {
+    if (packet_num < 0) return set_error(INA_EINVAL, "packet_num < 0%s", "");
+    if (packet_num == 0) return INA_OK;
+    if (!gradient || !pkts) return set_error(INA_EINVAL, "null pointer%s", "");
+    if ((uintptr_t)pkts & 3u) return set_error(INA_EINVAL, "packets must be 4-byte aligned%s", "");
+    // 1 << (worker_id-1): x86 masks the shift count (communicator.cc:18, UB for 0)
+    uint32_t bitmap = 1u << ((unsigned)(worker_id - 1) & 31u);
+    size_t total = (size_t)packet_num * 131;
+    hipLaunchKernelGGL(k_pack_c128, dim3(grid_for(total, 1)), dim3(kBlock), 0, hs(stream), gradient,
+                       (size_t)packet_num, bitmap, aggregator_index, tensor_index,
+                       reinterpret_cast<uint32_t*>(pkts));
+    return check_launch("pack_c128");
+}
+
+int ina_checksum_i32(const int32_t* x, size_t n, uint32_t* out_dev, ina_stream_t stream) {
+    if (!out_dev) return set_error(INA_EINVAL, "null out%s", "");
+    hipStream_t s = hs(stream);
+    if (hipMemsetAsync(out_dev, 0, sizeof(uint32_t), s) != hipSuccess)
+        return set_error(INA_EHIP, "memset checksum%s", "");
+    if (n == 0) return INA_OK;
+    if (!x) return set_error(INA_EINVAL, "null pointer%s", "");
+    int vec = aligned16(x);
+    hipLaunchKernelGGL(k_checksum_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 1)), dim3(kBlock), 0, s, x, n,
+                       vec, out_dev);
+    return check_launch("checksum_i32");
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+"""ctypes binding of libina.so (the C ABI in include/ina.h).
+
+The library is built in-tree by distributed-training-ina_amd/csrc/Makefile (or
+__graft_entry__.build()).  There is no fallback: if libina.so is missing or does
+not load, every op raises -- the device path is the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libina.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+INA_OK, INA_EINVAL, INA_EHIP, INA_ESOCK, INA_ENOMEM = 0, -1, -2, -3, -4
+MAX_WORKERS = 64
+NGA_HDR_BYTES = 15
+NUM_REGISTER = 16384
+C128_VALUES = 128
+C128_BYTES = 524
+FLAG_OVERFLOW, FLAG_ACK, FLAG_COLLISION, FLAG_RESEND = 0x80, 0x40, 0x20, 0x10
+ACT_DROP, ACT_FWD_AGG, ACT_FWD_COLLISION, ACT_FWD_ACK, ACT_FWD_OTHER = range(5)
+
+
+class InaError(RuntimeError):
+    pass
+
+
+class NgaParams(C.Structure):
+    _fields_ = [("bitmap", C.c_uint32), ("count", C.c_uint8), ("flags", C.c_uint8),
+                ("switch_id", C.c_uint8), ("pad", C.c_uint8), ("seq0", C.c_uint32),
+                ("num_slots", C.c_uint32), ("V", C.c_int32)]
+
+
+class NgaFields(C.Structure):
+    _fields_ = [("bitmap", C.c_void_p), ("count", C.c_void_p), ("flags", C.c_void_p),
+                ("index", C.c_void_p), ("switch_id", C.c_void_p), ("frag_id", C.c_void_p)]
+
+
+class SwitchState(C.Structure):
+    _fields_ = [("num_slots", C.c_uint32), ("V", C.c_int32), ("switch_id", C.c_int32),
+                ("count", C.c_void_p), ("frag", C.c_void_p), ("regs", C.c_void_p)]
+
+
+# exported symbol -> argtypes (restype int unless listed in _RESTYPE)
+_vp, _sz, _i, _u32, _d = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_double
+SIGNATURES = {
+    "ina_version": [],
+    "ina_last_error_string": [],
+    "ina_set_tuning": [_i, _i],
+    "ina_quantize_f32_i32": [_vp, _vp, _sz, _i, _vp],
+    "ina_quantize_f32_i16_sat": [_vp, _vp, _sz, _i, _i, _vp, _vp],
+    "ina_dequantize_i32_f32": [_vp, _vp, _sz, _i, _vp],
+    "ina_dequantize_i16_f32": [_vp, _vp, _sz, _i, _vp],
+    "ina_sum_reduce_i32": [_vp, _i, _vp, _sz, _vp],
+    "ina_sum_reduce_i16_sat": [_vp, _i, _vp, _sz, _i, _vp, _vp],
+    "ina_quantize_reduce_f32_i32": [_vp, _i, _vp, _sz, _i, _vp],
+    "ina_quantize_reduce_f32_i16_sat": [_vp, _i, _vp, _sz, _i, _i, _vp, _vp],
+    "ina_ps_combine_f32": [_vp, _vp, _i, _d, _vp, _sz, _vp],
+    "ina_ps_apply_i32": [_vp, _vp, _i, _d, _vp, _sz, _vp],
+    "ina_pack_nga": [_vp, _sz, C.POINTER(NgaParams), _vp, _vp, _sz, _vp],
+    "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
+    "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
+    "ina_switch_scratch_bytes": [_sz, _u32],
+    "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
+    "ina_checksum_i32": [_vp, _sz, _vp, _vp],
+    "send_gradients": [C.POINTER(C.c_uint32), _i, _u32, _i, _u32, _i],
+    "ina_send_gradients_fd": [_i, _vp, _i, _u32, _i, _u32, _i],
+}
+_RESTYPE = {"ina_version": C.c_char_p, "ina_last_error_string": C.c_char_p,
+            "ina_switch_scratch_bytes": C.c_size_t, "send_gradients": None}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> C.CDLL:
+    """Load libina.so (raises InaError if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise InaError(f"libina.so not built at {LIB_PATH}; run "
+                               f"`make -C {CSRC}` or __graft_entry__.build()")
+            lib = C.CDLL(LIB_PATH)
+            for name, args in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPE.get(name, C.c_int)
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = "ina call") -> int:
+    if rc < 0:
+        msg = load().ina_last_error_string().decode(errors="replace")
+        raise InaError(f"{what} failed (rc={rc}): {msg}")
+    return rc
+
+
+def ptr_array(ptrs):
+    return (C.c_void_p * len(ptrs))(*ptrs)

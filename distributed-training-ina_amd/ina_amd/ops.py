@@ -1,0 +1,281 @@
+"""torch-facing wrappers over libina.so's device entry points.
+
+Tensors must be CUDA (HIP) tensors on one device, contiguous, of the stated
+dtype.  Every call is asynchronous on torch's current stream of that device.
+These are the kernels that replace the reference's CPU / switch arithmetic:
+
+  quantize / dequantize      float_to_int / int_to_float (absent; DataManager.py:9,
+                             NGAPacket.py:5) -- build-defined, see DESIGN.md
+  sum_reduce                 the switch's per-slot Processor add (processor.p4:14-24)
+  quantize_reduce            worker quantise fused with the aggregator sum
+  pack_nga / unpack_nga      DataManager._send_data (DataManager.py:111-165) and the
+                             PS-side parse (NGAPacket.py:62-143), headers.p4 layout
+  pack_c128                  send_gradients' packet loop (communicator.cc:23-37)
+  ps_combine                 aggregate() (launch.py:42-52)
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from ._lib import NGA_HDR_BYTES, NUM_REGISTER, check, load, ptr_array
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _req(t: torch.Tensor, dtype, name: str):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device (HIP) tensor; the INA path has no CPU fallback")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _same_device(*ts):
+    d = ts[0].device
+    for t in ts[1:]:
+        if t.device != d:
+            raise ValueError("all tensors must be on the same device")
+
+
+def nga_stride(V: int) -> int:
+    """Recommended device packet stride: 15 + 4V rounded up to 16 bytes."""
+    return (NGA_HDR_BYTES + 4 * V + 15) // 16 * 16
+
+
+# -- quantise / dequantise -------------------------------------------------------------
+def quantize(x: torch.Tensor, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    _req(x, torch.float32, "x")
+    out = torch.empty(x.shape, dtype=torch.int32, device=x.device) if out is None else out
+    _req(out, torch.int32, "out")
+    check(load().ina_quantize_f32_i32(x.data_ptr(), out.data_ptr(), x.numel(), k, _stream(x)),
+          "quantize")
+    return out
+
+
+def quantize_i16(x: torch.Tensor, k: int, V: int, out=None, overflow=None):
+    _req(x, torch.float32, "x")
+    out = torch.empty(x.shape, dtype=torch.int16, device=x.device) if out is None else out
+    nslot = (x.numel() + V - 1) // V
+    overflow = torch.empty(nslot, dtype=torch.uint8, device=x.device) if overflow is None else overflow
+    _req(out, torch.int16, "out")
+    _req(overflow, torch.uint8, "overflow")
+    check(load().ina_quantize_f32_i16_sat(x.data_ptr(), out.data_ptr(), x.numel(), k, V,
+                                          overflow.data_ptr(), _stream(x)), "quantize_i16")
+    return out, overflow
+
+
+def dequantize(s: torch.Tensor, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    out = torch.empty(s.shape, dtype=torch.float32, device=s.device) if out is None else out
+    _req(out, torch.float32, "out")
+    if s.dtype == torch.int16:
+        _req(s, torch.int16, "s")
+        rc = load().ina_dequantize_i16_f32(s.data_ptr(), out.data_ptr(), s.numel(), k, _stream(s))
+    else:
+        _req(s, torch.int32, "s")
+        rc = load().ina_dequantize_i32_f32(s.data_ptr(), out.data_ptr(), s.numel(), k, _stream(s))
+    check(rc, "dequantize")
+    return out
+
+
+# -- aggregator --------------------------------------------------------------------------
+def _bufs(bufs, dtype, name="bufs"):
+    if isinstance(bufs, torch.Tensor):       # [W, n] stacked
+        bufs = list(bufs.unbind(0)) if bufs.dim() > 1 else [bufs]
+    bufs = list(bufs)
+    if not 1 <= len(bufs) <= _lib.MAX_WORKERS:
+        raise ValueError(f"need 1..{_lib.MAX_WORKERS} worker buffers, got {len(bufs)}")
+    n = bufs[0].numel()
+    for i, b in enumerate(bufs):
+        _req(b, dtype, f"{name}[{i}]")
+        if b.numel() != n:
+            raise ValueError("worker buffers differ in length")
+    _same_device(*bufs)
+    return bufs, n
+
+
+def sum_reduce(bufs, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = sum_w bufs[w][i] mod 2^32 (int32), the switch's slot sum."""
+    bufs, n = _bufs(bufs, torch.int32)
+    out = torch.empty(n, dtype=torch.int32, device=bufs[0].device) if out is None else out
+    _req(out, torch.int32, "out")
+    arr = ptr_array([b.data_ptr() for b in bufs])
+    check(load().ina_sum_reduce_i32(arr, len(bufs), out.data_ptr(), n, _stream(out)), "sum_reduce")
+    return out
+
+
+def sum_reduce_i16(bufs, V: int, out=None, overflow=None):
+    bufs, n = _bufs(bufs, torch.int16)
+    dev = bufs[0].device
+    out = torch.empty(n, dtype=torch.int16, device=dev) if out is None else out
+    overflow = (torch.empty((n + V - 1) // V, dtype=torch.uint8, device=dev)
+                if overflow is None else overflow)
+    arr = ptr_array([b.data_ptr() for b in bufs])
+    check(load().ina_sum_reduce_i16_sat(arr, len(bufs), out.data_ptr(), n, V, overflow.data_ptr(),
+                                        _stream(out)), "sum_reduce_i16")
+    return out, overflow
+
+
+def quantize_reduce(bufs, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    bufs, n = _bufs(bufs, torch.float32)
+    out = torch.empty(n, dtype=torch.int32, device=bufs[0].device) if out is None else out
+    _req(out, torch.int32, "out")
+    arr = ptr_array([b.data_ptr() for b in bufs])
+    check(load().ina_quantize_reduce_f32_i32(arr, len(bufs), out.data_ptr(), n, k, _stream(out)),
+          "quantize_reduce")
+    return out
+
+
+def quantize_reduce_i16(bufs, k: int, V: int, out=None, overflow=None):
+    bufs, n = _bufs(bufs, torch.float32)
+    dev = bufs[0].device
+    out = torch.empty(n, dtype=torch.int16, device=dev) if out is None else out
+    overflow = (torch.empty((n + V - 1) // V, dtype=torch.uint8, device=dev)
+                if overflow is None else overflow)
+    arr = ptr_array([b.data_ptr() for b in bufs])
+    check(load().ina_quantize_reduce_f32_i16_sat(arr, len(bufs), out.data_ptr(), n, k, V,
+                                                 overflow.data_ptr(), _stream(out)),
+          "quantize_reduce_i16")
+    return out, overflow
+
+
+# -- PS combine ----------------------------------------------------------------------------
+def ps_combine(local: torch.Tensor, paras, weight_step: float, out=None) -> torch.Tensor:
+    """launch.py:42-52: local + float(weight_step) * sum_w (paras[w] - local), bit-exact."""
+    _req(local, torch.float32, "local")
+    paras, n = _bufs(paras, torch.float32, "paras")
+    if n != local.numel():
+        raise ValueError("local and paras differ in length")
+    out = torch.empty_like(local) if out is None else out
+    arr = ptr_array([p.data_ptr() for p in paras])
+    check(load().ina_ps_combine_f32(local.data_ptr(), arr, len(paras), float(weight_step),
+                                    out.data_ptr(), n, _stream(local)), "ps_combine")
+    return out
+
+
+def ps_apply(local: torch.Tensor, sum_int: torch.Tensor, k: int, weight_step: float, out=None):
+    """INA update: local + float(weight_step) * dequantize(sum_int, k)."""
+    _req(local, torch.float32, "local")
+    _req(sum_int, torch.int32, "sum_int")
+    out = torch.empty_like(local) if out is None else out
+    check(load().ina_ps_apply_i32(local.data_ptr(), sum_int.data_ptr(), k, float(weight_step),
+                                  out.data_ptr(), local.numel(), _stream(local)), "ps_apply")
+    return out
+
+
+# -- packets -----------------------------------------------------------------------------------
+def pack_nga(vals: torch.Tensor, V: int, bitmap: int, count: int, switch_id: int, seq0: int,
+             flags: int = 0, num_slots: int = NUM_REGISTER, stride: int | None = None,
+             overflow: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Returns uint8 [npkts, stride] device packets (first 15 + 4V bytes of each row on the wire)."""
+    _req(vals, torch.int32, "vals")
+    stride = stride or nga_stride(V)
+    npk = (vals.numel() + V - 1) // V
+    out = torch.empty((npk, stride), dtype=torch.uint8, device=vals.device) if out is None else out
+    prm = _lib.NgaParams(bitmap & 0xFFFFFFFF, count & 0xFF, flags & 0xFF, switch_id & 0xFF, 0,
+                         seq0 & 0xFFFFFFFF, num_slots, V)
+    ovp = None
+    if overflow is not None:
+        _req(overflow, torch.uint8, "overflow")
+        ovp = overflow.data_ptr()
+    check(load().ina_pack_nga(vals.data_ptr(), vals.numel(), C.byref(prm), ovp, out.data_ptr(),
+                              stride, _stream(vals)), "pack_nga")
+    return out
+
+
+def unpack_nga(pkts: torch.Tensor, V: int, stride: int | None = None, with_values: bool = True):
+    """Returns (fields dict of device tensors, int32 values [npkts*V] or None)."""
+    _req(pkts, torch.uint8, "pkts")
+    stride = stride or (pkts.shape[1] if pkts.dim() == 2 else nga_stride(V))
+    npk = pkts.numel() // stride
+    dev = pkts.device
+    f = {"bitmap": torch.empty(npk, dtype=torch.int32, device=dev),
+         "count": torch.empty(npk, dtype=torch.uint8, device=dev),
+         "flags": torch.empty(npk, dtype=torch.uint8, device=dev),
+         "index": torch.empty(npk, dtype=torch.int32, device=dev),
+         "switch_id": torch.empty(npk, dtype=torch.uint8, device=dev),
+         "frag_id": torch.empty(npk, dtype=torch.int32, device=dev)}
+    fs = _lib.NgaFields(*[f[k].data_ptr() for k in
+                          ("bitmap", "count", "flags", "index", "switch_id", "frag_id")])
+    vals = torch.empty(npk * V, dtype=torch.int32, device=dev) if with_values else None
+    check(load().ina_unpack_nga(pkts.data_ptr(), npk, V, stride, C.byref(fs),
+                                vals.data_ptr() if vals is not None else None, _stream(pkts)),
+          "unpack_nga")
+    return f, vals
+
+
+def pack_c128(gradient: torch.Tensor, packet_num: int, worker_id: int, aggregator_index: int,
+              tensor_index: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """communicator.cc's packet_t x packet_num as uint8 [packet_num, 524] (device)."""
+    if gradient.dtype not in (torch.int32, torch.uint32):
+        raise TypeError("gradient must be int32/uint32")
+    if not gradient.is_cuda or not gradient.is_contiguous():
+        raise ValueError("gradient must be a contiguous device tensor")
+    if gradient.numel() < packet_num * 128:
+        raise ValueError("gradient shorter than packet_num * 128")
+    out = (torch.empty((packet_num, _lib.C128_BYTES), dtype=torch.uint8, device=gradient.device)
+           if out is None else out)
+    check(load().ina_pack_c128(gradient.data_ptr(), packet_num, worker_id,
+                               aggregator_index & 0xFFFFFFFF, tensor_index, out.data_ptr(),
+                               _stream(gradient)), "pack_c128")
+    return out
+
+
+# -- integrity --------------------------------------------------------------------------------
+def checksum(x: torch.Tensor) -> torch.Tensor:
+    """Device u32 (as int64 tensor view) of sum_i x[i]*(2i+1) mod 2^32."""
+    _req(x, torch.int32, "x")
+    out = torch.empty(1, dtype=torch.int32, device=x.device)
+    check(load().ina_checksum_i32(x.data_ptr(), x.numel(), out.data_ptr(), _stream(x)), "checksum")
+    return out
+
+
+# -- device packet-stream switch ---------------------------------------------------------------
+class Switch:
+    """ngaa.p4's aggregator with its registers in HBM (count u8, frag u32, V x u32 per slot)."""
+
+    def __init__(self, V: int = 32, num_slots: int = NUM_REGISTER, switch_id: int = 1,
+                 device: str | torch.device = "cuda"):
+        self.V, self.num_slots, self.switch_id = V, num_slots, switch_id
+        self.count = torch.zeros(num_slots, dtype=torch.uint8, device=device)
+        self.frag = torch.zeros(num_slots, dtype=torch.int32, device=device)
+        self.regs = torch.zeros((num_slots, V), dtype=torch.int32, device=device)
+        self._state = _lib.SwitchState(num_slots, V, switch_id, self.count.data_ptr(),
+                                       self.frag.data_ptr(), self.regs.data_ptr())
+        self._scratch = None
+
+    def process(self, pkts: torch.Tensor, actions: torch.Tensor | None = None) -> torch.Tensor:
+        """Runs packets (uint8 [npkts, stride], arrival order) through the switch in place;
+        returns the uint8 action per packet (ACT_*)."""
+        _req(pkts, torch.uint8, "pkts")
+        npk, stride = pkts.shape
+        actions = torch.empty(npk, dtype=torch.uint8, device=pkts.device) if actions is None else actions
+        need = load().ina_switch_scratch_bytes(npk, self.num_slots)
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
+        check(load().ina_switch_process(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                        actions.data_ptr(), self._scratch.data_ptr(),
+                                        _stream(pkts)), "switch_process")
+        return actions
+
+
+def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
+               nontemporal: bool | None = None):
+    lib = load()
+    if max_blocks is not None:
+        check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
+    if unroll is not None:
+        check(lib.ina_set_tuning(1, int(unroll)), "set_tuning")
+    if nontemporal is not None:
+        check(lib.ina_set_tuning(2, int(bool(nontemporal))), "set_tuning")
+
+
+def version() -> str:
+    return load().ina_version().decode()

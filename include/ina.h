@@ -1,0 +1,183 @@
+/*
+ * ina.h -- C ABI of libina.so, the MI355X-native gradient-aggregation path.
+ *
+ * Drop-in boundary for the reference Fangjin98/distributed-training-INA:
+ *   - the in-switch aggregator (src/p4/p4src/ngaa.p4, processor.p4, fragcheck.p4)
+ *     becomes device kernels (sum-reduce, packet-stream switch);
+ *   - the worker-side quantise/packetise code (src/common/DataManager.py,
+ *     communicator.{h,cc,py}, NGAPacket.py) becomes device quantise/pack/unpack;
+ *   - the legacy C symbol send_gradients (communicator.h:27) keeps its exact
+ *     signature so the reference's ctypes loader (communicator.py:15-24) binds it.
+ *
+ * Conventions (all ina_* entry points):
+ *   - plain pointers and sizes; every data pointer is a DEVICE pointer (hipMalloc /
+ *     torch CUDA tensor) owned by the caller, borrowed for the call;
+ *   - arrays of worker buffers (`bufs`) are HOST arrays of W device pointers; the
+ *     array itself is copied into the kernel arguments, so it may live on the stack;
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream); calls are
+ *     asynchronous on that stream and never synchronise, allocate or free;
+ *   - return 0 on success, a negative INA_E* code otherwise (no exit(), unlike
+ *     communicator.cc:11-12,38-39); ina_last_error_string() describes the last error.
+ * Vector fast paths need 16-byte aligned pointers; other alignments take a slower
+ * scalar path with identical results.
+ */
+#ifndef INA_H
+#define INA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INA_OK 0
+#define INA_EINVAL (-1)   /* bad argument */
+#define INA_EHIP (-2)     /* HIP runtime / launch error */
+#define INA_ESOCK (-3)    /* socket error (host send path) */
+#define INA_ENOMEM (-4)
+
+#define INA_MAX_WORKERS 64      /* W per launch */
+#define INA_NGA_HDR_BYTES 15    /* ngaa_h, headers.p4:27-38 */
+#define INA_NUM_REGISTER 16384u /* aggregator slots, config.p4:5 */
+#define INA_C128_VALUES 128     /* TENSOR_NUM, communicator.h:18 */
+#define INA_C128_BYTES 524      /* sizeof(packet_t), communicator.h:20-25 */
+
+/* ngaa_h flag byte: overflow|is_ack|collision|resend|timestamp[3:0] (headers.p4:30-34) */
+#define INA_FLAG_OVERFLOW 0x80u
+#define INA_FLAG_ACK 0x40u
+#define INA_FLAG_COLLISION 0x20u
+#define INA_FLAG_RESEND 0x10u
+
+/* forwarding decision per packet of the switch (ngaa.p4:120-196) */
+#define INA_ACT_DROP 0
+#define INA_ACT_FWD_AGG 1        /* aggregation complete: payload = slot sum */
+#define INA_ACT_FWD_COLLISION 2  /* frag mismatch: collision=1, payload untouched */
+#define INA_ACT_FWD_ACK 3        /* PS ack: frag register cleared */
+#define INA_ACT_FWD_OTHER 4      /* switch_id not ours */
+
+typedef void* ina_stream_t; /* hipStream_t */
+
+const char* ina_version(void);
+const char* ina_last_error_string(void);
+
+/* ---- quantise / dequantise ---------------------------------------------------
+ * Replaces float_to_int / int_to_float, imported at DataManager.py:9 and
+ * NGAPacket.py:5 (used DataManager.py:37,168, NGAPacket.py:118) but absent from
+ * the reference repo.  Build-defined: q = sat(round_half_even(x * 2^k)), NaN -> 0,
+ * k in [-126, 127]; dequantise y = (float)q * 2^-k (exact scaling).            */
+int ina_quantize_f32_i32(const float* x, int32_t* q, size_t n, int k, ina_stream_t stream);
+/* int16 saturating (config 4): overflow_per_slot[s] = 1 iff an element of slot s
+ * (V consecutive values) saturated or was NaN, else 0 (every slot written). May be NULL. */
+int ina_quantize_f32_i16_sat(const float* x, int16_t* q, size_t n, int k, int V,
+                             uint8_t* overflow_per_slot, ina_stream_t stream);
+int ina_dequantize_i32_f32(const int32_t* s, float* y, size_t n, int k, ina_stream_t stream);
+int ina_dequantize_i16_f32(const int16_t* s, float* y, size_t n, int k, ina_stream_t stream);
+
+/* ---- the aggregator ------------------------------------------------------------
+ * Replaces the switch's per-slot Processor add (processor.p4:14-24, x32 at
+ * ngaa.p4:87-168): out[i] = sum_w bufs[w][i] mod 2^32, bit-identical to the
+ * switch for any arrival order.  1 <= W <= INA_MAX_WORKERS.  out may alias bufs[0]. */
+int ina_sum_reduce_i32(const int32_t* const* bufs, int W, int32_t* out, size_t n,
+                       ina_stream_t stream);
+/* int16 narrow path: exact int32 accumulation, one saturation to int16; overflow
+ * flag per slot of V values as above. */
+int ina_sum_reduce_i16_sat(const int16_t* const* bufs, int W, int16_t* out, size_t n, int V,
+                           uint8_t* overflow_per_slot, ina_stream_t stream);
+/* fused quantise + reduce from W fp32 worker buffers (configs 2 and 4) */
+int ina_quantize_reduce_f32_i32(const float* const* bufs, int W, int32_t* out, size_t n, int k,
+                                ina_stream_t stream);
+int ina_quantize_reduce_f32_i16_sat(const float* const* bufs, int W, int16_t* out, size_t n,
+                                    int k, int V, uint8_t* overflow_per_slot,
+                                    ina_stream_t stream);
+
+/* ---- PS combine ------------------------------------------------------------------
+ * launch.py:42-52 / launch_async.py:42-57 aggregate(), fused, bit-exact to the
+ * torch fp32 sequence: out = local + float(weight_step) * (0 + sum_w (paras[w] - local)).
+ * out may alias local. */
+int ina_ps_combine_f32(const float* local, const float* const* paras, int W, double weight_step,
+                       float* out, size_t n, ina_stream_t stream);
+/* INA form of the same update: out = local + float(weight_step) * dequant(sum_int) */
+int ina_ps_apply_i32(const float* local, const int32_t* sum_int, int k, double weight_step,
+                     float* out, size_t n, ina_stream_t stream);
+
+/* ---- packets ------------------------------------------------------------------- */
+typedef struct ina_nga_params {
+    uint32_t bitmap;    /* header word 0; DataManager passes worker_id raw (DataManager.py:124) */
+    uint8_t count;      /* aggregation degree (ngaa_h.count) */
+    uint8_t flags;      /* flag byte; INA_FLAG_OVERFLOW is OR-ed per slot from overflow_per_slot */
+    uint8_t switch_id;
+    uint8_t pad;
+    uint32_t seq0;      /* packet p: frag_id = seq0 + p, index = (seq0 + p) % num_slots */
+    uint32_t num_slots; /* INA_NUM_REGISTER (DataManager.py:119 uses 16384) */
+    int32_t V;          /* payload words per packet (32 = the P4 program; 128, 256, ...) */
+} ina_nga_params_t;
+
+typedef struct ina_nga_fields { /* SoA header fields; any pointer may be NULL */
+    uint32_t* bitmap;
+    uint8_t* count;
+    uint8_t* flags;
+    uint32_t* index;
+    uint8_t* switch_id;
+    uint32_t* frag_id;
+} ina_nga_fields_t;
+
+/* NGA-V pack (DataManager._send_data, DataManager.py:111-165 / headers.p4:27-80):
+ * ceil(n/V) packets at `stride` bytes (>= 15 + 4V): 15-byte big-endian header,
+ * V big-endian 32-bit words, zero-padded tail.  stride % 16 == 0 with 16-byte
+ * aligned buffers takes the vector path (the recommended layout; each packet is a
+ * sendmmsg iovec of 15 + 4V bytes).  overflow_per_slot may be NULL. */
+int ina_pack_nga(const int32_t* vals, size_t n, const ina_nga_params_t* prm,
+                 const uint8_t* overflow_per_slot, uint8_t* pkts, size_t stride,
+                 ina_stream_t stream);
+/* PS-side parse (NGAPacket.py:62-143 / get_data_from_nic, utils.py:61-64), following
+ * headers.p4: payload at byte 15, big-endian.  vals gets npkts*V int32 (may be NULL). */
+int ina_unpack_nga(const uint8_t* pkts, size_t npkts, int V, size_t stride,
+                   const ina_nga_fields_t* fields, int32_t* vals, ina_stream_t stream);
+/* C-128 pack (communicator.cc:23-37): npkts x 524-byte packet_t, all words htonl. */
+int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id,
+                  uint32_t aggregator_index, int tensor_index, uint8_t* pkts,
+                  ina_stream_t stream);
+
+/* ---- packet-stream switch (ngaa.p4:120-196 restated on the device) -------------
+ * State lives in device memory: count[num_slots] u8, frag[num_slots] u32,
+ * regs[num_slots*V] u32 (zero-initialise once, like the P4 registers).  Packets are
+ * processed in array order per slot (different slots are independent); packets are
+ * rewritten in place (running sum, collision bit) and actions[p] gets INA_ACT_*.
+ * scratch: device buffer of ina_switch_scratch_bytes(npkts, num_slots) bytes.  */
+typedef struct ina_switch_state {
+    uint32_t num_slots;
+    int32_t V;
+    int32_t switch_id;  /* the switch_check entry (ngaa.p4:27-37); -1 = none */
+    uint8_t* count;
+    uint32_t* frag;
+    uint32_t* regs;
+} ina_switch_state_t;
+size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots);
+int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
+                       uint8_t* actions, void* scratch, ina_stream_t stream);
+
+/* ---- integrity ------------------------------------------------------------------
+ * *out_dev (device u32) = sum_i x[i]*(2i+1) mod 2^32 (linear in x, so the checksum
+ * of a reduce equals the wrapped sum of the input checksums). */
+int ina_checksum_i32(const int32_t* x, size_t n, uint32_t* out_dev, ina_stream_t stream);
+
+/* ---- host send path --------------------------------------------------------------
+ * Legacy symbol, exact reference signature and behaviour (communicator.h:27,
+ * communicator.cc:3-47): gradient_array is a HOST pointer to packet_num*128 u32;
+ * packets are built on the GPU (ina_pack_c128) and sent with sendmmsg on a raw
+ * IPPROTO_UDP socket to dst_ip (host order).  Like the reference, a socket
+ * failure prints perror and exits the process with -1. */
+void send_gradients(uint32_t* gradient_array, int packet_num, uint32_t dst_ip, int worker_id,
+                    uint32_t aggregator_index, int tensor_index);
+/* Same as send_gradients but returns a status instead of exiting, and sends on a
+ * caller-provided datagram socket fd (connected, or dst_ip used as AF_INET dest
+ * when dst_ip != 0).  Returns packets sent (>= 0) or INA_E*. */
+int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num,
+                          uint32_t dst_ip, int worker_id, uint32_t aggregator_index,
+                          int tensor_index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INA_H */

@@ -1,0 +1,74 @@
+"""C-ABI boundary checks that need no GPU: libina.so loads, exports every
+function include/ina.h declares, and the Python layer rejects bad input before
+any device call (no CPU fallback exists)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "ina.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", src, flags=re.M)
+    return sorted({n for n in names if not n.startswith("INA_") and n not in ("defined",)})
+
+
+def test_header_declares_expected_surface():
+    fns = declared_functions()
+    for must in ("ina_sum_reduce_i32", "ina_quantize_f32_i32", "ina_pack_nga", "ina_unpack_nga",
+                 "ina_pack_c128", "ina_switch_process", "send_gradients", "ina_ps_combine_f32"):
+        assert must in fns
+    assert len(fns) >= 20
+
+
+def test_library_exports_every_declared_symbol():
+    from ina_amd import _lib
+    lib = _lib.load()
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    # and the Python binding knows every one of them
+    assert not [f for f in declared_functions() if f not in _lib.SIGNATURES]
+
+
+def test_legacy_symbol_is_unmangled_c():
+    """communicator.py:15-24 binds `send_gradients` by its C name."""
+    from ina_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    assert lib.send_gradients is not None
+    assert _lib.load().ina_version().decode().startswith("ina-mi355x")
+
+
+def test_error_codes_without_device_work():
+    from ina_amd import _lib
+    lib = _lib.load()
+    assert lib.ina_quantize_f32_i32(None, None, 10, 500, None) == _lib.INA_EINVAL
+    assert b"k out of range" in lib.ina_last_error_string()
+    assert lib.ina_sum_reduce_i32(None, 0, None, 10, None) == _lib.INA_EINVAL
+    assert lib.ina_sum_reduce_i32(None, 3, None, 0, None) == 0     # n == 0 is a no-op
+    assert lib.ina_pack_c128(None, -1, 1, 0, 0, None, None) == _lib.INA_EINVAL
+    prm = _lib.NgaParams(1, 2, 0, 1, 0, 1, 16384, 32)
+    assert lib.ina_pack_nga(None, 64, ctypes.byref(prm), None, None, 100, None) == _lib.INA_EINVAL
+    st = _lib.SwitchState(16384, 512, 1, None, None, None)
+    assert lib.ina_switch_process(ctypes.byref(st), None, 1, 2064, None, None, None) == _lib.INA_EINVAL
+
+
+def test_ops_refuse_cpu_tensors():
+    from ina_amd import ops
+    x = torch.zeros(16, dtype=torch.float32)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.quantize(x, 16)
+    with pytest.raises(ValueError):
+        ops.sum_reduce([torch.zeros(8, dtype=torch.int32)])
+
+
+def test_nga_stride():
+    from ina_amd import ops
+    assert ops.nga_stride(32) == 144 and ops.nga_stride(256) == 1040 and ops.nga_stride(128) == 528

@@ -1,0 +1,393 @@
+"""GPU parity: every libina.so device entry point against the CPU oracle (and,
+where the reference left outputs, against the reference's own bytes).
+
+Integer / byte / index work must be bit-exact.  The PS combine is bit-exact to
+the reference's torch fp32 sequence (tolerance 0 ULP).  The quantiser is
+build-defined (the reference's is missing), so its parity is against the
+oracle's restatement of the same definition (bit-exact).
+"""
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+from tests._golden import load_capture, manifest, ps_cases
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ina_amd import ops  # noqa: F401  (fails loudly if libina.so is missing)
+
+
+def ops():
+    from ina_amd import ops as o
+    return o
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def rand_i32(rng, n, full=True):
+    if full:
+        return rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+    return rng.integers(-2**20, 2**20, size=n, dtype=np.int64).astype(np.int32)
+
+
+# --------------------------------------------------------------------------------------
+# sum-reduce (processor.p4:14-24)
+# --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("W", [1, 2, 3, 4, 5, 8, 16, 17, 64])
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 1023, 4097, 100003])
+def test_sum_reduce_matches_oracle(W, n):
+    rng = np.random.default_rng(W * 1000 + n)
+    bufs = [rand_i32(rng, n) for _ in range(W)]
+    got = host(ops().sum_reduce([dev(b) for b in bufs]))
+    assert np.array_equal(got, orc.sum_reduce_i32(bufs))
+
+
+def test_sum_reduce_unaligned_views_take_scalar_path():
+    rng = np.random.default_rng(5)
+    n = 5001
+    big = [dev(rand_i32(rng, n + 1)) for _ in range(8)]
+    views = [b[1:] for b in big]            # 4-byte offset: not 16-byte aligned
+    got = host(ops().sum_reduce(views))
+    assert np.array_equal(got, orc.sum_reduce_i32([host(v) for v in views]))
+
+
+def test_sum_reduce_in_place_alias():
+    rng = np.random.default_rng(6)
+    bufs = [rand_i32(rng, 4099) for _ in range(4)]
+    want = orc.sum_reduce_i32(bufs)
+    d = [dev(b) for b in bufs]
+    ops().sum_reduce(d, out=d[0])
+    assert np.array_equal(host(d[0]), want)
+
+
+def test_sum_reduce_stacked_tensor_input():
+    rng = np.random.default_rng(7)
+    stack = np.stack([rand_i32(rng, 777) for _ in range(8)])
+    got = host(ops().sum_reduce(dev(stack)))
+    assert np.array_equal(got, orc.sum_reduce_i32(list(stack)))
+
+
+@pytest.mark.parametrize("unroll,blocks,nt", [(1, 2048, True), (4, 512, True), (2, 4096, False)])
+def test_sum_reduce_tunings_identical(unroll, blocks, nt):
+    rng = np.random.default_rng(8)
+    bufs = [rand_i32(rng, 300007) for _ in range(8)]
+    o = ops()
+    try:
+        o.set_tuning(max_blocks=blocks, unroll=unroll, nontemporal=nt)
+        got = host(o.sum_reduce([dev(b) for b in bufs]))
+    finally:
+        o.set_tuning(max_blocks=2048, unroll=2, nontemporal=True)
+    assert np.array_equal(got, orc.sum_reduce_i32(bufs))
+
+
+def test_sum_reduce_config3_full_size():
+    """BASELINE config 3: 8 workers x 100 MiB int32, full-range values (wraps)."""
+    n = 26_214_400
+    rng = np.random.default_rng(1234)
+    bufs = [rand_i32(rng, n) for _ in range(8)]
+    got = ops().sum_reduce([dev(b) for b in bufs])
+    want = orc.sum_reduce_i32(bufs)
+    g = host(got)
+    assert np.array_equal(g, want)
+    # size-independent property: the checksum of the sum == wrapped sum of checksums
+    cs = int(host(ops().checksum(got))[0]) & 0xFFFFFFFF
+    assert cs == sum(orc.checksum_i32(b) for b in bufs) % 2**32 == orc.checksum_i32(want)
+
+
+# --------------------------------------------------------------------------------------
+# quantise / dequantise (build-defined; parity vs the oracle's restatement)
+# --------------------------------------------------------------------------------------
+EDGE = np.array([0.0, -0.0, 0.5, 1.5, 2.5, -0.5, -1.5, 1e-45, -1e-45, 1e-38, np.inf, -np.inf,
+                 np.nan, 3e38, -3e38, 32767.5, -32768.5, 2147483520.0, 2147483648.0,
+                 -2147483648.0, -2147483904.0, 0.49999997, -0.49999997], np.float32)
+
+
+def mixed_floats(rng, n):
+    x = (rng.standard_normal(n) * 10.0 ** rng.integers(-8, 8, n)).astype(np.float32)
+    x[:min(n, len(EDGE))] = EDGE[:min(n, len(EDGE))]
+    return x
+
+
+@pytest.mark.parametrize("k", [0, 16, 24, -4, 127, -126])
+@pytest.mark.parametrize("n", [1, 23, 4096, 100001])
+def test_quantize_i32(k, n):
+    x = mixed_floats(np.random.default_rng(n + k), n)
+    assert np.array_equal(host(ops().quantize(dev(x), k)), orc.quantize_i32(x, k))
+
+
+@pytest.mark.parametrize("V", [32, 128, 256, 8, 512, 100])
+@pytest.mark.parametrize("n", [7, 8, 1000, 65537])
+def test_quantize_i16_flags(V, n):
+    x = (np.random.default_rng(V + n).standard_normal(n) * 40).astype(np.float32)
+    x[: min(n, len(EDGE))] = EDGE[: min(n, len(EDGE))]
+    q, ovf = ops().quantize_i16(dev(x), 10, V)
+    qo, ovfo = orc.quantize_i16_sat(x, 10, V)
+    assert np.array_equal(host(q), qo)
+    assert np.array_equal(host(ovf), ovfo)
+
+
+@pytest.mark.parametrize("k", [0, 16, 30])
+def test_dequantize(k):
+    rng = np.random.default_rng(k)
+    s = rand_i32(rng, 70001)
+    got = host(ops().dequantize(dev(s), k))
+    assert np.array_equal(got.view(np.uint32), orc.dequantize_i32(s, k).view(np.uint32))
+    s16 = rng.integers(-32768, 32768, 1001).astype(np.int16)
+    got16 = host(ops().dequantize(dev(s16), k))
+    assert np.array_equal(got16.view(np.uint32), orc.dequantize_i16(s16, k).view(np.uint32))
+
+
+def test_quantize_dequantize_round_trip_bound():
+    x = (np.random.default_rng(3).standard_normal(1 << 20) * 1e-2).astype(np.float32)
+    k = 16
+    y = host(ops().dequantize(ops().quantize(dev(x), k), k))
+    assert np.abs(y - x).max() <= 2.0 ** -(k + 1)
+
+
+# --------------------------------------------------------------------------------------
+# fused quantise + reduce (configs 2 and 4) and the int16 narrow reduce
+# --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("W", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("n", [5, 1024, 50003])
+def test_quantize_reduce_i32(W, n):
+    rng = np.random.default_rng(W + n)
+    bufs = [mixed_floats(rng, n) for _ in range(W)]
+    got = host(ops().quantize_reduce([dev(b) for b in bufs], 16))
+    assert np.array_equal(got, orc.quantize_reduce_i32(bufs, 16))
+
+
+@pytest.mark.parametrize("W", [3, 4, 8, 16])
+@pytest.mark.parametrize("V", [32, 256, 96])
+def test_quantize_reduce_i16(W, V):
+    rng = np.random.default_rng(W * V)
+    n = 20 * V + 13
+    bufs = [(rng.standard_normal(n) * 3).astype(np.float32) for _ in range(W)]
+    bufs[0][:len(EDGE)] = EDGE
+    out, ovf = ops().quantize_reduce_i16([dev(b) for b in bufs], 10, V)
+    wo, wf = orc.quantize_reduce_i16_sat(bufs, 10, V)
+    assert np.array_equal(host(out), wo)
+    assert np.array_equal(host(ovf), wf)
+    assert 0 < wf.sum() < len(wf)     # the overflow path is exercised, not universal
+
+
+@pytest.mark.parametrize("W,V", [(2, 32), (16, 256), (5, 100)])
+def test_sum_reduce_i16(W, V):
+    rng = np.random.default_rng(W + V)
+    n = 33 * V + 3
+    bufs = [rng.integers(-9000, 9000, n).astype(np.int16) for _ in range(W)]
+    out, ovf = ops().sum_reduce_i16([dev(b) for b in bufs], V)
+    wo, wf = orc.sum_reduce_i16_sat(bufs, V)
+    assert np.array_equal(host(out), wo) and np.array_equal(host(ovf), wf)
+
+
+def test_config2_full_size_fused():
+    """BASELINE config 2: ResNet-50-sized fp32 bucket (25,557,032), 4 workers, int32."""
+    n = 25_557_032
+    bufs = [(np.random.default_rng(1000 + w).standard_normal(n) * 1e-2).astype(np.float32)
+            for w in range(4)]
+    got = host(ops().quantize_reduce([dev(b) for b in bufs], 16))
+    assert np.array_equal(got, orc.quantize_reduce_i32(bufs, 16))
+
+
+def test_config4_full_size_int16():
+    """BASELINE config 4: ResNet-50 gradient, 16 workers, int16 saturating."""
+    n, W, V = 25_557_032, 16, 256
+    bufs = []
+    for w in range(W):
+        r = np.random.default_rng(1000 + w)
+        g = (r.standard_normal(n) * 1e-2).astype(np.float32)
+        out = r.random(n) < 0.01
+        g[out] *= 100
+        bufs.append(g)
+    k = 12   # 16 * max|g| * 2^k stays inside int16 for most values
+    q, ovf = ops().quantize_reduce_i16([dev(b) for b in bufs], k, V)
+    wq, wf = orc.quantize_reduce_i16_sat(bufs, k, V)
+    assert np.array_equal(host(q), wq) and np.array_equal(host(ovf), wf)
+    assert 0 < wf.sum() < len(wf)
+
+
+# --------------------------------------------------------------------------------------
+# PS combine (launch.py:42-52): bit-exact against the reference's own outputs
+# --------------------------------------------------------------------------------------
+def test_ps_combine_matches_reference_aggregate_outputs():
+    for name, c in ps_cases().items():
+        W, K = int(c["W"]), int(c["K"])
+        paras = list(c["paras"])
+        if K > 0:
+            paras, weight = paras[:K], 1.0 / K
+        else:
+            weight = 1.0 / (W + 1)
+        got = host(ops().ps_combine(dev(c["local"]), [dev(p) for p in paras],
+                                    weight * float(c["step"])))
+        assert np.array_equal(got.view(np.uint32), c["out"].view(np.uint32)), name
+
+
+def test_ps_combine_random_vs_oracle():
+    rng = np.random.default_rng(11)
+    n = 100_000
+    local = rng.standard_normal(n).astype(np.float32)
+    paras = [(local + rng.standard_normal(n).astype(np.float32) * 1e-3) for _ in range(7)]
+    got = host(ops().ps_combine(dev(local), [dev(p) for p in paras], 1.0 / 8))
+    want = orc.ps_combine_f32(local, paras, 1.0 / 8)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_ps_apply_ina_update():
+    rng = np.random.default_rng(12)
+    n, W, k = 50_001, 4, 16
+    local = rng.standard_normal(n).astype(np.float32)
+    paras = [(local + rng.standard_normal(n).astype(np.float32) * 1e-2) for _ in range(W)]
+    deltas = [dev(p - local) for p in paras]
+    s = ops().quantize_reduce(deltas, k)
+    out = host(ops().ps_apply(dev(local), s, k, 1.0 / (W + 1)))
+    d = orc.dequantize_i32(orc.quantize_reduce_i32([p - local for p in paras], k), k)
+    want = (local + (d * np.float32(1.0 / (W + 1))).astype(np.float32)).astype(np.float32)
+    assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
+    ref = orc.ps_combine_f32(local, paras, 1.0 / (W + 1))
+    # quantisation error bound: W * 2^-(k+1) * weight (+ fp32 rounding of the combine)
+    assert np.abs(out - ref).max() <= W * 2.0 ** -(k + 1) / (W + 1) + 4 * np.finfo(np.float32).eps * np.abs(ref).max()
+
+
+# --------------------------------------------------------------------------------------
+# packets
+# --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("V", [32, 128, 256, 4, 1, 33])
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 300, 8191])
+@pytest.mark.parametrize("padded", [True, False])
+def test_pack_nga_matches_oracle(V, n, padded):
+    o = ops()
+    rng = np.random.default_rng(V * 7 + n)
+    vals = rand_i32(rng, n)
+    npk = -(-n // V)
+    ovf = (rng.random(npk) < 0.3).astype(np.uint8)
+    stride = o.nga_stride(V) if padded else 15 + 4 * V
+    got = host(o.pack_nga(dev(vals), V, bitmap=0xDEADBEEF, count=8, switch_id=3, seq0=16380,
+                          flags=0x11, stride=stride, overflow=dev(ovf)))
+    want = orc.pack_nga(vals, V, 0xDEADBEEF, 8, 3, 16380, flags=0x11, stride=stride, ovf=ovf)
+    assert np.array_equal(got, want)
+    f, v = o.unpack_nga(dev(got), V, stride=stride)
+    fo, vo = orc.unpack_nga(want, V, stride=stride)
+    assert np.array_equal(host(v), vo)
+    for key in fo:
+        assert np.array_equal(host(f[key]).view(fo[key].dtype), fo[key]), key
+
+
+@pytest.mark.parametrize("case", manifest("nga_cases.json"), ids=lambda c: c["name"])
+def test_pack_nga_matches_reference_datagrams(case):
+    """Device packets == the datagrams DataManager._send_data emitted (same int payload)."""
+    q, pkts = load_capture(case["file"])
+    seq0 = {"send_data": 1, "fast_send_data": 0, "_send_data_end": 5}[case["entry"]]
+    data = [p for p in pkts if len(p) == 143]
+    got = host(ops().pack_nga(dev(q), 32, case["worker_id"], case["degree"], case["switch_id"],
+                              seq0))
+    assert len(got) == len(data)
+    for g, p in zip(got, data):
+        assert g[:143].tobytes() == p and not g[143:].any()
+
+
+@pytest.mark.parametrize("case", manifest("c128_cases.json"), ids=lambda c: c["name"])
+def test_pack_c128_matches_reference_bytes(case):
+    data, pkts = load_capture(case["file"])
+    if case["kind"] == "wrapper":
+        args = (case["packet_num"], case["worker_id"], case["aggregator_index"], case["tensor_index"])
+    elif case["kind"] == "single":
+        args = (len(data) // 128, 0, 0, 0)
+    else:
+        pytest.skip("thread fan-out compared in test_oracle_golden (host-side split)")
+    g = dev(data.view(np.int32))
+    got = host(ops().pack_c128(g, *args))
+    assert got.tobytes() == b"".join(pkts)
+
+
+def test_send_gradients_fd_over_socketpair():
+    """The host send path (legacy send_gradients body) delivers exactly the reference's
+    packet_t datagrams, one per packet, over a datagram socket."""
+    from ina_amd import _lib
+    data, pkts = load_capture("c128_w3_agg7_t10.bin")
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    try:
+        arr = np.ascontiguousarray(data)
+        rc = _lib.load().ina_send_gradients_fd(a.fileno(), arr.ctypes.data, 3, 0, 3, 7, 10)
+        assert rc == 3
+        got = [b.recv(2048) for _ in range(3)]
+    finally:
+        a.close()
+        b.close()
+    assert got == pkts
+
+
+# --------------------------------------------------------------------------------------
+# device packet-stream switch vs the oracle's P4 restatement
+# --------------------------------------------------------------------------------------
+def make_stream(rng, V, nslots_used, W, num_slots, collide=0.05, ack=0.1, other=0.05):
+    pk = []
+    for s in range(nslots_used):
+        frag = int(rng.integers(0, 4)) if rng.random() < 0.1 else 1000 + s
+        deg = int(rng.choice([W, W, W, 1, 0, 2]))
+        idx = int(rng.integers(0, num_slots * 2))
+        for w in range(W):
+            vals = rand_i32(rng, V)
+            f = frag if rng.random() > collide else frag + 1
+            flags = orc.FLAG_ACK if rng.random() < ack else 0
+            sw = 2 if rng.random() < other else 1
+            p = orc.pack_nga(vals, V, w + 1, deg, sw, 0, flags=flags,
+                             stride=ops().nga_stride(V))[0].copy()
+            p[6:10] = np.frombuffer(idx.to_bytes(4, "big"), np.uint8)
+            p[11:15] = np.frombuffer(f.to_bytes(4, "big"), np.uint8)
+            pk.append(p)
+    pk = np.stack(pk)
+    return pk[rng.permutation(len(pk))] if rng.random() < 0.5 else pk
+
+
+@pytest.mark.parametrize("V,num_slots,W", [(32, 16384, 4), (32, 64, 8), (256, 128, 3), (128, 16, 16)])
+def test_switch_stream_matches_oracle(V, num_slots, W):
+    rng = np.random.default_rng(V + num_slots + W)
+    o = ops()
+    sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV)
+    sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+    for rnd in range(3):                  # state persists across batches
+        stream = make_stream(rng, V, 60, W, num_slots)
+        want_pk, want_act = sw_orc.run(stream, stride=o.nga_stride(V))
+        d = dev(stream)
+        act = sw_dev.process(d)
+        assert np.array_equal(host(act), want_act), rnd
+        assert np.array_equal(host(d), want_pk), rnd
+        cnt, frag, regs = sw_orc.registers()
+        assert np.array_equal(host(sw_dev.count), cnt)
+        assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+        assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+
+
+def test_switch_collision_free_equals_bulk_reduce():
+    """Stateful device switch over a full W-worker stream == the bulk sum-reduce."""
+    rng = np.random.default_rng(77)
+    o = ops()
+    V, W, n = 256, 8, 256 * 500 + 17
+    bufs = [rand_i32(rng, n) for _ in range(W)]
+    sw = o.Switch(V, num_slots=16384, switch_id=1, device=DEV)
+    stream = torch.cat([o.pack_nga(dev(b), V, w + 1, W, 1, 1) for w, b in enumerate(bufs)])
+    act = host(sw.process(stream))
+    npk = -(-n // V)
+    done = np.nonzero(act == orc.ACT_FWD_AGG)[0]
+    assert len(done) == npk and (done >= (W - 1) * npk).all()
+    f, vals = o.unpack_nga(stream[torch.from_numpy(done).to(DEV)], V)
+    order = np.argsort(host(f["frag_id"]))
+    got = host(vals).reshape(npk, V)[order].reshape(-1)[:n]
+    assert np.array_equal(got, host(o.sum_reduce([dev(b) for b in bufs])))

@@ -1,0 +1,41 @@
+#!/bin/bash
+# GPU-box session: parity tests -> bench -> rocprofv3 kernel trace -> PMC passes.
+# Every GPU step has its own time limit; the script stops at the first crash,
+# abort or timeout (only an ordinary pytest failure, rc 1, lets it continue).
+# usage: tools/gpu_session.sh TAG [stages...]   stages: test bench prof pmc extra smoke
+set -u
+TAG=${1:-r01}; shift || true
+STAGES=${*:-"smoke test bench prof pmc extra"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { echo "STOP after $1 (rc=$2)"; exit "$2"; }
+ok_or_fail() { local rc=$2; if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then fatal "$1" "$rc"; fi; }
+for st in $STAGES; do
+  case $st in
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      rc=$?; tail -3 "$OUT/smoke.log"; [ $rc -ne 0 ] && fatal smoke $rc ;;
+    test)
+      timeout -k 10 1000 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
+      rc=$?; tail -25 "$OUT/pytest_gpu.log"; ok_or_fail pytest $rc ;;
+    bench)
+      timeout -k 10 400 python bench.py --steps 50 --warmup 10 > "$OUT/bench.json" 2> "$OUT/bench.err"
+      rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -ne 0 ] && fatal bench $rc ;;
+    prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+      rc=$?; tail -2 "$OUT/prof.err"; [ $rc -ne 0 ] && fatal prof $rc ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o run -- \
+          python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
+        rc=$?; tail -2 "$OUT/pmc_$c.err"; [ $rc -ne 0 ] && fatal "pmc $c" $rc
+      done ;;
+    extra)
+      timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extra > "$OUT/extra_bench.json" 2> "$OUT/extra.err"
+      rc=$?; tail -3 "$OUT/extra.err"; [ $rc -ne 0 ] && fatal extra $rc
+      cp gpurun_out/bench_extra.json "$OUT/" ;;
+  esac
+done
+echo "session $TAG done"
