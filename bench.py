@@ -195,7 +195,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "k_sum_reduce_i32_vec<8,2,nt>",
+                     "kernel": "ina::k_sum_reduce_i32_vec<8,4,true> (512 x 256 threads)",
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "avg_launch_us": round(avg_launch_s * 1e6, 2)},
         "parity_spot_check": parity,

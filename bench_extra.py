@@ -55,12 +55,12 @@ def run_extra(dev):
     sweep = []
     for nt in (True, False):
         for unroll in (1, 2, 4):
-            for blocks in (512, 1024, 2048, 4096, 8192, 1 << 20):
-                ops.set_tuning(max_blocks=blocks, unroll=unroll, nontemporal=nt)
+            for blocks in (256, 512, 1024, 2048):
+                ops.set_tuning(reduce_blocks=blocks, unroll=unroll, nontemporal=nt)
                 t = _time(lambda: ops.sum_reduce(b3, out=o3))
                 sweep.append(_row("sum_reduce_i32 W=8", t, (W3 + 1) * n3 * 4, nt=nt, unroll=unroll,
                                   max_blocks=blocks))
-    ops.set_tuning(max_blocks=2048, unroll=2, nontemporal=True)
+    ops.set_tuning(reduce_blocks=512, unroll=4, nontemporal=True)
     rows.append(max(sweep, key=lambda r: r["GB/s"]) | {"note": "best of sweep"})
     for W in (2, 4, 16):
         bw = [rnd_i32(n3) for _ in range(W)] if W != 16 else b3 + [rnd_i32(n3) for _ in range(8)]

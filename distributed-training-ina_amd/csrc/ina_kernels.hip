@@ -53,13 +53,16 @@ static int check_launch(const char* what) {
 // tuning (grid cap / unroll), overridable for sweeps through ina_set_tuning()
 // ---------------------------------------------------------------------------
 static std::atomic<int> g_max_blocks{2048};   // 8 workgroups x 256 CUs
-static std::atomic<int> g_unroll{2};
+// sum-reduce: measured best on MI355X (tools/lab/reduce_lab.py, interleaved A/B):
+// 512 x 256-thread workgroups (2 per CU), 4 x 16 B per worker per thread in flight
+static std::atomic<int> g_reduce_blocks{512};
+static std::atomic<int> g_unroll{4};
 static std::atomic<int> g_nontemporal{1};
 
-static inline unsigned grid_for(size_t work_items, int per_thread) {
+static inline unsigned grid_for(size_t work_items, int per_thread, int cap_override = 0) {
     size_t per_block = (size_t)kBlock * (size_t)per_thread;
     size_t blocks = (work_items + per_block - 1) / per_block;
-    size_t cap = (size_t)g_max_blocks.load();
+    size_t cap = (size_t)(cap_override > 0 ? cap_override : g_max_blocks.load());
     if (blocks > cap) blocks = cap;
     if (blocks == 0) blocks = 1;
     return (unsigned)blocks;
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_scalar(PtrPack<int32_
 template <int W, int U>
 static void launch_reduce_w(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
                             hipStream_t s) {
-    unsigned g = grid_for(n4, U);
+    unsigned g = grid_for(n4, U, g_reduce_blocks.load());
     if (g_nontemporal.load())
         hipLaunchKernelGGL((k_sum_reduce_i32_vec<W, U, true>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
     else
@@ -228,8 +231,8 @@ static void launch_reduce_u(const PtrPack<int32_t>& pk, int32_t* out, size_t n4,
                             hipStream_t s) {
     switch (g_unroll.load()) {
         case 1: launch_reduce_w<W, 1>(pk, out, n4, n, s); break;
-        case 4: launch_reduce_w<W, 4>(pk, out, n4, n, s); break;
-        default: launch_reduce_w<W, 2>(pk, out, n4, n, s); break;
+        case 2: launch_reduce_w<W, 2>(pk, out, n4, n, s); break;
+        default: launch_reduce_w<W, 4>(pk, out, n4, n, s); break;
     }
 }
 
@@ -505,6 +508,21 @@ __global__ __launch_bounds__(kBlock) void k_ps_apply_i32(const float* __restrict
     }
 }
 
+// INA form: out = local + ws * ((float)sum_w q(paras[w] - local) * 2^-k), one pass
+__global__ __launch_bounds__(kBlock) void k_ps_combine_ina(const float* __restrict__ local,
+                                                           PtrPack<float> paras, int W, float s,
+                                                           float inv, float ws,
+                                                           float* __restrict__ out, size_t n) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        float l = local[i];
+        uint32_t acc = 0;
+        for (int w = 0; w < W; ++w) acc += (uint32_t)q32(__fsub_rn(paras.p[w][i], l), s);
+        float y = __fmul_rn((float)(int32_t)acc, inv);
+        out[i] = __fadd_rn(l, __fmul_rn(y, ws));
+    }
+}
+
 // ===========================================================================
 // 5. NGA-V packets (15-byte BE header, V BE words, zero tail)
 // ===========================================================================
@@ -747,6 +765,7 @@ int ina_set_tuning(int key, int value) {
         case 0: if (value < 1) return INA_EINVAL; g_max_blocks = value; return INA_OK;
         case 1: if (value != 1 && value != 2 && value != 4) return INA_EINVAL; g_unroll = value; return INA_OK;
         case 2: g_nontemporal = value ? 1 : 0; return INA_OK;
+        case 3: if (value < 1) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
         default: return INA_EINVAL;
     }
 }
@@ -921,6 +940,19 @@ int ina_ps_apply_i32(const float* local, const int32_t* sum_int, int k, double w
     hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), local,
                        sum_int, ldexpf(1.0f, -k), (float)weight_step, out, n);
     return check_launch("ps_apply_i32");
+}
+
+int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W, int k,
+                           double weight_step, float* out, size_t n, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n == 0) return INA_OK;
+    PtrPack<float> pk;
+    bool al;
+    if (int rc = fill_pack(pk, paras, W, al)) return rc;
+    if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
+    hipLaunchKernelGGL(k_ps_combine_ina, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), local, pk,
+                       W, ldexpf(1.0f, k), ldexpf(1.0f, -k), (float)weight_step, out, n);
+    return check_launch("ps_combine_ina_f32");
 }
 
 int ina_pack_nga(const int32_t* vals, size_t n, const ina_nga_params_t* prm, const uint8_t* ovf,

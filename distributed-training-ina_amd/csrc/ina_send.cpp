@@ -80,6 +80,14 @@ int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num
         hipStreamSynchronize(s) != hipSuccess)
         return ina::set_error(INA_EHIP, "D2H packet copy%s", "");
 
+    return ina_send_packets_fd(fd, g_stage.h_pkts, npk, INA_C128_BYTES, INA_C128_BYTES, dst_ip);
+}
+
+int ina_send_packets_fd(int fd, const uint8_t* host_pkts, size_t npk, size_t stride,
+                        size_t pkt_len, uint32_t dst_ip) {
+    if (npk == 0) return 0;
+    if (!host_pkts || pkt_len == 0 || stride < pkt_len)
+        return ina::set_error(INA_EINVAL, "bad packet buffer%s", "");
     sockaddr_in dst;
     memset(&dst, 0, sizeof dst);
     dst.sin_family = AF_INET;
@@ -91,8 +99,8 @@ int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num
     while (sent < npk) {
         size_t nb = npk - sent < kBatch ? npk - sent : kBatch;
         for (size_t i = 0; i < nb; ++i) {
-            iov[i].iov_base = g_stage.h_pkts + (sent + i) * INA_C128_BYTES;
-            iov[i].iov_len = INA_C128_BYTES;
+            iov[i].iov_base = const_cast<uint8_t*>(host_pkts) + (sent + i) * stride;
+            iov[i].iov_len = pkt_len;
             memset(&msgs[i], 0, sizeof(mmsghdr));
             msgs[i].msg_hdr.msg_iov = &iov[i];
             msgs[i].msg_hdr.msg_iovlen = 1;
@@ -108,6 +116,7 @@ int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num
         }
         sent += (size_t)r;
     }
+    if (sent > 0x7FFFFFFFu) sent = 0x7FFFFFFFu;
     return (int)sent;
 }
 

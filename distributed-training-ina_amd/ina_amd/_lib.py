@@ -60,6 +60,7 @@ SIGNATURES = {
     "ina_quantize_reduce_f32_i16_sat": [_vp, _i, _vp, _sz, _i, _i, _vp, _vp],
     "ina_ps_combine_f32": [_vp, _vp, _i, _d, _vp, _sz, _vp],
     "ina_ps_apply_i32": [_vp, _vp, _i, _d, _vp, _sz, _vp],
+    "ina_ps_combine_ina_f32": [_vp, _vp, _i, _i, _d, _vp, _sz, _vp],
     "ina_pack_nga": [_vp, _sz, C.POINTER(NgaParams), _vp, _vp, _sz, _vp],
     "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
@@ -68,6 +69,7 @@ SIGNATURES = {
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],
     "send_gradients": [C.POINTER(C.c_uint32), _i, _u32, _i, _u32, _i],
     "ina_send_gradients_fd": [_i, _vp, _i, _u32, _i, _u32, _i],
+    "ina_send_packets_fd": [_i, _vp, _sz, _sz, _sz, _u32],
 }
 _RESTYPE = {"ina_version": C.c_char_p, "ina_last_error_string": C.c_char_p,
             "ina_switch_scratch_bytes": C.c_size_t, "send_gradients": None}

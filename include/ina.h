@@ -101,6 +101,12 @@ int ina_ps_combine_f32(const float* local, const float* const* paras, int W, dou
 int ina_ps_apply_i32(const float* local, const int32_t* sum_int, int k, double weight_step,
                      float* out, size_t n, ina_stream_t stream);
 
+/* INA-semantics update in one pass (what the switch path computes end to end):
+ * out = local + float(weight_step) * ((float)(sum_w q(paras[w] - local)) * 2^-k),
+ * q = the quantiser above, integer sum mod 2^32. */
+int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W, int k,
+                           double weight_step, float* out, size_t n, ina_stream_t stream);
+
 /* ---- packets ------------------------------------------------------------------- */
 typedef struct ina_nga_params {
     uint32_t bitmap;    /* header word 0; DataManager passes worker_id raw (DataManager.py:124) */
@@ -176,6 +182,14 @@ void send_gradients(uint32_t* gradient_array, int packet_num, uint32_t dst_ip, i
 int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num,
                           uint32_t dst_ip, int worker_id, uint32_t aggregator_index,
                           int tensor_index);
+
+/* Batched datagram egress for packets already in HOST memory (e.g. copied back
+ * from ina_pack_nga): sends npkts datagrams of pkt_len bytes found at `stride`
+ * apart with sendmmsg() on fd (to dst_ip, host order, when != 0).  Replaces the
+ * per-packet sendto() loops of DataManager.py:134,153 and communicator.cc:37.
+ * Returns packets sent or INA_E*. */
+int ina_send_packets_fd(int fd, const uint8_t* host_pkts, size_t npkts, size_t stride,
+                        size_t pkt_len, uint32_t dst_ip);
 
 #ifdef __cplusplus
 }

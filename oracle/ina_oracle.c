@@ -200,6 +200,25 @@ int orc_ps_combine_f32(const float* local, const float* const* paras, int W,
     return 0;
 }
 
+/* INA form of the same update (build-defined: the reference never wires its
+ * quantiser into aggregate()): workers quantise their deltas d_w = p_w - local,
+ * the switch sums the integers mod 2^32, the PS dequantises and applies
+ * out = local + float(w*step) * ((float)sum * 2^-k). */
+int orc_ps_combine_ina_f32(const float* local, const float* const* paras, int W, int k,
+                           double weight_step, float* out, size_t n) {
+    if (W <= 0 || k < -126 || k > 127) return ORC_EINVAL;
+    float s = pow2f(k), inv = pow2f(-k), ws = (float)weight_step;
+    for (size_t i = 0; i < n; ++i) {
+        float l = local[i];
+        uint32_t acc = 0;
+        for (int w = 0; w < W; ++w) acc += (uint32_t)orc_q_i32(paras[w][i] - l, s);
+        float y = (float)(int32_t)acc * inv;
+        float t = y * ws;
+        out[i] = l + t;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------- */
 /* a3: NGA-V packetiser.  DataManager._send_data (DataManager.py:111-165):     */
 /*   header struct.pack('!IbbIbI', worker_id, degree, 0, seq%16384, switch_id, */

@@ -74,6 +74,8 @@ int orc_quantize_reduce_f32_i16_sat(const float* const* bufs, int W, int16_t* ou
                                     int k, int V, uint8_t* ovf);
 int orc_ps_combine_f32(const float* local, const float* const* paras, int W,
                        double weight_step, float* out, size_t n);
+int orc_ps_combine_ina_f32(const float* local, const float* const* paras, int W, int k,
+                           double weight_step, float* out, size_t n);
 void orc_nga_write_header(uint8_t* p, uint32_t bitmap, uint8_t count, uint8_t flags,
                           uint32_t index, uint8_t switch_id, uint32_t frag_id);
 int orc_pack_nga(const int32_t* vals, size_t n, const orc_nga_params_t* prm, const uint8_t* ovf,

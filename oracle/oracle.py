@@ -74,6 +74,7 @@ def lib():
             "orc_quantize_reduce_f32_i32": [vp, i, vp, sz, i],
             "orc_quantize_reduce_f32_i16_sat": [vp, i, vp, sz, i, i, vp],
             "orc_ps_combine_f32": [vp, vp, i, C.c_double, vp, sz],
+            "orc_ps_combine_ina_f32": [vp, vp, i, i, C.c_double, vp, sz],
             "orc_pack_nga": [vp, sz, C.POINTER(NgaParams), vp, vp, sz],
             "orc_unpack_nga": [vp, sz, i, sz, C.POINTER(NgaFields), vp],
             "orc_pack_c128": [vp, i, i, u32, i, vp],
@@ -182,6 +183,15 @@ def ps_combine_f32(local: np.ndarray, paras, weight_step: float) -> np.ndarray:
     out = np.empty_like(local)
     _chk(lib().orc_ps_combine_f32(_p(local), _ptr_array(paras), len(paras), float(weight_step),
                                   _p(out), local.size))
+    return out
+
+
+def ps_combine_ina_f32(local: np.ndarray, paras, k: int, weight_step: float) -> np.ndarray:
+    local = np.ascontiguousarray(local, np.float32)
+    paras = [np.ascontiguousarray(p, np.float32) for p in paras]
+    out = np.empty_like(local)
+    _chk(lib().orc_ps_combine_ina_f32(_p(local), _ptr_array(paras), len(paras), k,
+                                      float(weight_step), _p(out), local.size))
     return out
 
 
