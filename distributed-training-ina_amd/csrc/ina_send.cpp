@@ -92,6 +92,11 @@ int ina_send_packets_fd(int fd, const uint8_t* host_pkts, size_t npk, size_t str
     memset(&dst, 0, sizeof dst);
     dst.sin_family = AF_INET;
     dst.sin_addr.s_addr = htonl(dst_ip);   // communicator.cc:8 (host-order argument)
+    // an IPv4 destination only means something on an AF_INET socket (a connected or
+    // AF_UNIX datagram socket, e.g. a capture socketpair, takes no address)
+    int domain = AF_INET;
+    socklen_t dl = sizeof domain;
+    if (getsockopt(fd, SOL_SOCKET, SO_DOMAIN, &domain, &dl) == 0 && domain != AF_INET) dst_ip = 0;
     constexpr size_t kBatch = 1024;
     std::vector<mmsghdr> msgs(kBatch);
     std::vector<iovec> iov(kBatch);
