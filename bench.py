@@ -52,18 +52,30 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 22,
                     help="values per worker in the bounded CPU-baseline sample")
     ap.add_argument("--extra", action="store_true")
+    ap.add_argument("--mode", choices=("reduce", "sharded"), default="reduce",
+                    help="reduce: the headline (config 3); sharded: config 5, one 1 GiB fp32 "
+                         "bucket per rank aggregated with quantise -> RCCL reduce-scatter -> "
+                         "dequantise -> all-gather")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_sum_reduce_c3.json"))
     return ap.parse_args()
+
+
+BACKEND = os.environ.get("INA_BENCH_BACKEND", "nccl")   # "gloo": rehearse N>1 on one GPU
 
 
 def init_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if BACKEND == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(BACKEND)
     return rank, world, local
 
 
@@ -78,7 +90,7 @@ def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if BACKEND == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -134,11 +146,51 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
     }
 
 
+def run_sharded(args, rank, world, dev):
+    """Config 5: every rank is one worker with an n-value fp32 bucket (default 1 GiB)."""
+    from ina_amd.dist import ShardedAggregator
+    n = args.values if args.values != N_VALUES else 268_435_456
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    bucket = torch.randn(n, device=dev, generator=g) * 1e-2
+    agg = ShardedAggregator(n, k=16, device=dev)
+    for _ in range(args.warmup):
+        agg(bucket)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        agg(bucket)
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    shard_bytes = agg.plan.shard * 4
+    return {
+        "metric": "aggregated-gradient GB/s (config 5: 1 GiB fp32 bucket per rank, sharded RCCL)",
+        "value": round(world * n * 4 * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": "C5: 1 GiB fp32 bucket per worker, quantise k=16 -> "
+                               "reduce_scatter(int32,SUM) -> dequantise -> all_gather(fp32)",
+                   "values_per_worker": n, "workers": world, "shard_values": agg.plan.shard,
+                   "parallelism": f"RCCL x {world}"},
+        "xgmi": {"rs_bytes_per_rank": (world - 1) * shard_bytes,
+                 "ag_bytes_per_rank": (world - 1) * shard_bytes},
+    }
+
+
 def main():
     args = parse()
     rank, world, local = init_dist(args)
     dev = torch.device(f"cuda:{local}")
     from ina_amd import ops
+    if args.mode == "sharded":
+        line = run_sharded(args, rank, world, dev)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
 
     W, n = args.workers, args.values
     sets = [make_inputs(W, n, 1000 + 100 * (rank * ROTATE + r), dev) for r in range(ROTATE)]

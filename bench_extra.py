@@ -36,9 +36,27 @@ def _row(name, secs, nbytes, **kw):
     return r
 
 
+DEFAULTS = {"max_blocks": 2048, "reduce_blocks": 512, "stream_blocks": 1024}
+
+
+def _sweep(ops, rows, sweeps, name, knob, values, fn, nbytes):
+    """Time fn at each grid cap of one knob; keep all points, restore the default."""
+    best = None
+    for v in values:
+        ops.set_tuning(**{knob: v})
+        r = _row(name, _time(fn), nbytes, **{knob: v})
+        sweeps.append(r)
+        best = r if best is None or r["GB/s"] > best["GB/s"] else best
+    ops.set_tuning(**{knob: DEFAULTS[knob]})
+    r = _row(name, _time(fn), nbytes, note=f"default {knob}={DEFAULTS[knob]}")
+    r["best_of_sweep"] = {knob: best[knob], "GB/s": best["GB/s"]}
+    rows.append(r)
+
+
 def run_extra(dev):
     from ina_amd import ops
     rows = []
+    gsweep = []
     gen = torch.Generator(device=dev)
     gen.manual_seed(7)
 
@@ -71,28 +89,34 @@ def run_extra(dev):
     # --- quantise / dequantise ------------------------------------------------------------
     x = rnd_f32(n3)
     q = torch.empty(n3, dtype=torch.int32, device=dev)
-    rows.append(_row("quantize_f32_i32", _time(lambda: ops.quantize(x, 16, out=q)), 8 * n3))
+    _sweep(ops, rows, gsweep, "quantize_f32_i32", "stream_blocks", (512, 1024, 2048, 4096),
+           lambda: ops.quantize(x, 16, out=q), 8 * n3)
     y = torch.empty(n3, dtype=torch.float32, device=dev)
-    rows.append(_row("dequantize_i32_f32", _time(lambda: ops.dequantize(q, 16, out=y)), 8 * n3))
+    _sweep(ops, rows, gsweep, "dequantize_i32_f32", "stream_blocks", (512, 1024, 2048, 4096),
+           lambda: ops.dequantize(q, 16, out=y), 8 * n3)
 
     # --- config 2: fused quantise + reduce, 4 x ResNet-50 fp32 -----------------------------
     n2 = 25_557_032
     b2 = [rnd_f32(n2) for _ in range(4)]
     o2 = torch.empty(n2, dtype=torch.int32, device=dev)
-    rows.append(_row("quantize_reduce_f32_i32 W=4 (C2)",
-                     _time(lambda: ops.quantize_reduce(b2, 16, out=o2)), (4 * 4 + 4) * n2))
+    _sweep(ops, rows, gsweep, "quantize_reduce_f32_i32 W=4 (C2)", "reduce_blocks",
+           (256, 512, 1024, 2048), lambda: ops.quantize_reduce(b2, 16, out=o2), (4 * 4 + 4) * n2)
     # --- config 4: int16 saturating, 16 workers --------------------------------------------
     b4 = b2 + [rnd_f32(n2) for _ in range(12)]
     o4 = torch.empty(n2, dtype=torch.int16, device=dev)
     f4 = torch.empty((n2 + 255) // 256, dtype=torch.uint8, device=dev)
-    rows.append(_row("quantize_reduce_f32_i16 W=16 V=256 (C4)",
-                     _time(lambda: ops.quantize_reduce_i16(b4, 12, 256, out=o4, overflow=f4)),
-                     (16 * 4 + 2) * n2 + f4.numel()))
+    _sweep(ops, rows, gsweep, "quantize_reduce_f32_i16 W=16 V=256 (C4)", "max_blocks",
+           (512, 1024, 2048, 4096),
+           lambda: ops.quantize_reduce_i16(b4, 13, 256, out=o4, overflow=f4),
+           (16 * 4 + 2) * n2 + f4.numel())
     # --- PS combine (launch.py:42-52), W=4 ---------------------------------------------------
     local = rnd_f32(n2, 1.0)
     oc = torch.empty_like(local)
-    rows.append(_row("ps_combine_f32 W=4", _time(lambda: ops.ps_combine(local, b2[:4], 0.2, out=oc)),
-                     (4 + 2) * 4 * n2))
+    _sweep(ops, rows, gsweep, "ps_combine_f32 W=4", "reduce_blocks", (256, 512, 1024, 2048),
+           lambda: ops.ps_combine(local, b2[:4], 0.2, out=oc), (4 + 2) * 4 * n2)
+    from ina_amd import ps as ps_mod
+    _sweep(ops, rows, gsweep, "ps_combine_ina_f32 W=4", "reduce_blocks", (256, 512, 1024, 2048),
+           lambda: ps_mod.combine_ina(local, b2[:4], 16, 0.2, out=oc), (4 + 2) * 4 * n2)
     del b4, b2, local, oc, o4
 
     # --- packets, V = 256 over the C3 aggregate ------------------------------------------------
@@ -137,4 +161,4 @@ def run_extra(dev):
     t = _time(e2e, reps=5, warm=1)
     rows.append(_row("end-to-end pinned H2D(8x100MiB)+reduce+D2H", t, (W3 + 1) * n3 * 4,
                      aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2)))
-    return {"rows": rows, "sweep": sweep}
+    return {"rows": rows, "sweep": sweep, "grid_sweeps": gsweep}

@@ -57,6 +57,8 @@ static std::atomic<int> g_max_blocks{2048};   // 8 workgroups x 256 CUs
 // 512 x 256-thread workgroups (2 per CU), 4 x 16 B per worker per thread in flight
 static std::atomic<int> g_reduce_blocks{512};
 static std::atomic<int> g_unroll{4};
+// the other chunk_loop<4> streaming kernels
+static std::atomic<int> g_stream_blocks{1024};
 static std::atomic<int> g_nontemporal{1};
 
 static inline unsigned grid_for(size_t work_items, int per_thread, int cap_override = 0) {
@@ -133,6 +135,22 @@ static inline bool slot_ballot_ok(int V) {
     if (V % 8) return false;
     int l = V / 8;
     return l >= 1 && l <= 64 && (l & (l - 1)) == 0;
+}
+
+
+template <int W>
+constexpr int kUnrW = W > 0 ? W : 1;
+
+// Grid-stride loop over 16-byte chunks with UU independent chunks per thread per
+// iteration (chunks i, i+stride, ..., all loads issued before use), then a 1-chunk
+// remainder loop: the geometry the reduce lab measured fastest (tools/lab).
+template <int U, typename Body>
+__device__ __forceinline__ void chunk_loop(size_t n4, Body&& body) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    size_t i = tid;
+    for (; i + (U - 1) * stride < n4; i += U * stride) body.template operator()<U>(i, stride);
+    for (; i < n4; i += stride) body.template operator()<1>(i, stride);
 }
 
 // ===========================================================================
@@ -242,17 +260,24 @@ static void launch_reduce_u(const PtrPack<int32_t>& pk, int32_t* out, size_t n4,
 __global__ __launch_bounds__(kBlock) void k_quantize_i32(const float* __restrict__ x,
                                                          int32_t* __restrict__ q, size_t n,
                                                          float s, int vec) {
-    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const size_t stride = (size_t)gridDim.x * kBlock;
     size_t n4 = vec ? n / 4 : 0;
-    for (size_t i = tid; i < n4; i += stride) {
-        f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x) + i);
-        u32x4 r;
-        r.x = (uint32_t)q32(v.x, s); r.y = (uint32_t)q32(v.y, s);
-        r.z = (uint32_t)q32(v.z, s); r.w = (uint32_t)q32(v.w, s);
-        __builtin_nontemporal_store(r, reinterpret_cast<u32x4*>(q) + i);
-    }
-    for (size_t i = 4 * n4 + tid; i < n; i += stride) q[i] = q32(x[i], s);
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+    u32x4* q4 = reinterpret_cast<u32x4*>(q);
+    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+        f32x4 v[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) v[u] = __builtin_nontemporal_load(x4 + i + u * st);
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            u32x4 r;
+            r.x = (uint32_t)q32(v[u].x, s); r.y = (uint32_t)q32(v[u].y, s);
+            r.z = (uint32_t)q32(v[u].z, s); r.w = (uint32_t)q32(v[u].w, s);
+            __builtin_nontemporal_store(r, q4 + i + u * st);
+        }
+    });
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        q[i] = q32(x[i], s);
 }
 
 // int16: thread owns 8 values (two float4 loads, one 16-byte store)
@@ -308,17 +333,24 @@ __global__ __launch_bounds__(kBlock) void k_quantize_i16_scalar(const float* __r
 __global__ __launch_bounds__(kBlock) void k_dequantize_i32(const int32_t* __restrict__ sv,
                                                            float* __restrict__ y, size_t n,
                                                            float inv, int vec) {
-    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const size_t stride = (size_t)gridDim.x * kBlock;
     size_t n4 = vec ? n / 4 : 0;
-    for (size_t i = tid; i < n4; i += stride) {
-        u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sv) + i);
-        f32x4 r;
-        r.x = (float)(int32_t)v.x * inv; r.y = (float)(int32_t)v.y * inv;
-        r.z = (float)(int32_t)v.z * inv; r.w = (float)(int32_t)v.w * inv;
-        __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(y) + i);
-    }
-    for (size_t i = 4 * n4 + tid; i < n; i += stride) y[i] = (float)sv[i] * inv;
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(sv);
+    f32x4* y4 = reinterpret_cast<f32x4*>(y);
+    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+        u32x4 v[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) v[u] = __builtin_nontemporal_load(s4 + i + u * st);
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            f32x4 r;
+            r.x = (float)(int32_t)v[u].x * inv; r.y = (float)(int32_t)v[u].y * inv;
+            r.z = (float)(int32_t)v[u].z * inv; r.w = (float)(int32_t)v[u].w * inv;
+            __builtin_nontemporal_store(r, y4 + i + u * st);
+        }
+    });
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        y[i] = (float)sv[i] * inv;
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequantize_i16(const int16_t* __restrict__ sv,
@@ -333,30 +365,45 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_i16(const int16_t* __rest
 // 3. fused quantise + reduce (configs 2 and 4) and the int16 narrow reduce
 // ===========================================================================
 template <int W>
-__device__ __forceinline__ u32x4 quant_sum4(const PtrPack<float>& in, int Wd, size_t i, float s) {
-    constexpr int UNR = W > 0 ? W : 1;
-    u32x4 acc = {0u, 0u, 0u, 0u};
-    const int nw = W > 0 ? W : Wd;
-#pragma unroll UNR
-    for (int w = 0; w < nw; ++w) {
-        f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w]) + i);
-        acc.x += (uint32_t)q32(v.x, s); acc.y += (uint32_t)q32(v.y, s);
-        acc.z += (uint32_t)q32(v.z, s); acc.w += (uint32_t)q32(v.w, s);
-    }
-    return acc;
-}
-
-template <int W>
 __global__ __launch_bounds__(kBlock) void k_quant_reduce_i32(PtrPack<float> in, int Wd,
                                                              int32_t* __restrict__ out,
                                                              size_t n, float s, int vec) {
-    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const size_t stride = (size_t)gridDim.x * kBlock;
     const int nw = W > 0 ? W : Wd;
     size_t n4 = vec ? n / 4 : 0;
-    for (size_t i = tid; i < n4; i += stride)
-        __builtin_nontemporal_store(quant_sum4<W>(in, Wd, i, s), reinterpret_cast<u32x4*>(out) + i);
-    for (size_t i = 4 * n4 + tid; i < n; i += stride) {
+    u32x4* o4 = reinterpret_cast<u32x4*>(out);
+    if constexpr (W > 0) {
+        chunk_loop<(W <= 8 ? 4 : 2)>(n4, [&]<int UU>(size_t i, size_t st) {
+            f32x4 v[W][UU];
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+#pragma unroll
+                for (int u = 0; u < UU; ++u)
+                    v[w][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w]) + i + u * st);
+#pragma unroll
+            for (int u = 0; u < UU; ++u) {
+                u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    acc.x += (uint32_t)q32(v[w][u].x, s); acc.y += (uint32_t)q32(v[w][u].y, s);
+                    acc.z += (uint32_t)q32(v[w][u].z, s); acc.w += (uint32_t)q32(v[w][u].w, s);
+                }
+                __builtin_nontemporal_store(acc, o4 + i + u * st);
+            }
+        });
+    } else {
+        const size_t stride = (size_t)gridDim.x * kBlock;
+        for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
+            u32x4 acc = {0u, 0u, 0u, 0u};
+            for (int w = 0; w < nw; ++w) {
+                f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w]) + i);
+                acc.x += (uint32_t)q32(v.x, s); acc.y += (uint32_t)q32(v.y, s);
+                acc.z += (uint32_t)q32(v.z, s); acc.w += (uint32_t)q32(v.w, s);
+            }
+            __builtin_nontemporal_store(acc, o4 + i);
+        }
+    }
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         uint32_t a = 0;
         for (int w = 0; w < nw; ++w) a += (uint32_t)q32(in.p[w][i], s);
         out[i] = (int32_t)a;
@@ -485,14 +532,47 @@ __global__ __launch_bounds__(kBlock) void k_sum_reduce_i16_scalar(PtrPack<int16_
 // 4. PS combine (launch.py:42-52), bit-exact fp32 op sequence; built with
 //    -ffp-contract=off so no FMA fuses the sub/add/mul.
 // ===========================================================================
+// W-templated (0 = runtime W) fp32 combine over float4 chunks
+template <int W>
 __global__ __launch_bounds__(kBlock) void k_ps_combine_f32(const float* __restrict__ local,
-                                                           PtrPack<float> paras, int W, float ws,
-                                                           float* __restrict__ out, size_t n) {
+                                                           PtrPack<float> paras, int Wd, float ws,
+                                                           float* __restrict__ out, size_t n,
+                                                           int vec) {
+    const int nw = W > 0 ? W : Wd;
+    size_t n4 = vec ? n / 4 : 0;
+    const f32x4* l4 = reinterpret_cast<const f32x4*>(local);
+    f32x4* o4 = reinterpret_cast<f32x4*>(out);
+    chunk_loop<(W > 0 && W <= 4) ? 4 : 2>(n4, [&]<int UU>(size_t i, size_t st) {
+        f32x4 l[UU], acc[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) { l[u] = l4[i + u * st]; acc[u] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll kUnrW<W>
+        for (int w = 0; w < nw; ++w) {
+            f32x4 p[UU];
+#pragma unroll
+            for (int u = 0; u < UU; ++u)
+                p[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(paras.p[w]) + i + u * st);
+#pragma unroll
+            for (int u = 0; u < UU; ++u) {       // python sum(): 0 + d_0 + d_1 + ...
+                acc[u].x = __fadd_rn(acc[u].x, __fsub_rn(p[u].x, l[u].x));
+                acc[u].y = __fadd_rn(acc[u].y, __fsub_rn(p[u].y, l[u].y));
+                acc[u].z = __fadd_rn(acc[u].z, __fsub_rn(p[u].z, l[u].z));
+                acc[u].w = __fadd_rn(acc[u].w, __fsub_rn(p[u].w, l[u].w));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            f32x4 r;
+            r.x = __fadd_rn(l[u].x, __fmul_rn(acc[u].x, ws)); r.y = __fadd_rn(l[u].y, __fmul_rn(acc[u].y, ws));
+            r.z = __fadd_rn(l[u].z, __fmul_rn(acc[u].z, ws)); r.w = __fadd_rn(l[u].w, __fmul_rn(acc[u].w, ws));
+            o4[i + u * st] = r;
+        }
+    });
     const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         float l = local[i];
-        float acc = 0.0f;                      // python sum() starts at int 0
-        for (int w = 0; w < W; ++w) acc = __fadd_rn(acc, __fsub_rn(paras.p[w][i], l));
+        float acc = 0.0f;
+        for (int w = 0; w < nw; ++w) acc = __fadd_rn(acc, __fsub_rn(paras.p[w][i], l));
         out[i] = __fadd_rn(l, __fmul_rn(acc, ws));
     }
 }
@@ -500,24 +580,79 @@ __global__ __launch_bounds__(kBlock) void k_ps_combine_f32(const float* __restri
 __global__ __launch_bounds__(kBlock) void k_ps_apply_i32(const float* __restrict__ local,
                                                          const int32_t* __restrict__ sum,
                                                          float inv, float ws,
-                                                         float* __restrict__ out, size_t n) {
+                                                         float* __restrict__ out, size_t n, int vec) {
+    size_t n4 = vec ? n / 4 : 0;
+    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+        f32x4 l[UU];
+        u32x4 q[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            l[u] = reinterpret_cast<const f32x4*>(local)[i + u * st];
+            q[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sum) + i + u * st);
+        }
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            f32x4 r;
+            r.x = __fadd_rn(l[u].x, __fmul_rn(__fmul_rn((float)(int32_t)q[u].x, inv), ws));
+            r.y = __fadd_rn(l[u].y, __fmul_rn(__fmul_rn((float)(int32_t)q[u].y, inv), ws));
+            r.z = __fadd_rn(l[u].z, __fmul_rn(__fmul_rn((float)(int32_t)q[u].z, inv), ws));
+            r.w = __fadd_rn(l[u].w, __fmul_rn(__fmul_rn((float)(int32_t)q[u].w, inv), ws));
+            reinterpret_cast<f32x4*>(out)[i + u * st] = r;
+        }
+    });
     const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         float d = __fmul_rn((float)sum[i], inv);
         out[i] = __fadd_rn(local[i], __fmul_rn(d, ws));
     }
 }
 
 // INA form: out = local + ws * ((float)sum_w q(paras[w] - local) * 2^-k), one pass
+template <int W>
 __global__ __launch_bounds__(kBlock) void k_ps_combine_ina(const float* __restrict__ local,
-                                                           PtrPack<float> paras, int W, float s,
+                                                           PtrPack<float> paras, int Wd, float s,
                                                            float inv, float ws,
-                                                           float* __restrict__ out, size_t n) {
+                                                           float* __restrict__ out, size_t n,
+                                                           int vec) {
+    const int nw = W > 0 ? W : Wd;
+    size_t n4 = vec ? n / 4 : 0;
+    chunk_loop<(W > 0 && W <= 4) ? 4 : 2>(n4, [&]<int UU>(size_t i, size_t st) {
+        f32x4 l[UU];
+        u32x4 acc[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            l[u] = reinterpret_cast<const f32x4*>(local)[i + u * st];
+            acc[u] = u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll kUnrW<W>
+        for (int w = 0; w < nw; ++w) {
+            f32x4 p[UU];
+#pragma unroll
+            for (int u = 0; u < UU; ++u)
+                p[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(paras.p[w]) + i + u * st);
+#pragma unroll
+            for (int u = 0; u < UU; ++u) {
+                acc[u].x += (uint32_t)q32(__fsub_rn(p[u].x, l[u].x), s);
+                acc[u].y += (uint32_t)q32(__fsub_rn(p[u].y, l[u].y), s);
+                acc[u].z += (uint32_t)q32(__fsub_rn(p[u].z, l[u].z), s);
+                acc[u].w += (uint32_t)q32(__fsub_rn(p[u].w, l[u].w), s);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            f32x4 r;
+            r.x = __fadd_rn(l[u].x, __fmul_rn(__fmul_rn((float)(int32_t)acc[u].x, inv), ws));
+            r.y = __fadd_rn(l[u].y, __fmul_rn(__fmul_rn((float)(int32_t)acc[u].y, inv), ws));
+            r.z = __fadd_rn(l[u].z, __fmul_rn(__fmul_rn((float)(int32_t)acc[u].z, inv), ws));
+            r.w = __fadd_rn(l[u].w, __fmul_rn(__fmul_rn((float)(int32_t)acc[u].w, inv), ws));
+            reinterpret_cast<f32x4*>(out)[i + u * st] = r;
+        }
+    });
     const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         float l = local[i];
         uint32_t acc = 0;
-        for (int w = 0; w < W; ++w) acc += (uint32_t)q32(__fsub_rn(paras.p[w][i], l), s);
+        for (int w = 0; w < nw; ++w) acc += (uint32_t)q32(__fsub_rn(paras.p[w][i], l), s);
         float y = __fmul_rn((float)(int32_t)acc, inv);
         out[i] = __fadd_rn(l, __fmul_rn(y, ws));
     }
@@ -650,6 +785,42 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_vec(const uint8_t* __rest
     }
 }
 
+// wave-shuffle unpack: L = V/4 lanes per packet (L a power of two <= 64), lane j
+// loads 16-byte chunk j once and takes chunk j+1 from its neighbour (__shfl_down);
+// the packet's last lane loads the tail chunk L itself.
+__global__ __launch_bounds__(kBlock) void k_unpack_nga_shfl(const uint8_t* __restrict__ pkts,
+                                                            size_t npk, int log2L, size_t pstride,
+                                                            NgaFieldsDev f, int32_t* __restrict__ vals) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const uint32_t L = 1u << log2L;
+    const size_t total = npk << log2L;
+    const int lane = threadIdx.x & 63;
+    const size_t wave0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) & ~(size_t)63;
+    for (size_t base = wave0; base < total; base += gs) {
+        const size_t g = base + (size_t)lane;
+        const bool active = g < total;
+        const size_t p = g >> log2L;
+        const uint32_t j = (uint32_t)(g & (L - 1));
+        const uint8_t* pk = pkts + p * pstride;
+        u32x4 a = {0u, 0u, 0u, 0u};
+        if (active) a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk) + j);
+        u32x4 b;
+        b.x = __shfl_down(a.x, 1, 64); b.y = __shfl_down(a.y, 1, 64);
+        b.z = __shfl_down(a.z, 1, 64); b.w = __shfl_down(a.w, 1, 64);
+        if (!active) continue;
+        if (j == L - 1) b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk) + L);
+        if (j == 0) nga_store_header(f, p, a.x, a.y, a.z, a.w);
+        if (vals) {
+            u32x4 o;
+            o.x = bswap(__builtin_amdgcn_alignbyte(b.x, a.w, 3));
+            o.y = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
+            o.z = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
+            o.w = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
+            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(vals) + g);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t be32_at(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
@@ -766,6 +937,7 @@ int ina_set_tuning(int key, int value) {
         case 1: if (value != 1 && value != 2 && value != 4) return INA_EINVAL; g_unroll = value; return INA_OK;
         case 2: g_nontemporal = value ? 1 : 0; return INA_OK;
         case 3: if (value < 1) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
+        case 4: if (value < 1) return INA_EINVAL; g_stream_blocks = value; return INA_OK;
         default: return INA_EINVAL;
     }
 }
@@ -802,7 +974,7 @@ int ina_quantize_f32_i32(const float* x, int32_t* q, size_t n, int k, ina_stream
     if (n == 0) return INA_OK;
     if (!x || !q) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(x) && aligned16(q);
-    hipLaunchKernelGGL(k_quantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 1)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_quantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks)), dim3(kBlock), 0,
                        hs(stream), x, q, n, ldexpf(1.0f, k), vec);
     return check_launch("quantize_i32");
 }
@@ -833,7 +1005,7 @@ int ina_dequantize_i32_f32(const int32_t* sv, float* y, size_t n, int k, ina_str
     if (n == 0) return INA_OK;
     if (!sv || !y) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(sv) && aligned16(y);
-    hipLaunchKernelGGL(k_dequantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 1)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_dequantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks)), dim3(kBlock), 0,
                        hs(stream), sv, y, n, ldexpf(1.0f, -k), vec);
     return check_launch("dequantize_i32");
 }
@@ -879,7 +1051,7 @@ int ina_quantize_reduce_f32_i32(const float* const* bufs, int W, int32_t* out, s
     if (!out) return set_error(INA_EINVAL, "null out%s", "");
     int vec = al && aligned16(out);
     float sc = ldexpf(1.0f, k);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, 1);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_reduce_blocks);
     hipStream_t s = hs(stream);
     switch (W) {
         case 2: hipLaunchKernelGGL(k_quant_reduce_i32<2>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec); break;
@@ -927,8 +1099,16 @@ int ina_ps_combine_f32(const float* local, const float* const* paras, int W, dou
     bool al;
     if (int rc = fill_pack(pk, paras, W, al)) return rc;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
-    hipLaunchKernelGGL(k_ps_combine_f32, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), local, pk,
-                       W, (float)weight_step, out, n);
+    int vec = al && aligned16(local) && aligned16(out);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_reduce_blocks);
+    hipStream_t s = hs(stream);
+    float ws = (float)weight_step;
+    switch (W) {
+#define PSC(WW) case WW: hipLaunchKernelGGL(k_ps_combine_f32<WW>, dim3(g), dim3(kBlock), 0, s, local, pk, W, ws, out, n, vec); break;
+        PSC(1) PSC(2) PSC(3) PSC(4) PSC(5) PSC(6) PSC(7) PSC(8)
+#undef PSC
+        default: hipLaunchKernelGGL(k_ps_combine_f32<0>, dim3(g), dim3(kBlock), 0, s, local, pk, W, ws, out, n, vec);
+    }
     return check_launch("ps_combine_f32");
 }
 
@@ -937,8 +1117,9 @@ int ina_ps_apply_i32(const float* local, const int32_t* sum_int, int k, double w
     if (int rc = check_k(k)) return rc;
     if (n == 0) return INA_OK;
     if (!local || !sum_int || !out) return set_error(INA_EINVAL, "null pointer%s", "");
-    hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), local,
-                       sum_int, ldexpf(1.0f, -k), (float)weight_step, out, n);
+    int vec = aligned16(local) && aligned16(sum_int) && aligned16(out);
+    hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks)), dim3(kBlock), 0,
+                       hs(stream), local, sum_int, ldexpf(1.0f, -k), (float)weight_step, out, n, vec);
     return check_launch("ps_apply_i32");
 }
 
@@ -950,8 +1131,16 @@ int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W,
     bool al;
     if (int rc = fill_pack(pk, paras, W, al)) return rc;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
-    hipLaunchKernelGGL(k_ps_combine_ina, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), local, pk,
-                       W, ldexpf(1.0f, k), ldexpf(1.0f, -k), (float)weight_step, out, n);
+    int vec = al && aligned16(local) && aligned16(out);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_reduce_blocks);
+    hipStream_t s = hs(stream);
+    float sc = ldexpf(1.0f, k), inv = ldexpf(1.0f, -k), ws = (float)weight_step;
+    switch (W) {
+#define PSI(WW) case WW: hipLaunchKernelGGL(k_ps_combine_ina<WW>, dim3(g), dim3(kBlock), 0, s, local, pk, W, sc, inv, ws, out, n, vec); break;
+        PSI(1) PSI(2) PSI(3) PSI(4) PSI(5) PSI(6) PSI(7) PSI(8)
+#undef PSI
+        default: hipLaunchKernelGGL(k_ps_combine_ina<0>, dim3(g), dim3(kBlock), 0, s, local, pk, W, sc, inv, ws, out, n, vec);
+    }
     return check_launch("ps_combine_ina_f32");
 }
 
@@ -991,7 +1180,13 @@ int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
     if (fields) f = NgaFieldsDev{fields->bitmap, fields->count, fields->flags, fields->index,
                                  fields->switch_id, fields->frag_id};
     hipStream_t s = hs(stream);
-    if (pstride % 16 == 0 && V % 4 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
+    int log2L = -1;
+    if (V % 4 == 0 && V / 4 <= 64 && ((V / 4) & (V / 4 - 1)) == 0)
+        for (log2L = 0; (1 << log2L) < V / 4; ++log2L) {}
+    if (log2L >= 0 && pstride % 16 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
+        hipLaunchKernelGGL(k_unpack_nga_shfl, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
+                           s, pkts, npk, log2L, pstride, f, vals);
+    } else if (pstride % 16 == 0 && V % 4 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
         hipLaunchKernelGGL(k_unpack_nga_vec, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
                            s, pkts, npk, V, pstride, f, vals);
     } else {

@@ -11,6 +11,7 @@
 
 #include <arpa/inet.h>
 #include <netinet/in.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -123,6 +124,61 @@ int ina_send_packets_fd(int fd, const uint8_t* host_pkts, size_t npk, size_t str
     }
     if (sent > 0x7FFFFFFFu) sent = 0x7FFFFFFFu;
     return (int)sent;
+}
+
+int ina_recv_packets_fd(int fd, uint8_t* host_pkts, size_t max_pkts, size_t stride, size_t skip,
+                        int timeout_ms, uint32_t* lens) {
+    if (max_pkts == 0) return 0;
+    if (!host_pkts || stride == 0) return ina::set_error(INA_EINVAL, "bad packet buffer%s", "");
+    constexpr size_t kBatch = 1024;
+    std::vector<mmsghdr> msgs(kBatch);
+    std::vector<iovec> iov(2 * kBatch);
+    std::vector<uint8_t> skipbuf(skip ? skip : 1);
+    size_t got = 0;
+    timespec t0{};
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    const int64_t end_ns = (int64_t)t0.tv_sec * 1000000000LL + t0.tv_nsec +
+                           (int64_t)(timeout_ms < 0 ? 0 : timeout_ms) * 1000000LL;
+    // wait for data (poll) then drain what is queued (recvmmsg, non-blocking), until
+    // max_pkts have arrived or the deadline passes
+    while (got < max_pkts) {
+        size_t nb = max_pkts - got < kBatch ? max_pkts - got : kBatch;
+        for (size_t i = 0; i < nb; ++i) {
+            int k = 0;
+            if (skip) {                        // e.g. the 20-byte IPv4 header of a raw socket
+                iov[2 * i].iov_base = skipbuf.data();
+                iov[2 * i].iov_len = skip;
+                k = 1;
+            }
+            iov[2 * i + k].iov_base = host_pkts + (got + i) * stride;
+            iov[2 * i + k].iov_len = stride;
+            memset(&msgs[i], 0, sizeof(mmsghdr));
+            msgs[i].msg_hdr.msg_iov = &iov[2 * i];
+            msgs[i].msg_hdr.msg_iovlen = (size_t)(k + 1);
+        }
+        int r = recvmmsg(fd, msgs.data(), (unsigned)nb, MSG_DONTWAIT, nullptr);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            if (errno != EAGAIN && errno != EWOULDBLOCK)
+                return ina::set_error(INA_ESOCK, "recvmmsg: %s", strerror(errno));
+            timespec now{};
+            clock_gettime(CLOCK_MONOTONIC, &now);
+            int64_t left = end_ns - ((int64_t)now.tv_sec * 1000000000LL + now.tv_nsec);
+            if (left <= 0) break;
+            pollfd pfd{fd, POLLIN, 0};
+            int pr = poll(&pfd, 1, (int)((left + 999999) / 1000000));
+            if (pr < 0 && errno != EINTR) return ina::set_error(INA_ESOCK, "poll: %s", strerror(errno));
+            if (pr == 0) break;
+            continue;
+        }
+        for (int i = 0; i < r; ++i) {
+            size_t len = msgs[i].msg_len;
+            len = len > skip ? len - skip : 0;
+            if (lens) lens[got + i] = (uint32_t)len;
+        }
+        got += (size_t)r;
+    }
+    return (int)(got > 0x7FFFFFFFu ? 0x7FFFFFFFu : got);
 }
 
 void send_gradients(uint32_t* gradient_array, int packet_num, uint32_t dst_ip, int worker_id,

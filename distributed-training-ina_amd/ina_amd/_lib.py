@@ -70,6 +70,7 @@ SIGNATURES = {
     "send_gradients": [C.POINTER(C.c_uint32), _i, _u32, _i, _u32, _i],
     "ina_send_gradients_fd": [_i, _vp, _i, _u32, _i, _u32, _i],
     "ina_send_packets_fd": [_i, _vp, _sz, _sz, _sz, _u32],
+    "ina_recv_packets_fd": [_i, _vp, _sz, _sz, _sz, _i, _vp],
 }
 _RESTYPE = {"ina_version": C.c_char_p, "ina_last_error_string": C.c_char_p,
             "ina_switch_scratch_bytes": C.c_size_t, "send_gradients": None}

@@ -267,13 +267,16 @@ class Switch:
 
 
 def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
-               nontemporal: bool | None = None, reduce_blocks: int | None = None):
+               nontemporal: bool | None = None, reduce_blocks: int | None = None,
+               stream_blocks: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce, unroll is
     the sum-reduce's 16-byte chunks per worker per thread (1, 2 or 4)."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")
+    if stream_blocks is not None:
+        check(lib.ina_set_tuning(4, int(stream_blocks)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

@@ -191,6 +191,15 @@ int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num
 int ina_send_packets_fd(int fd, const uint8_t* host_pkts, size_t npkts, size_t stride,
                         size_t pkt_len, uint32_t dst_ip);
 
+/* Batched datagram ingest, the counterpart of get_data_from_nic (utils.py:61-64,
+ * one recvfrom per packet): up to max_pkts datagrams land in host_pkts at `stride`
+ * apart via recvmmsg(); the first `skip` bytes of each datagram (20 for the IPv4
+ * header a raw socket delivers) are discarded.  Returns once max_pkts datagrams have
+ * arrived or timeout_ms has passed (0 = drain what is queued).  lens (may be NULL)
+ * receives each packet's length after `skip`.  Returns packets received. */
+int ina_recv_packets_fd(int fd, uint8_t* host_pkts, size_t max_pkts, size_t stride, size_t skip,
+                        int timeout_ms, uint32_t* lens);
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,16 @@ for st in $STAGES; do
           python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
         rc=$?; tail -2 "$OUT/pmc_$c.err"; [ $rc -ne 0 ] && fatal "pmc $c" $rc
       done ;;
+    config1)
+      timeout -k 10 600 python examples/config1_loopback.py --epochs 3 --local-steps 5 > "$OUT/config1.log" 2>&1
+      rc=$?; tail -8 "$OUT/config1.log"; [ $rc -ne 0 ] && fatal config1 $rc ;;
+    rehearse)
+      INA_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 > "$OUT/rehearse2.json" 2> "$OUT/rehearse2.err"
+      rc=$?; cat "$OUT/rehearse2.json"; tail -3 "$OUT/rehearse2.err"; [ $rc -ne 0 ] && fatal rehearse $rc ;;
+    sharded)
+      timeout -k 10 400 python bench.py --mode sharded --steps 10 --warmup 3 > "$OUT/sharded1.json" 2> "$OUT/sharded1.err"
+      rc=$?; cat "$OUT/sharded1.json"; tail -3 "$OUT/sharded1.err"; [ $rc -ne 0 ] && fatal sharded $rc ;;
     extra)
       timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extra > "$OUT/extra_bench.json" 2> "$OUT/extra.err"
       rc=$?; tail -3 "$OUT/extra.err"; [ $rc -ne 0 ] && fatal extra $rc
