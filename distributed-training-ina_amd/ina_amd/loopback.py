@@ -34,6 +34,9 @@ class SwitchStandIn:
                  num_slots: int | None = None):
         self.n, self.W, self.V = n, W, V
         self.npk = -(-n // V)
+        # The Tofino pool is 16,384 slots (config.p4:5) and the reference sends a whole
+        # bucket with index = seq mod 16384 (DataManager.py:119), so buckets of more
+        # packets collide there.  HBM holds a pool for the whole bucket instead.
         self.num_slots = num_slots or max(_lib.NUM_REGISTER, self.npk)
         self.switch = ops.Switch(V, self.num_slots, switch_id, device)
         self.ring = PacketRing(W * self.npk, V, device)
@@ -65,10 +68,12 @@ class SwitchStandIn:
 
 
 def worker_send(sock, delta: torch.Tensor, worker_id: int, W: int, V: int, k: int, seq0: int,
-                switch_id: int = 1) -> int:
-    """Worker data plane: quantise -> NGA-V pack on the GPU -> sendmmsg."""
+                switch_id: int = 1, num_slots: int = _lib.NUM_REGISTER) -> int:
+    """Worker data plane: quantise -> NGA-V pack on the GPU -> sendmmsg.  num_slots must
+    be the aggregator's pool size (index = seq mod num_slots, DataManager.py:119)."""
     q = ops.quantize(delta.reshape(-1).contiguous(), k)
-    pk = ops.pack_nga(q, V, bitmap=worker_id, count=W, switch_id=switch_id, seq0=seq0)
+    pk = ops.pack_nga(q, V, bitmap=worker_id, count=W, switch_id=switch_id, seq0=seq0,
+                      num_slots=num_slots)
     return send_device_packets(sock, pk, _lib.NGA_HDR_BYTES + 4 * V)
 
 
@@ -96,7 +101,8 @@ def ps_serve(model, W: int, epochs: int, tcp_port: int, data_path: str, k: int =
             c, _ = srv.accept()
             conns.append(c)
         for c in conns:                                   # init (worker.py:56-61)
-            ps.send_data(c, {"para": local.cpu(), "epochs": epochs, "k": k, "V": V})
+            ps.send_data(c, {"para": local.cpu(), "epochs": epochs, "k": k, "V": V,
+                             "num_slots": sw.num_slots})
         for epoch in range(epochs):
             t0 = time.time()
             S = sw.aggregate(data, seq_base(epoch, sw.npk), timeout_ms)
@@ -133,7 +139,8 @@ def worker_serve(idx: int, W: int, tcp_port: int, data_path: str, make_model, tr
         for epoch in range(epochs):
             train_step(model, idx, epoch)
             p = torch.nn.utils.parameters_to_vector(model.parameters()).detach()
-            worker_send(data, p - glob, idx + 1, W, V, k, seq_base(epoch, npk))
+            worker_send(data, p - glob, idx + 1, W, V, k, seq_base(epoch, npk),
+                        num_slots=cfg["num_slots"])
             glob = ps.get_data(ctl).to(device)
             torch.nn.utils.vector_to_parameters(glob, model.parameters())
     finally:

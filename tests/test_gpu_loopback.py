@@ -18,12 +18,16 @@ from tests.conftest import PKG_ROOT, REPO
 
 pytestmark = pytest.mark.gpu
 
-N_IN, N_OUT = 100, 1000
 K = 16
+SIZES = {"small": (100, 1000), "big": (100, 6000)}   # big: 606,000 params -> 18,938 NGA-32 packets
 
 
-def make_model():
-    return torch.nn.Linear(N_IN, N_OUT)
+def make_small():
+    return torch.nn.Linear(*SIZES["small"])
+
+
+def make_big():
+    return torch.nn.Linear(*SIZES["big"])
 
 
 def noise(idx, epoch, n):
@@ -38,12 +42,12 @@ def train_step(model, idx, epoch):
         torch.nn.utils.vector_to_parameters(v, model.parameters())
 
 
-def _worker(idx, W, port, path):
+def _worker(idx, W, port, path, size):
     for p in (REPO, PKG_ROOT):
         if p not in sys.path:
             sys.path.insert(0, p)
     from ina_amd.loopback import worker_serve
-    worker_serve(idx, W, port, path, make_model, train_step)
+    worker_serve(idx, W, port, path, make_big if size == "big" else make_small, train_step)
 
 
 def _free_port():
@@ -52,21 +56,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("V", [256, 32])
-def test_loopback_two_workers_bit_exact(V):
+@pytest.mark.parametrize("V,size", [(256, "small"), (32, "small"), (32, "big")])
+def test_loopback_two_workers_bit_exact(V, size):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from ina_amd.loopback import ps_serve
     W, epochs = 2, 3
     torch.manual_seed(0)
-    model = make_model().cuda()
+    model = (make_big if size == "big" else make_small)().cuda()
     local0 = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
     port = _free_port()
     seen = []
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "switch.sock")
         ctx = mp.get_context("spawn")
-        procs = [ctx.Process(target=_worker, args=(i, W, port, path)) for i in range(W)]
+        procs = [ctx.Process(target=_worker, args=(i, W, port, path, size)) for i in range(W)]
         # the PS binds first; workers retry their connect inside create_connection's backlog
         import threading
         out = {}
