@@ -144,8 +144,9 @@ def run_extra(dev):
         sw.count.zero_()
         sw.frag.zero_()
         sw.process(stream, acts)
-    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts)", _time(sw_round, reps=5, warm=1),
-                     2 * stream.numel() + 4 * (1 << 17) * V * 2))
+    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort)",
+                     _time(sw_round, reps=5, warm=1),
+                     2 * stream.numel() + 2 * npk * V * 4))
     del stream
 
     # --- end to end: pinned host -> HBM -> reduce -> pinned host -------------------------------

@@ -138,6 +138,16 @@ static inline bool slot_ballot_ok(int V) {
 }
 
 
+// Cross-lane moves by one lane as DPP row moves (measured on gfx950, tools/lab/dpp_lab.hip):
+// wave_shl:1 -> lane i reads lane i+1 (lane 63 keeps its own value); wave_shr:1 -> lane i
+// reads lane i-1 (lane 0 keeps its own).  One VALU op instead of an LDS ds_bpermute.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x138, 0xF, 0xF, false);
+}
+
 template <int W>
 constexpr int kUnrW = W > 0 ? W : 1;
 
@@ -805,8 +815,8 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_shfl(const uint8_t* __res
         u32x4 a = {0u, 0u, 0u, 0u};
         if (active) a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk) + j);
         u32x4 b;
-        b.x = __shfl_down(a.x, 1, 64); b.y = __shfl_down(a.y, 1, 64);
-        b.z = __shfl_down(a.z, 1, 64); b.w = __shfl_down(a.w, 1, 64);
+        b.x = from_next_lane(a.x); b.y = from_next_lane(a.y);
+        b.z = from_next_lane(a.z); b.w = from_next_lane(a.w);
         if (!active) continue;
         if (j == L - 1) b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk) + L);
         if (j == 0) nga_store_header(f, p, a.x, a.y, a.z, a.w);

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "ina.h"
 #include "ina_internal.h"
 
@@ -22,6 +24,16 @@ using u32x4s = uint32_t __attribute__((ext_vector_type(4)));
 constexpr int kSwBlock = 256;               // 4 waves, one slot segment each
 constexpr int kMaxV = 256;                  // 4 payload words per lane
 constexpr int kMaxStride = 16 + 4 * kMaxV;  // 1040 B, LDS staging per wave
+
+// Cross-lane moves by one lane as DPP row moves (measured on gfx950, tools/lab/dpp_lab.hip):
+// wave_shl:1 -> lane i reads lane i+1 (lane 63 keeps its own value); wave_shr:1 -> lane i
+// reads lane i-1 (lane 0 keeps its own).  One VALU op instead of an LDS ds_bpermute.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x138, 0xF, 0xF, false);
+}
 
 __device__ __forceinline__ uint32_t rd_be32(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
@@ -150,6 +162,152 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
     }
 }
 
+
+// 2c. register-resident segment processor (stride % 16 == 0, V % 4 == 0, V <= 256).
+// Lane l owns payload values 4l..4l+3.  Value j sits at bytes 15+4j, so lane l's
+// values are decoded from chunks l and l+1 (16-byte chunk c = bytes 16c..16c+15) and
+// chunk c (c >= 1) is re-encoded from lane c-1's values plus lane c's first value.
+// Lanes 0..L (L = V/4) load chunks 0..L; when L = 64 the tail chunk 64 is held by
+// lane 63 in a second register.  A wave loads up to kB packets of its segment at
+// once, runs the P4 state machine over them in arrival order with the slot's
+// registers in VGPRs, re-encodes and stores each packet.  Each wave owns windows of
+// 64 sorted positions and runs the segments that start in them.
+constexpr int kB = 8;
+
+__device__ __forceinline__ uint32_t enc_lo(uint32_t prev, uint32_t v) {
+    // LE dword: BE bytes 1..3 of prev followed by BE byte 0 of v
+    return (__builtin_bswap32(prev) >> 8) | (v & 0xFF000000u);
+}
+
+__global__ __launch_bounds__(kSwBlock) void k_switch_run2(ina_switch_state_t st,
+                                                          uint8_t* __restrict__ pkts, size_t npk,
+                                                          size_t stride,
+                                                          const uint32_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ ids,
+                                                          uint8_t* __restrict__ actions) {
+    const int lane = threadIdx.x & 63;
+    const int V = st.V;
+    const int L = V >> 2;                       // lanes holding values
+    const bool vl = lane < L;
+    const bool wide = L == 64;                  // tail chunk lives in lane 63's t[]
+    const size_t wave = ((size_t)blockIdx.x * kSwBlock + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
+    const uint32_t NS = st.num_slots;
+    // each wave takes windows of 64 sorted positions and processes the segments that
+    // START in its window (a segment may run past the window's end)
+    for (size_t w0 = wave * 64; w0 < npk; w0 += nwaves * 64) {
+        const size_t i = w0 + (size_t)lane;
+        const uint32_t ki = i < npk ? keys[i] : NS;
+        const uint32_t idw = i < npk ? ids[i] : 0u;     // packet ids of the window, one load
+        const uint32_t kp = (i > 0 && i <= npk) ? keys[i - 1] : 0xFFFFFFFFu;
+        unsigned long long hm = __ballot(i < npk && ki < NS && (i == 0 || kp != ki));
+        while (hm) {
+        const int hl = __builtin_ctzll(hm);
+        hm &= hm - 1;
+        const size_t pos = w0 + (size_t)hl;
+        const uint32_t slot = __builtin_amdgcn_readlane(ki, hl);
+        // segment end: first later position whose key differs (vector scan)
+        size_t end;
+        {
+            unsigned long long dm = __ballot(ki != slot) & ~((2ull << hl) - 1ull);
+            if (dm) {
+                end = w0 + (size_t)__builtin_ctzll(dm);
+            } else {
+                size_t j0 = w0 + 64;
+                for (;;) {
+                    const size_t j = j0 + (size_t)lane;
+                    const bool diff = j >= npk || keys[j] != slot;
+                    const unsigned long long m = __ballot(diff);
+                    if (m) { end = j0 + (size_t)__builtin_ctzll(m); break; }
+                    j0 += 64;
+                }
+            }
+        }
+        uint32_t cnt = st.count[slot];
+        uint32_t frag = st.frag[slot];
+        u32x4s reg = {0u, 0u, 0u, 0u};
+        if (vl) reg = *reinterpret_cast<const u32x4s*>(st.regs + (size_t)slot * V + 4 * lane);
+        for (size_t q0 = pos; q0 < end; q0 += kB) {
+            const int nb = (int)((end - q0) < (size_t)kB ? (end - q0) : (size_t)kB);
+            u32x4s a[kB], t[kB];
+            uint32_t pid[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const size_t q = q0 + (size_t)b;
+                pid[b] = b >= nb ? 0u
+                         : (q < w0 + 64 ? __builtin_amdgcn_readlane(idw, (int)(q - w0)) : ids[q]);
+                const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[b] * stride);
+                a[b] = (b < nb && lane <= L) ? pk[lane] : u32x4s{0u, 0u, 0u, 0u};
+                t[b] = (b < nb && wide && lane == 63) ? pk[64] : u32x4s{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                if (b >= nb) break;
+                const uint32_t h1 = __builtin_amdgcn_readlane(a[b].y, 0),
+                               h2 = __builtin_amdgcn_readlane(a[b].z, 0),
+                               h3 = __builtin_amdgcn_readlane(a[b].w, 0);
+                const uint32_t hcount = h1 & 0xFFu, flags = (h1 >> 8) & 0xFFu;
+                const uint32_t frag_in = __builtin_bswap32((h2 >> 24) | (h3 << 8));
+                uint8_t act;
+                if ((flags >> 6) & 1u) {                     // ack: reset_id (fragcheck.p4:26-31)
+                    frag = 0;
+                    act = INA_ACT_FWD_ACK;
+                } else {
+                    if (frag == 0) frag = frag_in;           // write_read_id (fragcheck.p4:14-24)
+                    if (frag != frag_in) {                   // collision (ngaa.p4:177-181)
+                        if (lane == 0) a[b].y |= (uint32_t)INA_FLAG_COLLISION << 8;
+                        act = INA_ACT_FWD_COLLISION;
+                    } else {
+                        cnt = (cnt + 1u) & 0xFFu;            // read_add_count (ngaa.p4:66-78)
+                        if (cnt == hcount) cnt = 0;
+                        const bool first = cnt == 1u;
+                        u32x4s c;                            // chunk l+1
+                        c.x = from_next_lane(a[b].x); c.y = from_next_lane(a[b].y);
+                        c.z = from_next_lane(a[b].z); c.w = from_next_lane(a[b].w);
+                        if (wide && lane == 63) c = t[b];
+                        u32x4s v;                            // values 4l..4l+3
+                        v.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.x, a[b].w, 3));
+                        v.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.y, c.x, 3));
+                        v.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.z, c.y, 3));
+                        v.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.w, c.z, 3));
+                        reg = first ? v : reg + v;           // processor.p4:16-21
+                        // out_value -> payload (processor.p4:22)
+                        u32x4s p;                            // lane l-1's values
+                        p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
+                        p.z = from_prev_lane(reg.z); p.w = from_prev_lane(reg.w);
+                        if (lane == 0) {
+                            a[b].w = (a[b].w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                        } else if (lane <= L) {
+                            a[b].x = enc_lo(p.x, p.y);
+                            a[b].y = enc_lo(p.y, p.z);
+                            a[b].z = enc_lo(p.z, p.w);
+                            a[b].w = lane < L ? enc_lo(p.w, reg.x)
+                                              : ((__builtin_bswap32(p.w) >> 8) | (a[b].w & 0xFF000000u));
+                        }
+                        if (wide && lane == 63) {            // tail chunk 64 from lane 63's values
+                            t[b].x = enc_lo(reg.x, reg.y);
+                            t[b].y = enc_lo(reg.y, reg.z);
+                            t[b].z = enc_lo(reg.z, reg.w);
+                            t[b].w = (__builtin_bswap32(reg.w) >> 8) | (t[b].w & 0xFF000000u);
+                        }
+                        act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
+                    }
+                }
+                u32x4s* pk = reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride);
+                if (lane <= L) pk[lane] = a[b];
+                if (wide && lane == 63) pk[64] = t[b];
+                if (lane == 0) actions[pid[b]] = act;
+            }
+        }
+        if (lane == 0) {
+            st.count[slot] = (uint8_t)cnt;
+            st.frag[slot] = frag;
+        }
+        if (vl) *reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane) = reg;
+        }
+    }
+}
+
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 static int end_bit_for(uint32_t num_slots) {
@@ -204,9 +362,17 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
     if (hipcub::DeviceRadixSort::SortPairs(temp, tb, k_in, k_out, v_in, v_out, (int)npk, 0,
                                            end_bit_for(st->num_slots), s) != hipSuccess)
         return set_error(INA_EHIP, "switch radix sort%s", "");
-    unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
-    hipLaunchKernelGGL(k_switch_run, dim3(gw), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, k_out,
-                       v_out, actions);
+    const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
+                      st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
+    if (fast) {
+        unsigned gr = (unsigned)std::min<size_t>((npk + kSwBlock - 1) / kSwBlock, 2048);
+        hipLaunchKernelGGL(k_switch_run2, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, k_out,
+                           v_out, actions);
+    } else {
+        unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
+        hipLaunchKernelGGL(k_switch_run, dim3(gw), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, k_out,
+                           v_out, actions);
+    }
     if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch run launch%s", "");
     return INA_OK;
 }

@@ -1,0 +1,27 @@
+"""Profile target: the device packet-stream switch on 8 workers x NGA-256 packets of
+a config-3 bucket (run under rocprofv3 --kernel-trace --stats)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "distributed-training-ina_amd"))
+from ina_amd import ops  # noqa: E402
+
+n, W, V = int(os.environ.get("N", 26_214_400)), 8, 256
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(1)
+bufs = [torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
+        for _ in range(W)]
+slots = 1 << 17
+stream = torch.cat([ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots) for w, b in enumerate(bufs)])
+sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
+acts = torch.empty(stream.shape[0], dtype=torch.uint8, device=dev)
+for i in range(int(os.environ.get("REPS", 5))):
+    sw.count.zero_()
+    sw.frag.zero_()
+    sw.process(stream, acts)
+torch.cuda.synchronize()
+ok = torch.equal(stream.view(W, -1, stream.shape[1])[-1, :, 15:15 + 4 * V].contiguous().view(-1).view(torch.uint8)[:8], stream[stream.shape[0] // W * (W - 1), 15:23])
+print("done", stream.shape, int((acts == 1).sum()))
