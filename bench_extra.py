@@ -36,7 +36,7 @@ def _row(name, secs, nbytes, **kw):
     return r
 
 
-DEFAULTS = {"max_blocks": 2048, "reduce_blocks": 512, "stream_blocks": 1024}
+DEFAULTS = {"max_blocks": 8192, "reduce_blocks": 512, "stream_blocks": 8192}
 
 
 def _sweep(ops, rows, sweeps, name, knob, values, fn, nbytes):
@@ -89,24 +89,24 @@ def run_extra(dev):
     # --- quantise / dequantise ------------------------------------------------------------
     x = rnd_f32(n3)
     q = torch.empty(n3, dtype=torch.int32, device=dev)
-    _sweep(ops, rows, gsweep, "quantize_f32_i32", "stream_blocks", (512, 1024, 2048, 4096),
+    _sweep(ops, rows, gsweep, "quantize_f32_i32", "stream_blocks", (512, 2048, 8192),
            lambda: ops.quantize(x, 16, out=q), 8 * n3)
     y = torch.empty(n3, dtype=torch.float32, device=dev)
-    _sweep(ops, rows, gsweep, "dequantize_i32_f32", "stream_blocks", (512, 1024, 2048, 4096),
+    _sweep(ops, rows, gsweep, "dequantize_i32_f32", "stream_blocks", (512, 2048, 8192),
            lambda: ops.dequantize(q, 16, out=y), 8 * n3)
 
     # --- config 2: fused quantise + reduce, 4 x ResNet-50 fp32 -----------------------------
     n2 = 25_557_032
     b2 = [rnd_f32(n2) for _ in range(4)]
     o2 = torch.empty(n2, dtype=torch.int32, device=dev)
-    _sweep(ops, rows, gsweep, "quantize_reduce_f32_i32 W=4 (C2)", "reduce_blocks",
-           (256, 512, 1024, 2048), lambda: ops.quantize_reduce(b2, 16, out=o2), (4 * 4 + 4) * n2)
+    _sweep(ops, rows, gsweep, "quantize_reduce_f32_i32 W=4 (C2)", "stream_blocks",
+           (512, 2048, 8192), lambda: ops.quantize_reduce(b2, 16, out=o2), (4 * 4 + 4) * n2)
     # --- config 4: int16 saturating, 16 workers --------------------------------------------
     b4 = b2 + [rnd_f32(n2) for _ in range(12)]
     o4 = torch.empty(n2, dtype=torch.int16, device=dev)
     f4 = torch.empty((n2 + 255) // 256, dtype=torch.uint8, device=dev)
     _sweep(ops, rows, gsweep, "quantize_reduce_f32_i16 W=16 V=256 (C4)", "max_blocks",
-           (512, 1024, 2048, 4096),
+           (2048, 8192, 16384),
            lambda: ops.quantize_reduce_i16(b4, 13, 256, out=o4, overflow=f4),
            (16 * 4 + 2) * n2 + f4.numel())
     # --- PS combine (launch.py:42-52), W=4 ---------------------------------------------------
