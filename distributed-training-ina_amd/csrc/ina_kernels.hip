@@ -468,67 +468,6 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i16(PtrPack<float> in, 
     }
 }
 
-// int16, coalesced form: a wave owns a 512-value tile as two 256-value halves; lane l
-// holds values 4l..4l+3 of each half (two fully coalesced float4 loads per worker),
-// stores 8 bytes per half, and a slot of V values (V/4 a power of two <= 64) is V/4
-// adjacent lanes of one half -> one ballot per half decides the slot flags.
-template <int W>
-__global__ __launch_bounds__(kBlock) void k_quant_reduce_i16_tile(PtrPack<float> in, int Wd,
-                                                                  int16_t* __restrict__ out, size_t n,
-                                                                  float s, int V, int lanes_per_slot,
-                                                                  uint8_t* __restrict__ ovf) {
-    const int nw = W > 0 ? W : Wd;
-    constexpr int UNR = W > 0 ? W : 1;
-    const int lane = threadIdx.x & 63;
-    const size_t wave = ((size_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const size_t nwaves = ((size_t)gridDim.x * kBlock) >> 6;
-    const size_t ntiles = (n + 511) / 512;
-    for (size_t t = wave; t < ntiles; t += nwaves) {
-        bool sat[2] = {false, false};
-        const size_t e0 = t * 512 + 4 * (size_t)lane;          // half 0; half 1 at +256
-        const bool full = t * 512 + 512 <= n;
-        if (full) {
-            int32_t a[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll UNR
-            for (int w = 0; w < nw; ++w) {
-                f32x4 u = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w] + e0));
-                f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w] + e0 + 256));
-                a[0][0] += q16(u.x, s, sat[0]); a[0][1] += q16(u.y, s, sat[0]);
-                a[0][2] += q16(u.z, s, sat[0]); a[0][3] += q16(u.w, s, sat[0]);
-                a[1][0] += q16(v.x, s, sat[1]); a[1][1] += q16(v.y, s, sat[1]);
-                a[1][2] += q16(v.z, s, sat[1]); a[1][3] += q16(v.w, s, sat[1]);
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                uint2 o;
-                o.x = (uint32_t)(uint16_t)sat16(a[h][0], sat[h]) | ((uint32_t)sat16(a[h][1], sat[h]) << 16);
-                o.y = (uint32_t)(uint16_t)sat16(a[h][2], sat[h]) | ((uint32_t)sat16(a[h][3], sat[h]) << 16);
-                __builtin_nontemporal_store(o.x, reinterpret_cast<uint32_t*>(out + e0 + 256 * h));
-                __builtin_nontemporal_store(o.y, reinterpret_cast<uint32_t*>(out + e0 + 256 * h) + 1);
-            }
-        } else {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                for (size_t j = e0 + 256 * h; j < e0 + 256 * h + 4 && j < n; ++j) {
-                    int32_t a = 0;
-                    for (int w = 0; w < nw; ++w) a += q16(in.p[w][j], s, sat[h]);
-                    out[j] = (int16_t)sat16(a, sat[h]);
-                }
-        }
-        if (ovf) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                unsigned long long m = __ballot(sat[h]);
-                const size_t e = e0 + 256 * h;
-                int g0 = lane & ~(lanes_per_slot - 1);
-                unsigned long long gm = lanes_per_slot == 64 ? ~0ull
-                                        : (((1ull << lanes_per_slot) - 1ull) << g0);
-                if (e < n && (lane & (lanes_per_slot - 1)) == 0) ovf[e / (size_t)V] = (m & gm) ? 1 : 0;
-            }
-        }
-    }
-}
-
 __global__ __launch_bounds__(kBlock) void k_quant_reduce_i16_scalar(PtrPack<float> in, int W,
                                                                     int16_t* __restrict__ out,
                                                                     size_t n, float s, int V,

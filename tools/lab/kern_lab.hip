@@ -14,9 +14,6 @@ extern "C" int lab_kern(int which, int grid, const void* const* bufs, int W, voi
     if (which == 0) {                                     // C4 int16 fused (row form), W = 16
         hipLaunchKernelGGL(k_quant_reduce_i16<16>, dim3(grid), dim3(kBlock), 0, s, pk, W,
                            (int16_t*)out, n, sc, V, V / 8, (uint8_t*)ovf);
-    } else if (which == 1) {                              // C4 int16 fused (tile form)
-        hipLaunchKernelGGL(k_quant_reduce_i16_tile<16>, dim3(grid), dim3(kBlock), 0, s, pk, W,
-                           (int16_t*)out, n, sc, V, V / 4, (uint8_t*)ovf);
     } else if (which == 2) {                              // C2 int32 fused, W = 4
         hipLaunchKernelGGL(k_quant_reduce_i32<4>, dim3(grid), dim3(kBlock), 0, s, pk, W,
                            (int32_t*)out, n, 65536.0f, 1);

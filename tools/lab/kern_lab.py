@@ -22,22 +22,18 @@ f16 = [torch.empty((n + 255) // 256, dtype=torch.uint8, device=dev) for _ in ran
 o32 = torch.empty(n, dtype=torch.int32, device=dev)
 st = torch.cuda.current_stream().cuda_stream
 
-for which in (0, 1):
-    assert lab.lab_kern(which, 2048, arr16, 16, o16[which].data_ptr(), n, 256,
-                        f16[which].data_ptr(), st) == 0
-torch.cuda.synchronize()
-print("i16 tile == row:", torch.equal(o16[0], o16[1]), torch.equal(f16[0], f16[1]),
-      int(f16[0].sum()))
+# (round 1 also compared a coalesced 512-value "tile" form of the int16 kernel: equal
+#  results, equal speed within noise -- not kept)
 
 cfgs = []
 for G in (256, 512, 1024, 2048, 4096, 8192):
-    cfgs += [("C4 row", 0, G, (16 * 4 + 2) * n), ("C4 tile", 1, G, (16 * 4 + 2) * n),
+    cfgs += [("C4 row", 0, G, (16 * 4 + 2) * n),
              ("C2", 2, G, (4 * 4 + 4) * n), ("quantize", 3, G, 8 * n)]
 
 
 def run(c):
     name, which, G, _ = c
-    if which in (0, 1):
+    if which == 0:
         return lab.lab_kern(which, G, arr16, 16, o16[0].data_ptr(), n, 256, f16[0].data_ptr(), st)
     if which == 2:
         return lab.lab_kern(2, G, arr16, 4, o32.data_ptr(), n, 256, None, st)
@@ -61,7 +57,7 @@ for c, ts in times.items():
     m = statistics.median(ts)
     rows.append({"kernel": c[0], "grid": c[2], "us": round(m * 1e6, 1),
                  "GBps": round(c[3] / m / 1e9, 1)})
-for k in ("C4 row", "C4 tile", "C2", "quantize"):
+for k in ("C4 row", "C2", "quantize"):
     for r in sorted([r for r in rows if r["kernel"] == k], key=lambda r: -r["GBps"]):
         print(r)
 os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
