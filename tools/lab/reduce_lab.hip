@@ -163,6 +163,36 @@ __global__ __launch_bounds__(B) void v_ldsdma2(Ptrs in, u32x4* __restrict__ out,
     }
 }
 
+
+// v8: explicit "all loads, then adds" with an optional scheduling fence (SB) so the
+// compiler cannot interleave the adds (and full vmcnt(0) waits) between load pairs
+template <int W, int U, int B, int SB>
+__global__ __launch_bounds__(B) void v_gs_sb(Ptrs in, u32x4* __restrict__ out, size_t n4) {
+    const size_t tid = (size_t)blockIdx.x * B + threadIdx.x, stride = (size_t)gridDim.x * B;
+    size_t i = tid;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        u32x4 v[W][U];
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[w][u] = ldnt(in.p[w] + i + u * stride);
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            u32x4 a = v[0][u];
+#pragma unroll
+            for (int w = 1; w < W; ++w) a += v[w][u];
+            __builtin_nontemporal_store(a, out + i + u * stride);
+        }
+    }
+    for (; i < n4; i += stride) {
+        u32x4 a = ldnt(in.p[0] + i);
+#pragma unroll
+        for (int w = 1; w < W; ++w) a += ldnt(in.p[w] + i);
+        __builtin_nontemporal_store(a, out + i);
+    }
+}
+
 // ceilings: W-stream read with a negligible write; 1->1 copy
 template <int W, int B>
 __global__ __launch_bounds__(B) void v_readonly(Ptrs in, u32x4* __restrict__ out, size_t n4) {
@@ -193,6 +223,8 @@ static Kfn pick(int variant, int U) {
         case 5: if constexpr (B <= 512 && (B % 64) == 0) return U == 1 ? v_ldsdma2<8, B, 0> : v_ldsdma2<8, B, 2>; else return nullptr;
         case 6: return v_readonly<8, B>;
         case 7: return v_copy<B>;
+        case 8: return U == 2 ? v_gs_sb<8, 2, B, 0> : v_gs_sb<8, 4, B, 0>;
+        case 9: return U == 2 ? v_gs_sb<8, 2, B, 1> : v_gs_sb<8, 4, B, 1>;
     }
     return nullptr;
 }

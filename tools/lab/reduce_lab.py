@@ -39,7 +39,14 @@ stream = torch.cuda.current_stream().cuda_stream
 
 configs = []
 FOCUS = os.environ.get("FOCUS", "")
-if FOCUS == "grid":
+if FOCUS == "sched":
+    for U, B, G in itertools.product((2, 4), (256, 512), (256, 512, 1024)):
+        configs.append(("gridstride", 1, U, B, G))
+        configs.append(("loads_first", 8, U, B, G))
+        configs.append(("loads_first_schedbarrier", 9, U, B, G))
+    for G in (1024, 2048):
+        configs.append(("readonly8", 6, 1, 256, G))
+elif FOCUS == "grid":
     for U, B, G in itertools.product((2, 4, 6, 8), (128, 256, 512, 768, 1024), (128, 192, 256, 320, 384, 512, 768)):
         configs.append(("gridstride", 1, U, B, G))
     for G in (1024, 2048):
