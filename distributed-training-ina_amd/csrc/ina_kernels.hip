@@ -795,39 +795,59 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_vec(const uint8_t* __rest
     }
 }
 
-// wave-shuffle unpack: L = V/4 lanes per packet (L a power of two <= 64), lane j
-// loads 16-byte chunk j once and takes chunk j+1 from its neighbour (__shfl_down);
-// the packet's last lane loads the tail chunk L itself.
+// wave-shuffle unpack (values only): L = V/4 lanes per packet (L a power of two
+// <= 64); lane j loads 16-byte chunk j once and takes chunk j+1 from its neighbour
+// (DPP wave_shl:1); the packet's last lane loads the tail chunk L itself.  Each
+// thread handles U wave-tiles per iteration (U loads in flight, as in chunk_loop).
+template <int U>
 __global__ __launch_bounds__(kBlock) void k_unpack_nga_shfl(const uint8_t* __restrict__ pkts,
                                                             size_t npk, int log2L, size_t pstride,
-                                                            NgaFieldsDev f, int32_t* __restrict__ vals) {
+                                                            int32_t* __restrict__ vals) {
     const size_t gs = (size_t)gridDim.x * kBlock;
     const uint32_t L = 1u << log2L;
     const size_t total = npk << log2L;
     const int lane = threadIdx.x & 63;
     const size_t wave0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) & ~(size_t)63;
-    for (size_t base = wave0; base < total; base += gs) {
-        const size_t g = base + (size_t)lane;
-        const bool active = g < total;
-        const size_t p = g >> log2L;
-        const uint32_t j = (uint32_t)(g & (L - 1));
-        const uint8_t* pk = pkts + p * pstride;
-        u32x4 a = {0u, 0u, 0u, 0u};
-        if (active) a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk) + j);
-        u32x4 b;
-        b.x = from_next_lane(a.x); b.y = from_next_lane(a.y);
-        b.z = from_next_lane(a.z); b.w = from_next_lane(a.w);
-        if (!active) continue;
-        if (j == L - 1) b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk) + L);
-        if (j == 0) nga_store_header(f, p, a.x, a.y, a.z, a.w);
-        if (vals) {
-            u32x4 o;
-            o.x = bswap(__builtin_amdgcn_alignbyte(b.x, a.w, 3));
-            o.y = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
-            o.z = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
-            o.w = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
-            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(vals) + g);
+    for (size_t base = wave0; base < total; base += U * gs) {
+        u32x4 a[U], t[U];
+        size_t g[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            g[u] = base + u * gs + (size_t)lane;
+            const size_t p = g[u] >> log2L;
+            const uint32_t j = (uint32_t)(g[u] & (L - 1));
+            const u32x4* pk = reinterpret_cast<const u32x4*>(pkts + p * pstride);
+            a[u] = g[u] < total ? __builtin_nontemporal_load(pk + j) : u32x4{0u, 0u, 0u, 0u};
+            t[u] = (g[u] < total && j == L - 1) ? __builtin_nontemporal_load(pk + L)
+                                               : u32x4{0u, 0u, 0u, 0u};
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            u32x4 b;
+            b.x = from_next_lane(a[u].x); b.y = from_next_lane(a[u].y);
+            b.z = from_next_lane(a[u].z); b.w = from_next_lane(a[u].w);
+            if ((g[u] & (L - 1)) == L - 1) b = t[u];
+            if (g[u] < total) {
+                u32x4 o;
+                o.x = bswap(__builtin_amdgcn_alignbyte(b.x, a[u].w, 3));
+                o.y = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
+                o.z = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
+                o.w = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
+                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(vals) + g[u]);
+            }
+        }
+    }
+}
+
+// header fields, one thread per packet (coalesced SoA stores); pairs with the
+// values-only k_unpack_nga_shfl
+__global__ __launch_bounds__(kBlock) void k_unpack_nga_hdr(const uint8_t* __restrict__ pkts,
+                                                           size_t npk, size_t pstride,
+                                                           NgaFieldsDev f) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    for (size_t p = (size_t)blockIdx.x * kBlock + threadIdx.x; p < npk; p += gs) {
+        u32x4 a = *reinterpret_cast<const u32x4*>(pkts + p * pstride);
+        nga_store_header(f, p, a.x, a.y, a.z, a.w);
     }
 }
 
@@ -1194,8 +1214,12 @@ int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
     if (V % 4 == 0 && V / 4 <= 64 && ((V / 4) & (V / 4 - 1)) == 0)
         for (log2L = 0; (1 << log2L) < V / 4; ++log2L) {}
     if (log2L >= 0 && pstride % 16 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
-        hipLaunchKernelGGL(k_unpack_nga_shfl, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
-                           s, pkts, npk, log2L, pstride, f, vals);
+        if (fields)
+            hipLaunchKernelGGL(k_unpack_nga_hdr, dim3(grid_for(npk, 1)), dim3(kBlock), 0, s, pkts, npk,
+                               pstride, f);
+        if (vals)
+            hipLaunchKernelGGL(k_unpack_nga_shfl<4>, dim3(grid_for(npk * (size_t)(V / 4), 4, g_stream_blocks)),
+                               dim3(kBlock), 0, s, pkts, npk, log2L, pstride, vals);
     } else if (pstride % 16 == 0 && V % 4 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
         hipLaunchKernelGGL(k_unpack_nga_vec, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
                            s, pkts, npk, V, pstride, f, vals);
