@@ -36,7 +36,7 @@ def _row(name, secs, nbytes, **kw):
     return r
 
 
-DEFAULTS = {"max_blocks": 8192, "reduce_blocks": 512, "stream_blocks": 8192}
+DEFAULTS = {"max_blocks": 8192, "reduce_blocks": 0, "stream_blocks": 8192, "combine_blocks": 512}
 
 
 def _sweep(ops, rows, sweeps, name, knob, values, fn, nbytes):
@@ -78,7 +78,7 @@ def run_extra(dev):
                 t = _time(lambda: ops.sum_reduce(b3, out=o3))
                 sweep.append(_row("sum_reduce_i32 W=8", t, (W3 + 1) * n3 * 4, nt=nt, unroll=unroll,
                                   max_blocks=blocks))
-    ops.set_tuning(reduce_blocks=512, unroll=4, nontemporal=True)
+    ops.set_tuning(reduce_blocks=0, unroll=4, nontemporal=True)
     rows.append(max(sweep, key=lambda r: r["GB/s"]) | {"note": "best of sweep"})
     for W in (2, 4, 16):
         bw = [rnd_i32(n3) for _ in range(W)] if W != 16 else b3 + [rnd_i32(n3) for _ in range(8)]
@@ -112,10 +112,10 @@ def run_extra(dev):
     # --- PS combine (launch.py:42-52), W=4 ---------------------------------------------------
     local = rnd_f32(n2, 1.0)
     oc = torch.empty_like(local)
-    _sweep(ops, rows, gsweep, "ps_combine_f32 W=4", "reduce_blocks", (256, 512, 1024, 2048),
+    _sweep(ops, rows, gsweep, "ps_combine_f32 W=4", "combine_blocks", (256, 512, 1024, 2048),
            lambda: ops.ps_combine(local, b2[:4], 0.2, out=oc), (4 + 2) * 4 * n2)
     from ina_amd import ps as ps_mod
-    _sweep(ops, rows, gsweep, "ps_combine_ina_f32 W=4", "reduce_blocks", (256, 512, 1024, 2048),
+    _sweep(ops, rows, gsweep, "ps_combine_ina_f32 W=4", "combine_blocks", (256, 512, 1024, 2048),
            lambda: ps_mod.combine_ina(local, b2[:4], 16, 0.2, out=oc), (4 + 2) * 4 * n2)
     del b4, b2, local, oc, o4
 

@@ -53,12 +53,15 @@ static int check_launch(const char* what) {
 // tuning (grid cap / unroll), overridable for sweeps through ina_set_tuning()
 // ---------------------------------------------------------------------------
 static std::atomic<int> g_max_blocks{8192};   // elementwise kernels (kern_lab: 8192 >= 2048)
-// sum-reduce: measured best on MI355X (tools/lab/reduce_lab.py, interleaved A/B):
-// 512 x 256-thread workgroups (2 per CU), 4 x 16 B per worker per thread in flight
-static std::atomic<int> g_reduce_blocks{512};
+// sum-reduce: measured best on MI355X (tools/lab/reduce_lab.py, reduce_w_lab.py,
+// interleaved A/B): 4 x 16 B per worker per thread in flight and 64*W 256-thread
+// workgroups (W = 2, 4: 256; W = 8: 512; W = 16: 1024).  0 = that rule; >0 overrides.
+static std::atomic<int> g_reduce_blocks{0};
 static std::atomic<int> g_unroll{4};
 // the other chunk_loop<4> streaming kernels
 static std::atomic<int> g_stream_blocks{8192};
+// PS combine kernels (W+2 streams)
+static std::atomic<int> g_combine_blocks{512};
 static std::atomic<int> g_nontemporal{1};
 
 static inline unsigned grid_for(size_t work_items, int per_thread, int cap_override = 0) {
@@ -247,7 +250,9 @@ __global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_scalar(PtrPack<int32_
 template <int W, int U>
 static void launch_reduce_w(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
                             hipStream_t s) {
-    unsigned g = grid_for(n4, U, g_reduce_blocks.load());
+    int cap = g_reduce_blocks.load();
+    if (cap <= 0) cap = W * 64 < 256 ? 256 : (W * 64 > 1024 ? 1024 : W * 64);
+    unsigned g = grid_for(n4, U, cap);
     if (g_nontemporal.load())
         hipLaunchKernelGGL((k_sum_reduce_i32_vec<W, U, true>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
     else
@@ -966,8 +971,9 @@ int ina_set_tuning(int key, int value) {
         case 0: if (value < 1) return INA_EINVAL; g_max_blocks = value; return INA_OK;
         case 1: if (value != 1 && value != 2 && value != 4) return INA_EINVAL; g_unroll = value; return INA_OK;
         case 2: g_nontemporal = value ? 1 : 0; return INA_OK;
-        case 3: if (value < 1) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
+        case 3: if (value < 0) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
         case 4: if (value < 1) return INA_EINVAL; g_stream_blocks = value; return INA_OK;
+        case 5: if (value < 1) return INA_EINVAL; g_combine_blocks = value; return INA_OK;
         default: return INA_EINVAL;
     }
 }
@@ -1130,7 +1136,7 @@ int ina_ps_combine_f32(const float* local, const float* const* paras, int W, dou
     if (int rc = fill_pack(pk, paras, W, al)) return rc;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = al && aligned16(local) && aligned16(out);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_reduce_blocks);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_combine_blocks);
     hipStream_t s = hs(stream);
     float ws = (float)weight_step;
     switch (W) {
@@ -1162,7 +1168,7 @@ int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W,
     if (int rc = fill_pack(pk, paras, W, al)) return rc;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = al && aligned16(local) && aligned16(out);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_reduce_blocks);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_combine_blocks);
     hipStream_t s = hs(stream);
     float sc = ldexpf(1.0f, k), inv = ldexpf(1.0f, -k), ws = (float)weight_step;
     switch (W) {

@@ -93,7 +93,7 @@ def test_sum_reduce_tunings_identical(unroll, blocks, nt):
         o.set_tuning(reduce_blocks=blocks, unroll=unroll, nontemporal=nt)
         got = host(o.sum_reduce([dev(b) for b in bufs]))
     finally:
-        o.set_tuning(max_blocks=8192, unroll=4, nontemporal=True, reduce_blocks=512)
+        o.set_tuning(max_blocks=8192, unroll=4, nontemporal=True, reduce_blocks=0)
     assert np.array_equal(got, orc.sum_reduce_i32(bufs))
 
 
