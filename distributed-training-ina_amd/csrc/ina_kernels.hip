@@ -682,17 +682,47 @@ struct NgaHdr {
     int V;
 };
 
-__device__ __forceinline__ uint32_t nga_val(const int32_t* __restrict__ vals, size_t n, size_t p,
-                                            int V, long j) {
+// Value sources of the pack kernels: stored int32 words, or fp32 gradients (optionally
+// minus a base vector: the worker's delta p - p_global) quantised on the fly -- the
+// fused worker-side quantise + packetise (DataManager.py:37 then 111-165, one pass).
+struct SrcI32 {
+    const int32_t* __restrict__ v;
+    __device__ __forceinline__ uint32_t one(size_t e) const { return (uint32_t)v[e]; }
+    __device__ __forceinline__ u32x4 four(size_t e) const {
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + e));
+    }
+};
+struct SrcQ32 {
+    const float* __restrict__ x;
+    const float* __restrict__ base;   // may be null
+    float s;
+    __device__ __forceinline__ uint32_t one(size_t e) const {
+        return (uint32_t)q32(base ? __fsub_rn(x[e], base[e]) : x[e], s);
+    }
+    __device__ __forceinline__ u32x4 four(size_t e) const {
+        f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + e));
+        if (base) {
+            f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base + e));
+            a.x = __fsub_rn(a.x, b.x); a.y = __fsub_rn(a.y, b.y);
+            a.z = __fsub_rn(a.z, b.z); a.w = __fsub_rn(a.w, b.w);
+        }
+        return u32x4{(uint32_t)q32(a.x, s), (uint32_t)q32(a.y, s), (uint32_t)q32(a.z, s),
+                     (uint32_t)q32(a.w, s)};
+    }
+};
+
+template <typename Src>
+__device__ __forceinline__ uint32_t nga_val(const Src& src, size_t n, size_t p, int V, long j) {
     // payload word j of packet p (0 outside [0, V) and past n: zero tail pad)
     if (j < 0 || j >= V) return 0u;
     size_t e = p * (size_t)V + (size_t)j;
-    return e < n ? (uint32_t)vals[e] : 0u;
+    return e < n ? src.one(e) : 0u;
 }
 
 // vector path: stride % 16 == 0, V % 4 == 0, 16-byte aligned buffers.
 // Thread per 16-byte chunk of the packet buffer.
-__global__ __launch_bounds__(kBlock) void k_pack_nga_vec(const int32_t* __restrict__ vals, size_t n,
+template <typename Src>
+__global__ __launch_bounds__(kBlock) void k_pack_nga_vec(Src src, size_t n,
                                                          NgaHdr h, const uint8_t* __restrict__ ovf,
                                                          uint8_t* __restrict__ pkts,
                                                          uint32_t chunks_per_pkt, size_t nchunks) {
@@ -712,18 +742,18 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_vec(const int32_t* __restri
             o.x = bswap(h.bitmap);
             o.y = count | (flags << 8) | (bi << 16);
             o.z = (bi >> 16) | (sw << 16) | (bf << 24);
-            o.w = (bf >> 8) | (bswap(nga_val(vals, n, p, V, 0)) << 24);
+            o.w = (bf >> 8) | (bswap(nga_val(src, n, p, V, 0)) << 24);
         } else {
             long j0 = 4 * (long)c - 4;   // out word m=4c+t takes payload words m-4, m-3
             uint32_t v[5];
             size_t e0 = p * (size_t)V + (size_t)j0;
             if (j0 + 4 < V && e0 + 5 <= n) {
-                u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vals + e0));
+                u32x4 a = src.four(e0);
                 v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-                v[4] = (uint32_t)vals[e0 + 4];
+                v[4] = src.one(e0 + 4);
             } else {
 #pragma unroll
-                for (int t = 0; t < 5; ++t) v[t] = nga_val(vals, n, p, V, j0 + t);
+                for (int t = 0; t < 5; ++t) v[t] = nga_val(src, n, p, V, j0 + t);
             }
             o.x = (bswap(v[0]) >> 8) | (v[1] & 0xFF000000u);
             o.y = (bswap(v[1]) >> 8) | (v[2] & 0xFF000000u);
@@ -735,7 +765,8 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_vec(const int32_t* __restri
 }
 
 // generic path: any stride / alignment, thread per output byte
-__global__ __launch_bounds__(kBlock) void k_pack_nga_bytes(const int32_t* __restrict__ vals, size_t n,
+template <typename Src>
+__global__ __launch_bounds__(kBlock) void k_pack_nga_bytes(Src src, size_t n,
                                                            NgaHdr h, const uint8_t* __restrict__ ovf,
                                                            uint8_t* __restrict__ pkts, size_t pstride,
                                                            size_t nbytes) {
@@ -754,7 +785,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_bytes(const int32_t* __rest
         else if (b < 15) out = (uint8_t)(seq >> (24 - 8 * (b - 11)));
         else if (b < 15 + 4 * (size_t)V) {
             size_t q = b - 15;
-            out = (uint8_t)(nga_val(vals, n, p, V, (long)(q / 4)) >> (24 - 8 * (q % 4)));
+            out = (uint8_t)(nga_val(src, n, p, V, (long)(q / 4)) >> (24 - 8 * (q % 4)));
         }
         pkts[g] = out;
     }
@@ -959,6 +990,32 @@ static int fill_pack(PtrPack<T>& pk, const T* const* bufs, int W, bool& all_alig
     }
     for (int w = W; w < INA_MAX_WORKERS; ++w) pk.p[w] = nullptr;
     return INA_OK;
+}
+
+template <typename Src>
+static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina_nga_params_t* prm,
+                           const uint8_t* ovf, uint8_t* pkts, size_t pstride, hipStream_t s) {
+    if (!prm || prm->V <= 0 || prm->num_slots == 0)
+        return set_error(INA_EINVAL, "bad nga params%s", "");
+    const int V = prm->V;
+    if (pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V)
+        return set_error(INA_EINVAL, "stride < 15 + 4V%s", "");
+    size_t npk = (n + (size_t)V - 1) / (size_t)V;
+    if (npk == 0) return INA_OK;
+    if (!pkts) return set_error(INA_EINVAL, "null pointer%s", "");
+    NgaHdr h{prm->bitmap, prm->seq0, prm->num_slots,
+             (uint32_t)prm->count | ((uint32_t)prm->flags << 8) | ((uint32_t)prm->switch_id << 16), V};
+    if (pstride % 16 == 0 && V % 4 == 0 && src_aligned && aligned16(pkts)) {
+        uint32_t cpp = (uint32_t)(pstride / 16);
+        size_t nchunks = npk * cpp;
+        hipLaunchKernelGGL(k_pack_nga_vec<Src>, dim3(grid_for(nchunks, 1)), dim3(kBlock), 0, s, src, n, h,
+                           ovf, pkts, cpp, nchunks);
+    } else {
+        size_t nbytes = npk * pstride;
+        hipLaunchKernelGGL(k_pack_nga_bytes<Src>, dim3(grid_for(nbytes, 1)), dim3(kBlock), 0, s, src, n,
+                           h, ovf, pkts, pstride, nbytes);
+    }
+    return check_launch("pack_nga");
 }
 
 extern "C" {
@@ -1182,28 +1239,18 @@ int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W,
 
 int ina_pack_nga(const int32_t* vals, size_t n, const ina_nga_params_t* prm, const uint8_t* ovf,
                  uint8_t* pkts, size_t pstride, ina_stream_t stream) {
-    if (!prm || prm->V <= 0 || prm->num_slots == 0)
-        return set_error(INA_EINVAL, "bad nga params%s", "");
-    const int V = prm->V;
-    if (pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V)
-        return set_error(INA_EINVAL, "stride < 15 + 4V%s", "");
-    size_t npk = (n + (size_t)V - 1) / (size_t)V;
-    if (npk == 0) return INA_OK;
-    if (!vals || !pkts) return set_error(INA_EINVAL, "null pointer%s", "");
-    NgaHdr h{prm->bitmap, prm->seq0, prm->num_slots,
-             (uint32_t)prm->count | ((uint32_t)prm->flags << 8) | ((uint32_t)prm->switch_id << 16), V};
-    hipStream_t s = hs(stream);
-    if (pstride % 16 == 0 && V % 4 == 0 && aligned16(vals) && aligned16(pkts)) {
-        uint32_t cpp = (uint32_t)(pstride / 16);
-        size_t nchunks = npk * cpp;
-        hipLaunchKernelGGL(k_pack_nga_vec, dim3(grid_for(nchunks, 1)), dim3(kBlock), 0, s, vals, n, h,
-                           ovf, pkts, cpp, nchunks);
-    } else {
-        size_t nbytes = npk * pstride;
-        hipLaunchKernelGGL(k_pack_nga_bytes, dim3(grid_for(nbytes, 1)), dim3(kBlock), 0, s, vals, n, h,
-                           ovf, pkts, pstride, nbytes);
-    }
-    return check_launch("pack_nga");
+    if (n && !vals) return set_error(INA_EINVAL, "null pointer%s", "");
+    return pack_nga_launch(SrcI32{vals}, aligned16(vals), n, prm, ovf, pkts, pstride, hs(stream));
+}
+
+int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
+                          const ina_nga_params_t* prm, uint8_t* pkts, size_t pstride,
+                          ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n && !x) return set_error(INA_EINVAL, "null pointer%s", "");
+    bool al = aligned16(x) && (!base || aligned16(base));
+    return pack_nga_launch(SrcQ32{x, base, ldexpf(1.0f, k)}, al, n, prm, nullptr, pkts, pstride,
+                           hs(stream));
 }
 
 int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,

@@ -62,6 +62,7 @@ SIGNATURES = {
     "ina_ps_apply_i32": [_vp, _vp, _i, _d, _vp, _sz, _vp],
     "ina_ps_combine_ina_f32": [_vp, _vp, _i, _i, _d, _vp, _sz, _vp],
     "ina_pack_nga": [_vp, _sz, C.POINTER(NgaParams), _vp, _vp, _sz, _vp],
+    "ina_quantize_pack_nga": [_vp, _vp, _sz, _i, C.POINTER(NgaParams), _vp, _sz, _vp],
     "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
     "ina_switch_scratch_bytes": [_sz, _u32],

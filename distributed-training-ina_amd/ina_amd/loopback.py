@@ -67,13 +67,14 @@ class SwitchStandIn:
         return self.out[: self.n]
 
 
-def worker_send(sock, delta: torch.Tensor, worker_id: int, W: int, V: int, k: int, seq0: int,
-                switch_id: int = 1, num_slots: int = _lib.NUM_REGISTER) -> int:
-    """Worker data plane: quantise -> NGA-V pack on the GPU -> sendmmsg.  num_slots must
-    be the aggregator's pool size (index = seq mod num_slots, DataManager.py:119)."""
-    q = ops.quantize(delta.reshape(-1).contiguous(), k)
-    pk = ops.pack_nga(q, V, bitmap=worker_id, count=W, switch_id=switch_id, seq0=seq0,
-                      num_slots=num_slots)
+def worker_send(sock, params: torch.Tensor, base: torch.Tensor, worker_id: int, W: int, V: int,
+                k: int, seq0: int, switch_id: int = 1, num_slots: int = _lib.NUM_REGISTER) -> int:
+    """Worker data plane: quantise(params - base) + NGA-V pack in one GPU pass, then
+    sendmmsg.  num_slots must be the aggregator's pool size (index = seq mod num_slots,
+    DataManager.py:119)."""
+    pk = ops.quantize_pack_nga(params.reshape(-1).contiguous(), k, V, bitmap=worker_id, count=W,
+                               switch_id=switch_id, seq0=seq0, base=base.reshape(-1).contiguous(),
+                               num_slots=num_slots)
     return send_device_packets(sock, pk, _lib.NGA_HDR_BYTES + 4 * V)
 
 
@@ -139,7 +140,7 @@ def worker_serve(idx: int, W: int, tcp_port: int, data_path: str, make_model, tr
         for epoch in range(epochs):
             train_step(model, idx, epoch)
             p = torch.nn.utils.parameters_to_vector(model.parameters()).detach()
-            worker_send(data, p - glob, idx + 1, W, V, k, seq_base(epoch, npk),
+            worker_send(data, p, glob, idx + 1, W, V, k, seq_base(epoch, npk),
                         num_slots=cfg["num_slots"])
             glob = ps.get_data(ctl).to(device)
             torch.nn.utils.vector_to_parameters(glob, model.parameters())

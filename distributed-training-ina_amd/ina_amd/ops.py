@@ -190,6 +190,29 @@ def pack_nga(vals: torch.Tensor, V: int, bitmap: int, count: int, switch_id: int
     return out
 
 
+def quantize_pack_nga(x: torch.Tensor, k: int, V: int, bitmap: int, count: int, switch_id: int,
+                      seq0: int, base: torch.Tensor | None = None, flags: int = 0,
+                      num_slots: int = NUM_REGISTER, stride: int | None = None,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+    """Fused worker side: NGA-V packets of quantize(x - base, k) in one pass (same bytes as
+    quantize() then pack_nga())."""
+    _req(x, torch.float32, "x")
+    if base is not None:
+        _req(base, torch.float32, "base")
+        if base.numel() != x.numel():
+            raise ValueError("base and x differ in length")
+        _same_device(x, base)
+    stride = stride or nga_stride(V)
+    npk = (x.numel() + V - 1) // V
+    out = torch.empty((npk, stride), dtype=torch.uint8, device=x.device) if out is None else out
+    prm = _lib.NgaParams(bitmap & 0xFFFFFFFF, count & 0xFF, flags & 0xFF, switch_id & 0xFF, 0,
+                         seq0 & 0xFFFFFFFF, num_slots, V)
+    check(load().ina_quantize_pack_nga(x.data_ptr(), base.data_ptr() if base is not None else None,
+                                       x.numel(), k, C.byref(prm), out.data_ptr(), stride,
+                                       _stream(x)), "quantize_pack_nga")
+    return out
+
+
 def unpack_nga(pkts: torch.Tensor, V: int, stride: int | None = None, with_values: bool = True):
     """Returns (fields dict of device tensors, int32 values [npkts*V] or None)."""
     _req(pkts, torch.uint8, "pkts")

@@ -136,6 +136,12 @@ typedef struct ina_nga_fields { /* SoA header fields; any pointer may be NULL */
 int ina_pack_nga(const int32_t* vals, size_t n, const ina_nga_params_t* prm,
                  const uint8_t* overflow_per_slot, uint8_t* pkts, size_t stride,
                  ina_stream_t stream);
+/* Fused worker side: quantise fp32 gradients (x - base when base != NULL: the
+ * worker's delta against the global parameters) and packetise in one pass, with
+ * exactly the bytes of ina_quantize_f32_i32 (+ fp32 subtraction) then ina_pack_nga. */
+int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
+                          const ina_nga_params_t* prm, uint8_t* pkts, size_t stride,
+                          ina_stream_t stream);
 /* PS-side parse (NGAPacket.py:62-143 / get_data_from_nic, utils.py:61-64), following
  * headers.p4: payload at byte 15, big-endian.  vals gets npkts*V int32 (may be NULL). */
 int ina_unpack_nga(const uint8_t* pkts, size_t npkts, int V, size_t stride,

@@ -391,3 +391,21 @@ def test_switch_collision_free_equals_bulk_reduce():
     order = np.argsort(host(f["frag_id"]))
     got = host(vals).reshape(npk, V)[order].reshape(-1)[:n]
     assert np.array_equal(got, host(o.sum_reduce([dev(b) for b in bufs])))
+
+
+@pytest.mark.parametrize("V", [32, 256, 33])
+@pytest.mark.parametrize("with_base", [False, True])
+@pytest.mark.parametrize("padded", [True, False])
+def test_quantize_pack_fused_matches_oracle(V, with_base, padded):
+    """Worker side in one pass: packets of quantize(x - base) == oracle quantize then pack."""
+    o = ops()
+    rng = np.random.default_rng(V + 2 * with_base + padded)
+    n = 77 * V + 5
+    x = mixed_floats(rng, n)
+    base = (rng.standard_normal(n) * 0.1).astype(np.float32) if with_base else None
+    stride = o.nga_stride(V) if padded else 15 + 4 * V
+    got = host(o.quantize_pack_nga(dev(x), 16, V, bitmap=3, count=4, switch_id=1, seq0=42,
+                                   base=dev(base) if with_base else None, stride=stride))
+    d = (x - base).astype(np.float32) if with_base else x
+    want = orc.pack_nga(orc.quantize_i32(d, 16), V, 3, 4, 1, 42, stride=stride)
+    assert np.array_equal(got, want)
