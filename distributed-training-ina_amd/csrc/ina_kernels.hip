@@ -875,6 +875,67 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_shfl(const uint8_t* __res
     }
 }
 
+// PS side, fused: for every packet the switch completed (actions[p] == FWD_AGG) decode
+// its V summed words, place them by slot = frag_id - seq0 (the sequence numbering of
+// DataManager.py:116-130), dequantise and apply the update
+//     out[slot*V + j] = local[..] + ws * ((float)sum * 2^-k)
+// (aggregate()'s update with the switch's integer sum, launch.py:46-50), and write the
+// slot's PS ack header (is_ack=1, fragcheck.p4:26-31) into ack row `slot`.  Same lane
+// layout as k_unpack_nga_shfl: L = V/4 lanes per packet.
+__global__ __launch_bounds__(kBlock) void k_apply_completed_nga(
+        const uint8_t* __restrict__ pkts, size_t npk, int log2L, size_t pstride,
+        const uint8_t* __restrict__ actions, uint32_t seq0, size_t nslots,
+        const float* __restrict__ local, float inv, float ws, float* __restrict__ out, size_t n,
+        uint8_t* __restrict__ acks, size_t ack_stride) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const uint32_t L = 1u << log2L;
+    const size_t total = npk << log2L;
+    const int lane = threadIdx.x & 63;
+    const int lead = lane & ~(int)(L - 1);                   // first lane of this packet group
+    const size_t wave0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) & ~(size_t)63;
+    for (size_t base = wave0; base < total; base += gs) {
+        const size_t g = base + (size_t)lane;
+        const bool in = g < total;
+        const size_t p = g >> log2L;
+        const uint32_t j = (uint32_t)(g & (L - 1));
+        const u32x4* pk = reinterpret_cast<const u32x4*>(pkts + p * pstride);
+        const bool done = in && actions[p] == INA_ACT_FWD_AGG;
+        u32x4 a = done ? __builtin_nontemporal_load(pk + j) : u32x4{0u, 0u, 0u, 0u};
+        u32x4 b;
+        b.x = from_next_lane(a.x); b.y = from_next_lane(a.y);
+        b.z = from_next_lane(a.z); b.w = from_next_lane(a.w);
+        // frag_id (header bytes 11..14) from the group's chunk 0
+        const uint32_t h2 = __shfl(a.z, lead, 64), h3 = __shfl(a.w, lead, 64);
+        if (!done) continue;
+        if (j == L - 1) b = __builtin_nontemporal_load(pk + L);
+        const size_t slot = (size_t)(uint32_t)(__builtin_bswap32((h2 >> 24) | (h3 << 8)) - seq0);
+        if (slot >= nslots) continue;                         // not from this bucket
+        if (j == 0 && acks) {
+            u32x4 hd = a;
+            hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+            *reinterpret_cast<u32x4*>(acks + slot * ack_stride) = hd;
+        }
+        const size_t e = slot * ((size_t)L * 4) + 4 * (size_t)j;
+        uint32_t v[4];
+        v[0] = bswap(__builtin_amdgcn_alignbyte(b.x, a.w, 3));
+        v[1] = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
+        v[2] = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
+        v[3] = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
+        if (e + 4 <= n) {
+            f32x4 l = *reinterpret_cast<const f32x4*>(local + e);
+            f32x4 r;
+            r.x = __fadd_rn(l.x, __fmul_rn(__fmul_rn((float)(int32_t)v[0], inv), ws));
+            r.y = __fadd_rn(l.y, __fmul_rn(__fmul_rn((float)(int32_t)v[1], inv), ws));
+            r.z = __fadd_rn(l.z, __fmul_rn(__fmul_rn((float)(int32_t)v[2], inv), ws));
+            r.w = __fadd_rn(l.w, __fmul_rn(__fmul_rn((float)(int32_t)v[3], inv), ws));
+            *reinterpret_cast<f32x4*>(out + e) = r;
+        } else {
+            for (int t = 0; t < 4 && e + t < n; ++t)
+                out[e + t] = __fadd_rn(local[e + t], __fmul_rn(__fmul_rn((float)(int32_t)v[t], inv), ws));
+        }
+    }
+}
+
 // header fields, one thread per packet (coalesced SoA stores); pairs with the
 // values-only k_unpack_nga_shfl
 __global__ __launch_bounds__(kBlock) void k_unpack_nga_hdr(const uint8_t* __restrict__ pkts,
@@ -1281,6 +1342,29 @@ int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
                            0, s, pkts, npk, V, pstride, f, vals);
     }
     return check_launch("unpack_nga");
+}
+
+int ina_apply_completed_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
+                            const uint8_t* actions, uint32_t seq0, const float* local, int k,
+                            double weight_step, float* out, size_t n, uint8_t* acks,
+                            size_t ack_stride, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    int log2L = -1;
+    if (V > 0 && V % 4 == 0 && V / 4 <= 64 && ((V / 4) & (V / 4 - 1)) == 0)
+        for (log2L = 0; (1 << log2L) < V / 4; ++log2L) {}
+    if (log2L < 0) return set_error(INA_EINVAL, "V must be 4 x a power of two <= 256%s", "");
+    if (pstride % 16 || pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V || !aligned16(pkts))
+        return set_error(INA_EINVAL, "packets must be 16-byte aligned rows of stride %% 16 == 0%s", "");
+    if (acks && (ack_stride % 16 || !aligned16(acks)))
+        return set_error(INA_EINVAL, "ack rows must be 16-byte aligned%s", "");
+    if (npk == 0 || n == 0) return INA_OK;
+    if (!actions || !local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
+    if (!aligned16(local) || !aligned16(out)) return set_error(INA_EINVAL, "local/out must be 16-byte aligned%s", "");
+    size_t nslots = (n + (size_t)V - 1) / (size_t)V;
+    hipLaunchKernelGGL(k_apply_completed_nga, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
+                       hs(stream), pkts, npk, log2L, pstride, actions, seq0, nslots, local,
+                       ldexpf(1.0f, -k), (float)weight_step, out, n, acks, ack_stride);
+    return check_launch("apply_completed_nga");
 }
 
 int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id, uint32_t aggregator_index,

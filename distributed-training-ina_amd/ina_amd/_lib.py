@@ -65,6 +65,7 @@ SIGNATURES = {
     "ina_quantize_pack_nga": [_vp, _vp, _sz, _i, C.POINTER(NgaParams), _vp, _sz, _vp],
     "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
+    "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],
     "ina_switch_scratch_bytes": [_sz, _u32],
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],

@@ -41,10 +41,10 @@ class SwitchStandIn:
         self.switch = ops.Switch(V, self.num_slots, switch_id, device)
         self.ring = PacketRing(W * self.npk, V, device)
         self.out = torch.empty(self.npk * V, dtype=torch.int32, device=device)
+        self.acks = torch.zeros((self.npk, self.ring.stride), dtype=torch.uint8, device=device)
         self.device = torch.device(device)
 
-    def aggregate(self, sock, seq0: int, timeout_ms: int = 30000) -> torch.Tensor:
-        """Receive W x npk packets, run them through the switch, return int32 [n]."""
+    def _switch_batch(self, sock, timeout_ms):
         want = self.W * self.npk
         got = 0
         while got < want:
@@ -54,10 +54,25 @@ class SwitchStandIn:
             got += r
         pk = self.ring.to_device(got)
         act = self.switch.process(pk)
-        done = torch.nonzero(act == _lib.ACT_FWD_AGG).flatten()
-        if done.numel() != self.npk:
+        ndone = int((act == _lib.ACT_FWD_AGG).sum())
+        if ndone != self.npk:
             bad = int((act == _lib.ACT_FWD_COLLISION).sum())
-            raise RuntimeError(f"{done.numel()}/{self.npk} slots completed ({bad} collisions)")
+            raise RuntimeError(f"{ndone}/{self.npk} slots completed ({bad} collisions)")
+        return pk, act
+
+    def aggregate_apply(self, sock, seq0: int, local: torch.Tensor, k: int, weight_step: float,
+                        timeout_ms: int = 30000) -> torch.Tensor:
+        """Receive, switch, then ONE fused kernel: completed slots -> dequantise -> update
+        (local + weight_step * sum * 2^-k) and PS acks, which then free the slots."""
+        pk, act = self._switch_batch(sock, timeout_ms)
+        new = ops.apply_completed(pk, act, self.V, seq0, local, k, weight_step, acks=self.acks)
+        self.switch.process(self.acks)
+        return new
+
+    def aggregate(self, sock, seq0: int, timeout_ms: int = 30000) -> torch.Tensor:
+        """Receive W x npk packets, run them through the switch, return int32 [n]."""
+        pk, act = self._switch_batch(sock, timeout_ms)
+        done = torch.nonzero(act == _lib.ACT_FWD_AGG).flatten()
         fin = pk.index_select(0, done)
         fields, vals = ops.unpack_nga(fin, self.V)
         slot = (fields["frag_id"].to(torch.int64) - seq0) % (1 << 32)
@@ -106,9 +121,9 @@ def ps_serve(model, W: int, epochs: int, tcp_port: int, data_path: str, k: int =
                              "num_slots": sw.num_slots})
         for epoch in range(epochs):
             t0 = time.time()
-            S = sw.aggregate(data, seq_base(epoch, sw.npk), timeout_ms)
+            new = sw.aggregate_apply(data, seq_base(epoch, sw.npk), local, k, 1.0 / (W + 1),
+                                     timeout_ms)
             t_agg = time.time()
-            new = ops.ps_apply(local, S, k, 1.0 / (W + 1))
             torch.nn.utils.vector_to_parameters(new, model.parameters())
             local = new
             host = local.cpu()

@@ -234,6 +234,27 @@ def unpack_nga(pkts: torch.Tensor, V: int, stride: int | None = None, with_value
     return f, vals
 
 
+def apply_completed(pkts: torch.Tensor, actions: torch.Tensor, V: int, seq0: int,
+                    local: torch.Tensor, k: int, weight_step: float, out=None, acks=None):
+    """PS side after Switch.process: completed slots (actions == ACT_FWD_AGG) are decoded,
+    dequantised and applied: out[slot*V + j] = local + weight_step * sum * 2^-k, slot =
+    frag_id - seq0.  With acks ([nslots, stride] uint8), row `slot` gets the PS ack header."""
+    _req(pkts, torch.uint8, "pkts")
+    _req(actions, torch.uint8, "actions")
+    _req(local, torch.float32, "local")
+    npk, stride = pkts.shape
+    out = torch.empty_like(local) if out is None else out
+    ack_ptr, ack_stride = None, 0
+    if acks is not None:
+        _req(acks, torch.uint8, "acks")
+        ack_ptr, ack_stride = acks.data_ptr(), acks.shape[1]
+    check(load().ina_apply_completed_nga(pkts.data_ptr(), npk, V, stride, actions.data_ptr(),
+                                         seq0 & 0xFFFFFFFF, local.data_ptr(), k, float(weight_step),
+                                         out.data_ptr(), local.numel(), ack_ptr, ack_stride,
+                                         _stream(pkts)), "apply_completed")
+    return out
+
+
 def pack_c128(gradient: torch.Tensor, packet_num: int, worker_id: int, aggregator_index: int,
               tensor_index: int, out: torch.Tensor | None = None) -> torch.Tensor:
     """communicator.cc's packet_t x packet_num as uint8 [packet_num, 524] (device)."""

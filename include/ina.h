@@ -146,6 +146,16 @@ int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
  * headers.p4: payload at byte 15, big-endian.  vals gets npkts*V int32 (may be NULL). */
 int ina_unpack_nga(const uint8_t* pkts, size_t npkts, int V, size_t stride,
                    const ina_nga_fields_t* fields, int32_t* vals, ina_stream_t stream);
+/* PS side, fused, after ina_switch_process: for each packet with actions[p] ==
+ * INA_ACT_FWD_AGG, slot = frag_id - seq0; out[slot*V + j] = local[..] +
+ * float(weight_step) * ((float)payload_j * 2^-k) for slot*V + j < n, and (acks !=
+ * NULL) row `slot` of acks (ack_stride bytes apart) gets the packet's header with
+ * is_ack = 1 -- the PS acknowledgement that frees the slot (fragcheck.p4:26-31).
+ * V = 4 x a power of two <= 256; 16-byte aligned rows. */
+int ina_apply_completed_nga(const uint8_t* pkts, size_t npkts, int V, size_t stride,
+                            const uint8_t* actions, uint32_t seq0, const float* local, int k,
+                            double weight_step, float* out, size_t n, uint8_t* acks,
+                            size_t ack_stride, ina_stream_t stream);
 /* C-128 pack (communicator.cc:23-37): npkts x 524-byte packet_t, all words htonl. */
 int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id,
                   uint32_t aggregator_index, int tensor_index, uint8_t* pkts,

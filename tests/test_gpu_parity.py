@@ -409,3 +409,28 @@ def test_quantize_pack_fused_matches_oracle(V, with_base, padded):
     d = (x - base).astype(np.float32) if with_base else x
     want = orc.pack_nga(orc.quantize_i32(d, 16), V, 3, 4, 1, 42, stride=stride)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("V,W", [(256, 8), (32, 3), (128, 4)])
+def test_switch_then_fused_apply_matches_oracle(V, W):
+    """PS side: device switch over W worker streams, then one fused kernel places,
+    dequantises and applies the completed slots; its ack rows free every slot."""
+    o = ops()
+    rng = np.random.default_rng(V * W)
+    n, k, seq0 = 60 * V + 11, 16, 5000
+    local = rng.standard_normal(n).astype(np.float32)
+    q = [rand_i32(rng, n, full=False) for _ in range(W)]
+    stream = torch.cat([o.pack_nga(dev(b), V, w + 1, W, 1, seq0) for w, b in enumerate(q)])
+    stream = stream[torch.randperm(stream.shape[0], device=stream.device)]
+    sw = o.Switch(V, num_slots=16384, switch_id=1, device=DEV)
+    act = sw.process(stream)
+    npk = -(-n // V)
+    acks = torch.zeros((npk, stream.shape[1]), dtype=torch.uint8, device=DEV)
+    out = host(o.apply_completed(stream, act, V, seq0, dev(local), k, 1.0 / (W + 1), acks=acks))
+    S = orc.sum_reduce_i32(q)
+    want = (local + (orc.dequantize_i32(S, k) * np.float32(1.0 / (W + 1))).astype(np.float32)).astype(np.float32)
+    assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
+    assert (host(sw.frag)[(seq0 + np.arange(npk)) % 16384] != 0).all()
+    ack_act = host(sw.process(acks))
+    assert (ack_act == orc.ACT_FWD_ACK).all()
+    assert not host(sw.frag).any()
