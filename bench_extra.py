@@ -144,9 +144,11 @@ def run_extra(dev):
         sw.count.zero_()
         sw.frag.zero_()
         sw.process(stream, acts)
+    # algorithmic bytes: every packet read once, the forwarded (completing) 1/Ws of them
+    # written back, each touched slot's V registers read and written once
     rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort)",
                      _time(sw_round, reps=5, warm=1),
-                     2 * stream.numel() + 2 * npk * V * 4))
+                     stream.numel() + stream.numel() // Ws + 2 * npk * V * 4))
     del stream
 
     # --- end to end: pinned host -> HBM -> reduce -> pinned host -------------------------------

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
                     }
                 }
                 act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
-                rewrite = true;
+                rewrite = act != INA_ACT_DROP || st.write_dropped;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -293,9 +293,11 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run2(ina_switch_state_t st,
                         act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
                     }
                 }
-                u32x4s* pk = reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride);
-                if (lane <= L) pk[lane] = a[b];
-                if (wide && lane == 63) pk[64] = t[b];
+                if (act != INA_ACT_DROP || st.write_dropped) {
+                    u32x4s* pk = reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride);
+                    if (lane <= L) pk[lane] = a[b];
+                    if (wide && lane == 63) pk[64] = t[b];
+                }
                 if (lane == 0) actions[pid[b]] = act;
             }
         }

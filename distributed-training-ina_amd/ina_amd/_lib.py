@@ -41,6 +41,7 @@ class NgaFields(C.Structure):
 
 class SwitchState(C.Structure):
     _fields_ = [("num_slots", C.c_uint32), ("V", C.c_int32), ("switch_id", C.c_int32),
+                ("write_dropped", C.c_int32),
                 ("count", C.c_void_p), ("frag", C.c_void_p), ("regs", C.c_void_p)]
 
 

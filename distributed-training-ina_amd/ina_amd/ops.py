@@ -286,13 +286,16 @@ class Switch:
     """ngaa.p4's aggregator with its registers in HBM (count u8, frag u32, V x u32 per slot)."""
 
     def __init__(self, V: int = 32, num_slots: int = NUM_REGISTER, switch_id: int = 1,
-                 device: str | torch.device = "cuda"):
+                 device: str | torch.device = "cuda", write_dropped: bool = False):
+        """write_dropped=True also rewrites dropped packets with their running sums (what
+        the P4 deparser emits before the drop); the default skips those unobservable writes."""
         self.V, self.num_slots, self.switch_id = V, num_slots, switch_id
         self.count = torch.zeros(num_slots, dtype=torch.uint8, device=device)
         self.frag = torch.zeros(num_slots, dtype=torch.int32, device=device)
         self.regs = torch.zeros((num_slots, V), dtype=torch.int32, device=device)
-        self._state = _lib.SwitchState(num_slots, V, switch_id, self.count.data_ptr(),
-                                       self.frag.data_ptr(), self.regs.data_ptr())
+        self._state = _lib.SwitchState(num_slots, V, switch_id, int(write_dropped),
+                                       self.count.data_ptr(), self.frag.data_ptr(),
+                                       self.regs.data_ptr())
         self._scratch = None
 
     def process(self, pkts: torch.Tensor, actions: torch.Tensor | None = None) -> torch.Tensor:

@@ -164,13 +164,17 @@ int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id,
 /* ---- packet-stream switch (ngaa.p4:120-196 restated on the device) -------------
  * State lives in device memory: count[num_slots] u8, frag[num_slots] u32,
  * regs[num_slots*V] u32 (zero-initialise once, like the P4 registers).  Packets are
- * processed in array order per slot (different slots are independent); packets are
- * rewritten in place (running sum, collision bit) and actions[p] gets INA_ACT_*.
+ * processed in array order per slot (different slots are independent); forwarded
+ * packets are rewritten in place (slot sum, collision bit; dropped ones too when
+ * write_dropped) and actions[p] gets INA_ACT_*.
  * scratch: device buffer of ina_switch_scratch_bytes(npkts, num_slots) bytes.  */
 typedef struct ina_switch_state {
     uint32_t num_slots;
     int32_t V;
     int32_t switch_id;  /* the switch_check entry (ngaa.p4:27-37); -1 = none */
+    int32_t write_dropped; /* 1: also rewrite packets that are dropped (their running sums,
+                              as the P4 deparser would); 0: leave them -- a dropped packet
+                              is never observed, and skipping saves (W-1)/W of the writes */
     uint8_t* count;
     uint32_t* frag;
     uint32_t* regs;

@@ -56,7 +56,7 @@ def test_error_codes_without_device_work():
     assert lib.ina_pack_c128(None, -1, 1, 0, 0, None, None) == _lib.INA_EINVAL
     prm = _lib.NgaParams(1, 2, 0, 1, 0, 1, 16384, 32)
     assert lib.ina_pack_nga(None, 64, ctypes.byref(prm), None, None, 100, None) == _lib.INA_EINVAL
-    st = _lib.SwitchState(16384, 512, 1, None, None, None)
+    st = _lib.SwitchState(16384, 512, 1, 0, None, None, None)
     assert lib.ina_switch_process(ctypes.byref(st), None, 1, 2064, None, None, None) == _lib.INA_EINVAL
 
 
