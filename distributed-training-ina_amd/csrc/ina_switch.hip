@@ -328,6 +328,42 @@ static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
 
 }  // namespace ina
 
+namespace ina {
+
+// 3. ipRoute (ngaa.p4:39-61): exact match of each forwarded packet's IPv4 destination
+//    against a table of <= 256 rows staged in LDS; every lane of a wave scans the same
+//    row at once (LDS broadcast), first hit wins, a miss is the default drop.
+__global__ __launch_bounds__(256) void k_route_ipv4(const uint8_t* __restrict__ actions,
+                                                    const uint32_t* __restrict__ dst_ip,
+                                                    uint32_t dst_default, size_t npk,
+                                                    const uint32_t* __restrict__ keys,
+                                                    const int32_t* __restrict__ ports, int nent,
+                                                    int32_t* __restrict__ egress) {
+    __shared__ uint32_t k_s[INA_ROUTE_MAX];
+    __shared__ int32_t p_s[INA_ROUTE_MAX];
+    for (int i = threadIdx.x; i < nent; i += blockDim.x) {
+        k_s[i] = keys[i];
+        p_s[i] = ports[i];
+    }
+    __syncthreads();
+    for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < npk;
+         p += (size_t)gridDim.x * blockDim.x) {
+        int32_t port = INA_PORT_DROP;
+        if (actions[p] != INA_ACT_DROP) {
+            const uint32_t d = dst_ip ? dst_ip[p] : dst_default;
+            for (int i = 0; i < nent; ++i) {
+                if (k_s[i] == d) {
+                    port = p_s[i];
+                    break;
+                }
+            }
+        }
+        egress[p] = port;
+    }
+}
+
+}  // namespace ina
+
 using namespace ina;
 
 extern "C" {
@@ -376,6 +412,21 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
                            v_out, actions);
     }
     if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch run launch%s", "");
+    return INA_OK;
+}
+
+int ina_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_default,
+                   size_t npk, const uint32_t* keys, const int32_t* ports, int nent,
+                   int32_t* egress, ina_stream_t stream) {
+    if (nent < 0 || nent > INA_ROUTE_MAX)
+        return set_error(INA_EINVAL, "route table must have 0..256 rows%s", "");
+    if (npk == 0) return INA_OK;
+    if (!actions || !egress || (nent > 0 && (!keys || !ports)))
+        return set_error(INA_EINVAL, "null pointer%s", "");
+    unsigned g = (unsigned)std::min<size_t>((npk + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_route_ipv4, dim3(g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       actions, dst_ip, dst_default, npk, keys, ports, nent, egress);
+    if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "route launch%s", "");
     return INA_OK;
 }
 

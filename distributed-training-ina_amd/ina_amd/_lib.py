@@ -22,6 +22,8 @@ C128_VALUES = 128
 C128_BYTES = 524
 FLAG_OVERFLOW, FLAG_ACK, FLAG_COLLISION, FLAG_RESEND = 0x80, 0x40, 0x20, 0x10
 ACT_DROP, ACT_FWD_AGG, ACT_FWD_COLLISION, ACT_FWD_ACK, ACT_FWD_OTHER = range(5)
+ROUTE_MAX = 256                    # ipRoute size, ngaa.p4:59
+PORT_DROP, PORT_NONE = -1, -2
 
 
 class InaError(RuntimeError):
@@ -69,6 +71,7 @@ SIGNATURES = {
     "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],
     "ina_switch_scratch_bytes": [_sz, _u32],
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
+    "ina_route_ipv4": [_vp, _vp, _u32, _sz, _vp, _vp, _i, _vp, _vp],
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],
     "send_gradients": [C.POINTER(C.c_uint32), _i, _u32, _i, _u32, _i],
     "ina_send_gradients_fd": [_i, _vp, _i, _u32, _i, _u32, _i],

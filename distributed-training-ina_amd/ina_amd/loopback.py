@@ -23,7 +23,7 @@ import time
 
 import torch
 
-from . import _lib, ops, ps
+from . import _lib, control, ops, ps
 from .nic import PacketRing, send_device_packets
 
 
@@ -31,14 +31,23 @@ class SwitchStandIn:
     """The Tofino's role on the PS GPU for one bucket of n values from W workers."""
 
     def __init__(self, n: int, W: int, V: int = 256, switch_id: int = 1, device="cuda",
-                 num_slots: int | None = None):
+                 num_slots: int | None = None, cp: control.ControlPlane | None = None,
+                 ps_addr: str = "127.0.0.1", ps_port: int = 0):
+        """cp: the switch's tables (switch_check / ipRoute, ngaa.p4:27-61); by default
+        switch_id aggregates and the PS address routes to ps_port.  Only completed
+        slots that ipRoute sends to ps_port reach the PS."""
         self.n, self.W, self.V = n, W, V
+        if cp is None:
+            cp = control.ControlPlane()
+            cp.Ingress.switch_check.add_with_set_agg(switch_id)
+            cp.Ingress.ipRoute.add_with_ipv4_forward(ps_addr, dst_mac=0, port=ps_port)
+        self.cp, self.ps_addr, self.ps_port = cp, control.ip2int(ps_addr), ps_port
         self.npk = -(-n // V)
         # The Tofino pool is 16,384 slots (config.p4:5) and the reference sends a whole
         # bucket with index = seq mod 16384 (DataManager.py:119), so buckets of more
         # packets collide there.  HBM holds a pool for the whole bucket instead.
         self.num_slots = num_slots or max(_lib.NUM_REGISTER, self.npk)
-        self.switch = ops.Switch(V, self.num_slots, switch_id, device)
+        self.switch = cp.make_switch(V, self.num_slots, device)
         self.ring = PacketRing(W * self.npk, V, device)
         self.out = torch.empty(self.npk * V, dtype=torch.int32, device=device)
         self.acks = torch.zeros((self.npk, self.ring.stride), dtype=torch.uint8, device=device)
@@ -54,10 +63,14 @@ class SwitchStandIn:
             got += r
         pk = self.ring.to_device(got)
         act = self.switch.process(pk)
-        ndone = int((act == _lib.ACT_FWD_AGG).sum())
+        eg = self.cp.egress(act, dst_default=self.ps_addr)       # ipRoute, ngaa.p4:39-61
+        routed = torch.where(eg == self.ps_port, act, torch.zeros_like(act))
+        ndone = int((routed == _lib.ACT_FWD_AGG).sum())
         if ndone != self.npk:
             bad = int((act == _lib.ACT_FWD_COLLISION).sum())
-            raise RuntimeError(f"{ndone}/{self.npk} slots completed ({bad} collisions)")
+            raise RuntimeError(f"{ndone}/{self.npk} slots completed and routed to the PS "
+                               f"({bad} collisions)")
+        act = routed
         return pk, act
 
     def aggregate_apply(self, sock, seq0: int, local: torch.Tensor, k: int, weight_step: float,

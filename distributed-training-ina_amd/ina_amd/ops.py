@@ -313,6 +313,32 @@ class Switch:
         return actions
 
 
+def route_ipv4(actions: torch.Tensor, keys: torch.Tensor, ports: torch.Tensor,
+               dst_ip: torch.Tensor | None = None, dst_default: int = 0,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """ipRoute (ngaa.p4:39-61) for a switched batch: int32 egress port per packet
+    (PORT_DROP for ingress drops, drop rows and table misses; PORT_NONE for NoAction).
+    keys uint32-valued int32/int64 IPv4 addresses and ports int32 (<= 256 rows, on the
+    device); dst_ip per packet (int32 view of the u32 address) or None for dst_default."""
+    _req(actions, torch.uint8, "actions")
+    _req(keys, torch.int32, "keys")
+    _req(ports, torch.int32, "ports")
+    if keys.numel() != ports.numel() or keys.numel() > _lib.ROUTE_MAX:
+        raise ValueError(f"route table: keys/ports must match and hold <= {_lib.ROUTE_MAX} rows")
+    if dst_ip is not None:
+        _req(dst_ip, torch.int32, "dst_ip")
+        if dst_ip.numel() != actions.numel():
+            raise ValueError("dst_ip must hold one address per packet")
+    out = torch.empty(actions.numel(), dtype=torch.int32, device=actions.device) if out is None else out
+    _req(out, torch.int32, "out")
+    _same_device(actions, keys, ports, out, *([dst_ip] if dst_ip is not None else []))
+    check(load().ina_route_ipv4(actions.data_ptr(), None if dst_ip is None else dst_ip.data_ptr(),
+                                dst_default & 0xFFFFFFFF, actions.numel(), keys.data_ptr(),
+                                ports.data_ptr(), keys.numel(), out.data_ptr(), _stream(actions)),
+          "route_ipv4")
+    return out
+
+
 def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                nontemporal: bool | None = None, reduce_blocks: int | None = None,
                stream_blocks: int | None = None, combine_blocks: int | None = None):

@@ -183,6 +183,23 @@ size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots);
 int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
                        uint8_t* actions, void* scratch, ina_stream_t stream);
 
+/* ---- ipRoute (ngaa.p4:39-61, entries as bfrt/setup.py:85-95 installs them) -------
+ * Every packet the ingress does not drop (actions FWD_AGG, FWD_COLLISION, FWD_ACK,
+ * FWD_OTHER) leaves through ipRoute: an exact match on the IPv4 destination.
+ * The table is n_entries <= INA_ROUTE_MAX rows (keys[i] = IPv4 address, host order;
+ * ports[i] = egress port >= 0 for ipv4_forward, INA_PORT_DROP for the drop action,
+ * INA_PORT_NONE for NoAction); the first matching row wins and a miss takes the
+ * default action, drop.  egress[p] = the port, INA_PORT_DROP for packets the ingress
+ * or the table dropped, INA_PORT_NONE for NoAction.  dst_ip is a per-packet device
+ * array, or NULL for dst_default on every packet (a stand-in without IP headers).
+ * keys, ports, actions, egress: device memory. */
+#define INA_ROUTE_MAX 256        /* ipRoute size = 1<<8, ngaa.p4:59 */
+#define INA_PORT_DROP (-1)
+#define INA_PORT_NONE (-2)
+int ina_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_default,
+                   size_t npkts, const uint32_t* keys, const int32_t* ports, int n_entries,
+                   int32_t* egress, ina_stream_t stream);
+
 /* ---- integrity ------------------------------------------------------------------
  * *out_dev (device u32) = sum_i x[i]*(2i+1) mod 2^32 (linear in x, so the checksum
  * of a reduce equals the wrapped sum of the input checksums). */

@@ -468,3 +468,22 @@ int orc_switch_run(orc_switch_t* sw, uint8_t* pkts, size_t np, size_t stride, ui
     }
     return 0;
 }
+
+/* ipRoute (ngaa.p4:39-61): every packet the ingress forwards -- aggregation done
+ * (170-172), ack (130-131), collision (177-180), other switch (184-186) -- is
+ * matched exactly on hdr.ipv4.dst_addr; ipv4_forward sets the egress port (46-51),
+ * a drop entry or a table miss (default_action = drop, 60) drops it, NoAction
+ * leaves the port unset.  Ingress drops (175) never reach the table. */
+void orc_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_default,
+                    size_t np, const uint32_t* keys, const int32_t* ports, int nent,
+                    int32_t* egress) {
+    for (size_t p = 0; p < np; ++p) {
+        int32_t port = ORC_PORT_DROP;
+        if (actions[p] != ORC_ACT_DROP) {
+            uint32_t d = dst_ip ? dst_ip[p] : dst_default;
+            for (int i = 0; i < nent; ++i)
+                if (keys[i] == d) { port = ports[i]; break; }
+        }
+        egress[p] = port;
+    }
+}

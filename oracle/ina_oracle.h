@@ -92,6 +92,11 @@ int orc_cpu_packetise_aggregate(const int32_t* const* bufs, int W, size_t n, int
                                 int32_t* out, double* seconds);
 uint32_t orc_checksum_i32(const int32_t* x, size_t n);
 int orc_switch_run(orc_switch_t* sw, uint8_t* pkts, size_t np, size_t stride, uint8_t* actions);
+#define ORC_PORT_DROP (-1)
+#define ORC_PORT_NONE (-2)
+void orc_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_default,
+                    size_t np, const uint32_t* keys, const int32_t* ports, int nent,
+                    int32_t* egress);
 
 #ifdef __cplusplus
 }

@@ -84,6 +84,7 @@ def lib():
             "orc_cpu_packetise_aggregate": [vp, i, sz, i, i, vp, C.POINTER(C.c_double)],
             "orc_checksum_i32": [vp, sz],
             "orc_c128_bitmap": [i],
+            "orc_route_ipv4": [vp, vp, u32, sz, vp, vp, i, vp],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -92,6 +93,7 @@ def lib():
         L.orc_checksum_i32.restype = C.c_uint32
         L.orc_c128_bitmap.restype = C.c_uint32
         L.orc_switch_free.restype = None
+        L.orc_route_ipv4.restype = None
     return _lib
 
 
@@ -291,3 +293,19 @@ def cpu_packetise_aggregate(bufs, V: int, threads: int = 1):
 def checksum_i32(x: np.ndarray) -> int:
     x = np.ascontiguousarray(x, np.int32)
     return int(lib().orc_checksum_i32(_p(x), x.size))
+
+
+PORT_DROP, PORT_NONE = -1, -2
+
+
+def route_ipv4(actions: np.ndarray, table, dst_ip=None, dst_default: int = 0) -> np.ndarray:
+    """ipRoute (ngaa.p4:39-61) over a batch: table = [(ipv4 int, port | PORT_DROP |
+    PORT_NONE), ...]; returns egress int32[np] (PORT_DROP for dropped packets)."""
+    actions = np.ascontiguousarray(actions, np.uint8)
+    keys = np.ascontiguousarray([k for k, _ in table] or [0], np.uint32)
+    ports = np.ascontiguousarray([v for _, v in table] or [0], np.int32)
+    dst = None if dst_ip is None else np.ascontiguousarray(dst_ip, np.uint32)
+    egress = np.empty(actions.size, np.int32)
+    lib().orc_route_ipv4(_p(actions), None if dst is None else _p(dst), dst_default & 0xFFFFFFFF,
+                         actions.size, _p(keys), _p(ports), len(table), _p(egress))
+    return egress
