@@ -10,7 +10,6 @@
 // the padded packet, byte-offset payload words at 15 + 4j extracted with
 // v_alignbyte), rewritten there (running sum, collision bit) and stored back.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
@@ -35,22 +34,220 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x138, 0xF, 0xF, false);
 }
 
+// threadIdx.x >> 6 is the same in every lane of a wave, but the compiler cannot see
+// that: without readfirstlane everything derived from it (chunk/window loops, the
+// slot state machine) is treated as divergent -- VGPR state and exec-mask branches.
+__device__ __forceinline__ int wave_in_block() {
+    return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+
 __device__ __forceinline__ uint32_t rd_be32(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
 
-// 1. keys: aggregator slot of each packet, or num_slots (sorts last) for packets
-//    that are not this switch's (switch_check miss, ngaa.p4:27-37,184-186)
-__global__ void k_switch_keys(const uint8_t* __restrict__ pkts, size_t npk, size_t stride,
-                              uint32_t num_slots, int switch_id, uint32_t* __restrict__ keys,
-                              uint32_t* __restrict__ ids, uint8_t* __restrict__ actions) {
-    size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= npk) return;
-    const uint8_t* pk = pkts + p * stride;
-    bool mine = switch_id >= 0 && pk[10] == (uint8_t)switch_id;
-    keys[p] = mine ? rd_be32(pk + 6) % num_slots : num_slots;
-    ids[p] = (uint32_t)p;
-    if (!mine) actions[p] = INA_ACT_FWD_OTHER;
+// ---- stable LSD radix sort of (slot key, packet id) --------------------------------
+// The P4 registers see each slot's packets in arrival order, so the batch is grouped by
+// slot with a STABLE sort.  Keys need only ceil(log2(num_slots + 1)) bits (18 at 2^17
+// slots), so the sort is 1-3 digit passes of <= 9 bits.  A block owns a chunk of 4096
+// consecutive items, its wave w the w-th 1024 of them (16 rounds of 64, in order; all
+// loads issued up front):
+//   hist     the chunk's digit counts (LDS) -> cnt[digit][chunk]
+//   colscan  one wave per digit: exclusive scan along the chunks (in place) + the
+//            digit's total
+//   scatter  base(digit, chunk, wave) = exclusive scan of the digit totals + the
+//            column prefix + the counts of the chunk's earlier waves; inside a round an
+//            item's rank is the number of lower lanes with the same digit (ballots over
+//            its bits)
+// so order is kept across rounds, lanes, waves and chunks.  (rocprim's radix sort ran
+// ~130 us at 819,200 pairs: 10 dependent merge passes, or onesweep + lookback resets.)
+constexpr int kRsMaxBits = 9;
+constexpr int kRsBins = 1 << kRsMaxBits;     // 512
+constexpr int kRsRounds = 16;
+constexpr int kRsBlock = 256;
+constexpr int kRsWaves = kRsBlock / 64;
+constexpr int kRsWaveItems = 64 * kRsRounds;            // 1024
+constexpr int kRsChunk = kRsWaves * kRsWaveItems;       // 4096 items per block
+
+__device__ __forceinline__ unsigned long long lanes_with_digit(uint32_t d, int bits, bool valid) {
+    unsigned long long m = __ballot(valid);
+    for (int b = 0; b < bits; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const unsigned long long mb = __ballot(bit);
+        m &= bit ? mb : ~mb;
+    }
+    return m;
+}
+
+// inclusive wave64 scan in DPP (no LDS round trips): Hillis-Steele inside each 16-lane
+// row with row_shr:1,2,4,8 (bound_ctrl: lanes shifted in from outside the row read 0),
+// then row_bcast:15 adds row r-1's last lane into rows 1 and 3 and row_bcast:31 adds
+// lane 31 into rows 2 and 3 (GFX9 DPP; disabled rows keep old = 0)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
+// 1. keys: aggregator slot of each packet, or num_slots (sorts last) for packets that
+//    are not this switch's (switch_check miss, ngaa.p4:27-37,184-186); fused with the
+//    first digit pass's chunk histogram.
+__global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restrict__ pkts,
+                                                          size_t npk, size_t stride,
+                                                          uint32_t num_slots, int switch_id,
+                                                          uint32_t* __restrict__ keys,
+                                                          uint8_t* __restrict__ actions, int bits,
+                                                          uint32_t* __restrict__ hist, size_t nch) {
+    __shared__ uint32_t h[kRsBins];
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const size_t c = blockIdx.x;
+    const uint32_t nb = 1u << bits;
+    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) h[d] = 0;
+    __syncthreads();
+    const size_t p0 = c * kRsChunk + (size_t)wv * kRsWaveItems + (size_t)lane;
+    uint32_t idx[kRsRounds], sid[kRsRounds];
+    if ((stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0) {   // header bytes 4..11
+#pragma unroll
+        for (int r = 0; r < kRsRounds; ++r) {
+            const size_t p = p0 + (size_t)r * 64;
+            uint32_t w1 = 0, w2 = 0;
+            if (p < npk) {
+                const uint32_t* pk = reinterpret_cast<const uint32_t*>(pkts + p * stride);
+                w1 = pk[1];
+                w2 = pk[2];
+            }
+            idx[r] = __builtin_bswap32((w1 >> 16) | (w2 << 16));
+            sid[r] = (w2 >> 16) & 0xFFu;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < kRsRounds; ++r) {
+            const size_t p = p0 + (size_t)r * 64;
+            idx[r] = p < npk ? rd_be32(pkts + p * stride + 6) : 0u;
+            sid[r] = p < npk ? pkts[p * stride + 10] : 0u;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kRsRounds; ++r) {
+        const size_t p = p0 + (size_t)r * 64;
+        if (p < npk) {
+            const bool mine = switch_id >= 0 && sid[r] == (uint32_t)(uint8_t)switch_id;
+            const uint32_t key = mine ? idx[r] % num_slots : num_slots;
+            keys[p] = key;
+            if (!mine) actions[p] = INA_ACT_FWD_OTHER;
+            atomicAdd(&h[key & (nb - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
+}
+
+// later passes: chunk histogram of digit (key >> shift)
+__global__ __launch_bounds__(kRsBlock) void k_rs_hist(const uint32_t* __restrict__ keys, size_t n,
+                                                      int shift, int bits,
+                                                      uint32_t* __restrict__ hist, size_t nch) {
+    __shared__ uint32_t h[kRsBins];
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const size_t c = blockIdx.x;
+    const uint32_t nb = 1u << bits;
+    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) h[d] = 0;
+    __syncthreads();
+    const size_t i0 = c * kRsChunk + (size_t)wv * kRsWaveItems + (size_t)lane;
+    uint32_t k[kRsRounds];
+#pragma unroll
+    for (int r = 0; r < kRsRounds; ++r) k[r] = i0 + (size_t)r * 64 < n ? keys[i0 + (size_t)r * 64] : 0u;
+#pragma unroll
+    for (int r = 0; r < kRsRounds; ++r)
+        if (i0 + (size_t)r * 64 < n) atomicAdd(&h[(k[r] >> shift) & (nb - 1)], 1u);
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
+}
+
+// one wave per digit: cnt[d][*] -> exclusive prefix along the chunks, totals[d]
+__global__ __launch_bounds__(kRsBlock) void k_rs_colscan(uint32_t* __restrict__ hist, size_t nch,
+                                                         uint32_t nb, uint32_t* __restrict__ totals) {
+    const int lane = threadIdx.x & 63;
+    const size_t d = (size_t)blockIdx.x * kRsWaves + wave_in_block();
+    if (d >= nb) return;
+    uint32_t* row = hist + d * nch;
+    uint32_t run = 0;
+    for (size_t c0 = 0; c0 < nch; c0 += 64) {
+        const size_t c = c0 + (size_t)lane;
+        const uint32_t x = c < nch ? row[c] : 0u;
+        const uint32_t inc = wave_incl_scan(x);
+        if (c < nch) row[c] = run + inc - x;
+        run += __builtin_amdgcn_readlane(inc, 63);
+    }
+    if (lane == 0) totals[d] = run;
+}
+
+// scatter: out position = base(digit, chunk, wave) + items of that digit the wave already
+// placed + rank among this round's lanes with the same digit
+template <bool kIds>
+__global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restrict__ kin,
+                                                         const uint32_t* __restrict__ vin,
+                                                         uint32_t* __restrict__ kout,
+                                                         uint32_t* __restrict__ vout, size_t n,
+                                                         int shift, int bits,
+                                                         const uint32_t* __restrict__ colpref,
+                                                         const uint32_t* __restrict__ totals,
+                                                         size_t nch) {
+    __shared__ uint32_t base[kRsWaves][kRsBins];   // per-wave counts, then per-wave bases
+    __shared__ uint32_t dbase[kRsBins];
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const size_t c = blockIdx.x;
+    const uint32_t nb = 1u << bits;
+    const size_t i0 = c * kRsChunk + (size_t)wv * kRsWaveItems + (size_t)lane;
+    uint32_t k[kRsRounds], v[kRsRounds];
+#pragma unroll
+    for (int r = 0; r < kRsRounds; ++r) {
+        const size_t i = i0 + (size_t)r * 64;
+        k[r] = i < n ? kin[i] : 0u;
+        v[r] = kIds ? (i < n ? vin[i] : 0u) : (uint32_t)i;
+    }
+    for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
+    if (wv == 0) {                                   // digit bases: scan of the totals
+        uint32_t carry = 0;
+        for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
+            const uint32_t d = d0 + (uint32_t)lane;
+            const uint32_t t = d < nb ? totals[d] : 0u;
+            const uint32_t inc = wave_incl_scan(t);
+            if (d < nb) dbase[d] = carry + inc - t;
+            carry += __builtin_amdgcn_readlane(inc, 63);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kRsRounds; ++r)              // this wave's digit counts
+        if (i0 + (size_t)r * 64 < n) atomicAdd(&base[wv][(k[r] >> shift) & (nb - 1)], 1u);
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) {
+        uint32_t b = dbase[d] + colpref[d * nch + c];
+#pragma unroll
+        for (int w = 0; w < kRsWaves; ++w) {
+            const uint32_t cw = base[w][d];
+            base[w][d] = b;
+            b += cw;
+        }
+    }
+    __syncthreads();
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < kRsRounds; ++r) {
+        if (i0 - (size_t)lane + (size_t)r * 64 >= n) break;      // wave-uniform
+        const bool valid = i0 + (size_t)r * 64 < n;
+        const uint32_t d = (k[r] >> shift) & (nb - 1);
+        const unsigned long long pm = lanes_with_digit(d, bits, valid);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(pm & below);
+        const uint32_t b0 = base[wv][d];
+        if (valid) {
+            kout[b0 + rank] = k[r];
+            vout[b0 + rank] = v[r];
+            if (rank == 0) base[wv][d] = b0 + (uint32_t)__builtin_popcountll(pm);
+        }
+    }
 }
 
 // 2. one wave per slot segment of the sorted stream
@@ -62,7 +259,7 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
                                                          uint8_t* __restrict__ actions) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kSwBlock / 64][kMaxStride];
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
+    const int wv = wave_in_block();
     const size_t pos = (size_t)blockIdx.x * (kSwBlock / 64) + wv;
     if (pos >= npk) return;
     const uint32_t slot = keys[pos];
@@ -172,14 +369,21 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
 // once, runs the P4 state machine over them in arrival order with the slot's
 // registers in VGPRs, re-encodes and stores each packet.  Each wave owns windows of
 // 64 sorted positions and runs the segments that start in them.
-constexpr int kB = 8;
+#ifndef INA_SWITCH_BATCH
+#define INA_SWITCH_BATCH 8
+#endif
+constexpr int kB = INA_SWITCH_BATCH;         // packets of a segment loaded at once
+// occupancy target of k_switch_run2 (waves per SIMD); 4 fits its registers, 5 spills 4
+#ifndef INA_SWITCH_WAVES
+#define INA_SWITCH_WAVES 4
+#endif
 
 __device__ __forceinline__ uint32_t enc_lo(uint32_t prev, uint32_t v) {
     // LE dword: BE bytes 1..3 of prev followed by BE byte 0 of v
     return (__builtin_bswap32(prev) >> 8) | (v & 0xFF000000u);
 }
 
-__global__ __launch_bounds__(kSwBlock) void k_switch_run2(ina_switch_state_t st,
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SWITCH_WAVES, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts, size_t npk,
                                                           size_t stride,
                                                           const uint32_t* __restrict__ keys,
@@ -190,7 +394,7 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run2(ina_switch_state_t st,
     const int L = V >> 2;                       // lanes holding values
     const bool vl = lane < L;
     const bool wide = L == 64;                  // tail chunk lives in lane 63's t[]
-    const size_t wave = ((size_t)blockIdx.x * kSwBlock + threadIdx.x) >> 6;
+    const size_t wave = (size_t)blockIdx.x * (kSwBlock / 64) + wave_in_block();
     const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
     const uint32_t NS = st.num_slots;
     // each wave takes windows of 64 sorted positions and processes the segments that
@@ -223,22 +427,49 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run2(ina_switch_state_t st,
                 }
             }
         }
-        uint32_t cnt = st.count[slot];
-        uint32_t frag = st.frag[slot];
+        // slot state: count and frag are wave-uniform (SGPRs, scalar branches); the V
+        // registers are loaded only if a packet adds to them before any overwrite
+        // (count_reg == 1 overwrites, processor.p4:16-21), i.e. rarely
+        uint32_t cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
+        uint32_t frag = __builtin_amdgcn_readfirstlane(st.frag[slot]);
         u32x4s reg = {0u, 0u, 0u, 0u};
-        if (vl) reg = *reinterpret_cast<const u32x4s*>(st.regs + (size_t)slot * V + 4 * lane);
+        bool have_reg = false;
         for (size_t q0 = pos; q0 < end; q0 += kB) {
             const int nb = (int)((end - q0) < (size_t)kB ? (end - q0) : (size_t)kB);
-            u32x4s a[kB], t[kB];
+            u32x4s a[kB];
             uint32_t pid[kB];
+            // packet ids first (no load in the common in-window case; one coalesced load
+            // otherwise), so the kB packet loads below issue back to back with no
+            // s_waitcnt between them
+            if (q0 + (size_t)nb <= w0 + 64) {
+                const int o = (int)(q0 - w0);
+#pragma unroll
+                for (int b = 0; b < kB; ++b)
+                    pid[b] = b < nb ? __builtin_amdgcn_readlane(idw, o + b < 64 ? o + b : 63) : 0u;
+            } else {
+                const uint32_t my = lane < nb ? ids[q0 + (size_t)lane] : 0u;
+#pragma unroll
+                for (int b = 0; b < kB; ++b) pid[b] = __builtin_amdgcn_readlane(my, b);
+            }
+            // tail chunks 64 (V = 256 only): lane b holds packet b's, 4 VGPRs for the whole
+            // batch instead of 4 per packet; lane 63 takes them by readlane when it needs
+            // them.  Issued first, so packet 0 can start once its own load is back.
+            // Every load is unconditional (slots past the batch re-read packet 0, lanes past
+            // L re-read chunk 0) so no load sits in a branch: the compiler's wait counting
+            // stays exact and packet b waits only for its own data.
+#pragma unroll
+            for (int b = 1; b < kB; ++b) pid[b] = b < nb ? pid[b] : pid[0];
+            u32x4s tl = {0u, 0u, 0u, 0u};
+            if (wide) {
+                uint32_t mypid = pid[0];
+#pragma unroll
+                for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
+                tl = reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride)[64];
+            }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
-                const size_t q = q0 + (size_t)b;
-                pid[b] = b >= nb ? 0u
-                         : (q < w0 + 64 ? __builtin_amdgcn_readlane(idw, (int)(q - w0)) : ids[q]);
                 const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[b] * stride);
-                a[b] = (b < nb && lane <= L) ? pk[lane] : u32x4s{0u, 0u, 0u, 0u};
-                t[b] = (b < nb && wide && lane == 63) ? pk[64] : u32x4s{0u, 0u, 0u, 0u};
+                a[b] = pk[lane <= L ? lane : 0];
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
@@ -247,56 +478,80 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run2(ina_switch_state_t st,
                                h2 = __builtin_amdgcn_readlane(a[b].z, 0),
                                h3 = __builtin_amdgcn_readlane(a[b].w, 0);
                 const uint32_t hcount = h1 & 0xFFu, flags = (h1 >> 8) & 0xFFu;
-                const uint32_t frag_in = __builtin_bswap32((h2 >> 24) | (h3 << 8));
+                // keep the state machine scalar (SGPRs + scalar branches)
+                const uint32_t frag_in =
+                    __builtin_amdgcn_readfirstlane(__builtin_bswap32((h2 >> 24) | (h3 << 8)));
                 uint8_t act;
                 if ((flags >> 6) & 1u) {                     // ack: reset_id (fragcheck.p4:26-31)
                     frag = 0;
                     act = INA_ACT_FWD_ACK;
                 } else {
                     if (frag == 0) frag = frag_in;           // write_read_id (fragcheck.p4:14-24)
-                    if (frag != frag_in) {                   // collision (ngaa.p4:177-181)
-                        if (lane == 0) a[b].y |= (uint32_t)INA_FLAG_COLLISION << 8;
-                        act = INA_ACT_FWD_COLLISION;
+                    if (frag != frag_in) {                   // collision (ngaa.p4:177-181):
+                        act = INA_ACT_FWD_COLLISION;         // only the flag byte changes
+                        if (lane == 0)
+                            reinterpret_cast<uint32_t*>(pkts + (size_t)pid[b] * stride)[1] =
+                                a[b].y | ((uint32_t)INA_FLAG_COLLISION << 8);
                     } else {
                         cnt = (cnt + 1u) & 0xFFu;            // read_add_count (ngaa.p4:66-78)
                         if (cnt == hcount) cnt = 0;
+                        cnt = __builtin_amdgcn_readfirstlane(cnt);
                         const bool first = cnt == 1u;
                         u32x4s c;                            // chunk l+1
                         c.x = from_next_lane(a[b].x); c.y = from_next_lane(a[b].y);
                         c.z = from_next_lane(a[b].z); c.w = from_next_lane(a[b].w);
-                        if (wide && lane == 63) c = t[b];
+                        uint32_t tw = 0;                     // old byte 1039 (padding) for the tail
+                        if (wide) {
+                            const uint32_t tx = __builtin_amdgcn_readlane(tl.x, b);
+                            const uint32_t ty = __builtin_amdgcn_readlane(tl.y, b);
+                            const uint32_t tz = __builtin_amdgcn_readlane(tl.z, b);
+                            tw = __builtin_amdgcn_readlane(tl.w, b);
+                            if (lane == 63) c = u32x4s{tx, ty, tz, tw};
+                        }
                         u32x4s v;                            // values 4l..4l+3
                         v.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.x, a[b].w, 3));
                         v.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.y, c.x, 3));
                         v.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.z, c.y, 3));
                         v.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.w, c.z, 3));
-                        reg = first ? v : reg + v;           // processor.p4:16-21
-                        // out_value -> payload (processor.p4:22)
-                        u32x4s p;                            // lane l-1's values
-                        p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
-                        p.z = from_prev_lane(reg.z); p.w = from_prev_lane(reg.w);
-                        if (lane == 0) {
-                            a[b].w = (a[b].w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
-                        } else if (lane <= L) {
-                            a[b].x = enc_lo(p.x, p.y);
-                            a[b].y = enc_lo(p.y, p.z);
-                            a[b].z = enc_lo(p.z, p.w);
-                            a[b].w = lane < L ? enc_lo(p.w, reg.x)
-                                              : ((__builtin_bswap32(p.w) >> 8) | (a[b].w & 0xFF000000u));
+                        if (first) {                         // processor.p4:16-21
+                            reg = v;
+                        } else if (have_reg) {
+                            reg += v;
+                        } else {                             // adds to a stored register:
+                            reg = vl ? *reinterpret_cast<const u32x4s*>(   // load it now
+                                           st.regs + (size_t)slot * V + 4 * lane)
+                                     : u32x4s{0u, 0u, 0u, 0u};
+                            reg += v;
                         }
-                        if (wide && lane == 63) {            // tail chunk 64 from lane 63's values
-                            t[b].x = enc_lo(reg.x, reg.y);
-                            t[b].y = enc_lo(reg.y, reg.z);
-                            t[b].z = enc_lo(reg.z, reg.w);
-                            t[b].w = (__builtin_bswap32(reg.w) >> 8) | (t[b].w & 0xFF000000u);
-                        }
+                        have_reg = true;
                         act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
+                        if (act != INA_ACT_DROP || st.write_dropped) {
+                            // out_value -> payload (processor.p4:22): chunk c from lane c-1
+                            u32x4s p;
+                            p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
+                            p.z = from_prev_lane(reg.z); p.w = from_prev_lane(reg.w);
+                            u32x4s e = a[b];
+                            if (lane == 0) {
+                                e.w = (e.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                            } else {
+                                e.x = enc_lo(p.x, p.y);
+                                e.y = enc_lo(p.y, p.z);
+                                e.z = enc_lo(p.z, p.w);
+                                e.w = lane < L ? enc_lo(p.w, reg.x)
+                                               : ((__builtin_bswap32(p.w) >> 8) | (e.w & 0xFF000000u));
+                            }
+                            if (lane <= L)
+                                reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride)[lane] = e;
+                            if (wide && lane == 63) {        // tail chunk 64 from lane 63's values
+                                u32x4s o;
+                                o.x = enc_lo(reg.x, reg.y);
+                                o.y = enc_lo(reg.y, reg.z);
+                                o.z = enc_lo(reg.z, reg.w);
+                                o.w = (__builtin_bswap32(reg.w) >> 8) | (tw & 0xFF000000u);
+                                reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride)[64] = o;
+                            }
+                        }
                     }
-                }
-                if (act != INA_ACT_DROP || st.write_dropped) {
-                    u32x4s* pk = reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride);
-                    if (lane <= L) pk[lane] = a[b];
-                    if (wide && lane == 63) pk[64] = t[b];
                 }
                 if (lane == 0) actions[pid[b]] = act;
             }
@@ -305,7 +560,7 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run2(ina_switch_state_t st,
             st.count[slot] = (uint8_t)cnt;
             st.frag[slot] = frag;
         }
-        if (vl) *reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane) = reg;
+        if (have_reg && vl) *reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane) = reg;
         }
     }
 }
@@ -318,12 +573,24 @@ static int end_bit_for(uint32_t num_slots) {
     return b;   // sentinel value num_slots fits
 }
 
+struct SortPlan {
+    int passes, bits;
+    size_t nch, hist_elems;
+};
+
+static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
+    SortPlan p;
+    const int eb = end_bit_for(num_slots);
+    p.passes = (eb + kRsMaxBits - 1) / kRsMaxBits;
+    p.bits = (eb + p.passes - 1) / p.passes;
+    p.nch = (npk + kRsChunk - 1) / kRsChunk;
+    p.hist_elems = ((size_t)1 << p.bits) * p.nch;
+    return p;
+}
+
 static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
-    size_t tb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)npk, 0,
-                                       end_bit_for(num_slots));
-    return tb;
+    const SortPlan p = sort_plan(npk, num_slots);
+    return align_up(p.hist_elems * 4, 256) + align_up((size_t)kRsBins * 4, 256);
 }
 
 }  // namespace ina
@@ -390,26 +657,44 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
     uint32_t* k_out = reinterpret_cast<uint32_t*>(base + arr);
     uint32_t* v_in = reinterpret_cast<uint32_t*>(base + 2 * arr);
     uint32_t* v_out = reinterpret_cast<uint32_t*>(base + 3 * arr);
-    void* temp = base + 4 * arr;
-    size_t tb = sort_temp_bytes(npk, st->num_slots);
+    const SortPlan sp = sort_plan(npk, st->num_slots);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(base + 4 * arr);
+    uint32_t* totals = reinterpret_cast<uint32_t*>(base + 4 * arr + align_up(sp.hist_elems * 4, 256));
+    const unsigned gc = (unsigned)sp.nch;
+    const uint32_t nb = 1u << sp.bits;
+    const unsigned gd = (nb + kRsWaves - 1) / kRsWaves;
 
-    unsigned g = (unsigned)((npk + 255) / 256);
-    hipLaunchKernelGGL(k_switch_keys, dim3(g), dim3(256), 0, s, pkts, npk, stride, st->num_slots,
-                       st->switch_id, k_in, v_in, actions);
+    hipLaunchKernelGGL(k_switch_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts, npk, stride,
+                       st->num_slots, st->switch_id, k_in, actions, sp.bits, hist, sp.nch);
     if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
-    if (hipcub::DeviceRadixSort::SortPairs(temp, tb, k_in, k_out, v_in, v_out, (int)npk, 0,
-                                           end_bit_for(st->num_slots), s) != hipSuccess)
-        return set_error(INA_EHIP, "switch radix sort%s", "");
+    // digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
+    uint32_t *kc = k_in, *vc = v_in, *kn = k_out, *vn = v_out;
+    for (int pass = 0; pass < sp.passes; ++pass) {
+        const int shift = pass * sp.bits;
+        if (pass > 0)
+            hipLaunchKernelGGL(k_rs_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits,
+                               hist, sp.nch);
+        hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, hist, sp.nch, nb, totals);
+        if (pass == 0)
+            hipLaunchKernelGGL(k_rs_scatter<false>, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn,
+                               vn, npk, shift, sp.bits, hist, totals, sp.nch);
+        else
+            hipLaunchKernelGGL(k_rs_scatter<true>, dim3(gc), dim3(kRsBlock), 0, s, kc, vc, kn, vn,
+                               npk, shift, sp.bits, hist, totals, sp.nch);
+        if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
+        std::swap(kc, kn);
+        std::swap(vc, vn);
+    }
     const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
                       st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
     if (fast) {
         unsigned gr = (unsigned)std::min<size_t>((npk + kSwBlock - 1) / kSwBlock, 2048);
-        hipLaunchKernelGGL(k_switch_run2, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, k_out,
-                           v_out, actions);
+        hipLaunchKernelGGL(k_switch_run2, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,
+                           vc, actions);
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
-        hipLaunchKernelGGL(k_switch_run, dim3(gw), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, k_out,
-                           v_out, actions);
+        hipLaunchKernelGGL(k_switch_run, dim3(gw), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,
+                           vc, actions);
     }
     if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch run launch%s", "");
     return INA_OK;

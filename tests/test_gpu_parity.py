@@ -336,7 +336,7 @@ def test_send_gradients_fd_over_socketpair():
 # --------------------------------------------------------------------------------------
 # device packet-stream switch vs the oracle's P4 restatement
 # --------------------------------------------------------------------------------------
-def make_stream(rng, V, nslots_used, W, num_slots, collide=0.05, ack=0.1, other=0.05):
+def make_stream(rng, V, nslots_used, W, num_slots, collide=0.05, ack=0.1, other=0.05, stride=None):
     pk = []
     for s in range(nslots_used):
         frag = int(rng.integers(0, 4)) if rng.random() < 0.1 else 1000 + s
@@ -348,7 +348,7 @@ def make_stream(rng, V, nslots_used, W, num_slots, collide=0.05, ack=0.1, other=
             flags = orc.FLAG_ACK if rng.random() < ack else 0
             sw = 2 if rng.random() < other else 1
             p = orc.pack_nga(vals, V, w + 1, deg, sw, 0, flags=flags,
-                             stride=ops().nga_stride(V))[0].copy()
+                             stride=stride or ops().nga_stride(V))[0].copy()
             p[6:10] = np.frombuffer(idx.to_bytes(4, "big"), np.uint8)
             p[11:15] = np.frombuffer(f.to_bytes(4, "big"), np.uint8)
             pk.append(p)
@@ -356,16 +356,26 @@ def make_stream(rng, V, nslots_used, W, num_slots, collide=0.05, ack=0.1, other=
     return pk[rng.permutation(len(pk))] if rng.random() < 0.5 else pk
 
 
+# (V, num_slots, W, slots used per batch, stride): multi-chunk batches (> 1024 packets),
+# 1-3 digit passes of the slot sort (num_slots 4 .. 2^18), segments longer than a wave
+# (small pools), and the LDS-staged path (V % 4 != 0 or a stride that is not 16-aligned)
+SWITCH_CASES = [(32, 16384, 4, 60, None), (32, 64, 8, 60, None), (256, 128, 3, 60, None),
+                (128, 16, 16, 60, None), (32, 4096, 8, 300, None), (64, 1 << 18, 4, 400, None),
+                (32, 4, 16, 40, None), (33, 256, 4, 60, None), (32, 512, 4, 80, 143),
+                (256, 1024, 8, 200, None)]
+
+
 @pytest.mark.parametrize("write_dropped", [True, False])
-@pytest.mark.parametrize("V,num_slots,W", [(32, 16384, 4), (32, 64, 8), (256, 128, 3), (128, 16, 16)])
-def test_switch_stream_matches_oracle(V, num_slots, W, write_dropped):
-    rng = np.random.default_rng(V + num_slots + W)
+@pytest.mark.parametrize("V,num_slots,W,used,stride", SWITCH_CASES)
+def test_switch_stream_matches_oracle(V, num_slots, W, used, stride, write_dropped):
+    rng = np.random.default_rng(V + num_slots + W + used)
     o = ops()
+    stride = stride or o.nga_stride(V)
     sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=write_dropped)
     sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
     for rnd in range(3):                  # state persists across batches
-        stream = make_stream(rng, V, 60, W, num_slots)
-        want_pk, want_act = sw_orc.run(stream, stride=o.nga_stride(V))
+        stream = make_stream(rng, V, used, W, num_slots, stride=stride)
+        want_pk, want_act = sw_orc.run(stream, stride=stride)
         d = dev(stream)
         act = sw_dev.process(d)
         assert np.array_equal(host(act), want_act), rnd

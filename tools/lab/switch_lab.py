@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of device-switch builds (experiment only): every tools/lab/libina_*.so
+given on the command line runs ina_switch_process on the same 8-worker NGA-256 stream
+(config-3 bucket), timed with HIP events; actions and forwarded packets must agree."""
+import ctypes as C
+import os
+import statistics
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
+from ina_amd import _lib, ops  # noqa: E402
+
+n, W, V = int(os.environ.get("N", 26_214_400)), 8, 256
+slots = 1 << 17
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(1)
+bufs = [torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
+        for _ in range(W)]
+src = torch.cat([ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots) for w, b in enumerate(bufs)])
+del bufs
+npk, stride = src.shape
+
+
+class Variant:
+    def __init__(self, path):
+        self.name = os.path.basename(path)
+        self.lib = C.CDLL(path)
+        for nm in ("ina_switch_process", "ina_switch_scratch_bytes"):
+            getattr(self.lib, nm).argtypes = _lib.SIGNATURES[nm]
+        self.lib.ina_switch_scratch_bytes.restype = C.c_size_t
+        self.count = torch.zeros(slots, dtype=torch.uint8, device=dev)
+        self.frag = torch.zeros(slots, dtype=torch.int32, device=dev)
+        self.regs = torch.zeros((slots, V), dtype=torch.int32, device=dev)
+        self.st = _lib.SwitchState(slots, V, 1, 0, self.count.data_ptr(), self.frag.data_ptr(),
+                                   self.regs.data_ptr())
+        self.scratch = torch.empty(self.lib.ina_switch_scratch_bytes(npk, slots), dtype=torch.uint8,
+                                   device=dev)
+        self.acts = torch.empty(npk, dtype=torch.uint8, device=dev)
+        self.times = []
+
+    def run(self, pk):
+        self.count.zero_()
+        self.frag.zero_()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        rc = self.lib.ina_switch_process(C.byref(self.st), pk.data_ptr(), npk, stride,
+                                         self.acts.data_ptr(), self.scratch.data_ptr(),
+                                         torch.cuda.current_stream().cuda_stream)
+        b.record()
+        assert rc == 0, rc
+        return a, b
+
+
+vs = [Variant(p) for p in sys.argv[1:]]
+work = src.clone()
+ref = None
+for v in vs:                                   # correctness: identical outputs
+    work.copy_(src)
+    v.run(work)
+    torch.cuda.synchronize()
+    out = (v.acts.clone(), work[v.acts == 1].clone())
+    if ref is None:
+        ref = out
+    else:
+        assert torch.equal(ref[0], out[0]) and torch.equal(ref[1], out[1]), v.name
+for r in range(int(os.environ.get("ROUNDS", 8))):
+    for v in vs:
+        evs = []
+        for _ in range(3):
+            work.copy_(src)
+            evs.append(v.run(work))
+        torch.cuda.synchronize()
+        v.times += [a.elapsed_time(b) * 1e3 for a, b in evs]
+for v in vs:
+    print(f"{v.name:24s} median {statistics.median(v.times):8.1f} us  min {min(v.times):8.1f} us")
