@@ -132,6 +132,18 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
     t1, _ = res[1]
     W = len(bufs_host)
     ok = bool(np.array_equal(outP, gpu_out_sample))
+    # the PS's own float update, aggregate() as launch.py:42-52 writes it, in torch on the
+    # same host cores over fp32 buffers of the same sample size
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(7)
+    paras = [torch.randn(n, generator=g) * 1e-2 for _ in range(W)]
+    local = torch.randn(n, generator=g)
+    ta = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        local += (1.0 / (W + 1)) * 1.0 * sum([p - local for p in paras])
+        ta.append(time.perf_counter() - t0)
+    t_agg = statistics.median(ta)
     return {
         "value": round(W * n * 4 / tP / 1e9, 3), "unit": "GB/s", "cores": threads,
         "kind": "port",
@@ -141,6 +153,7 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
                    f"registers, ngaa.p4:120-196) -> PS ack, median of 3, {threads} threads split "
                    f"as communicator.py:133-157"),
         "value_1core": round(W * n * 4 / t1 / 1e9, 3),
+        "torch_aggregate_GBps": round(W * n * 4 / t_agg / 1e9, 3),
         "affinity_cores": cores,
         "matches_gpu": ok,
     }

@@ -62,11 +62,17 @@ __device__ __forceinline__ uint32_t rd_be32(const uint8_t* p) {
 // ~130 us at 819,200 pairs: 10 dependent merge passes, or onesweep + lookback resets.)
 constexpr int kRsMaxBits = 9;
 constexpr int kRsBins = 1 << kRsMaxBits;     // 512
-constexpr int kRsRounds = 16;
-constexpr int kRsBlock = 256;
+#ifndef INA_RS_WAVES
+#define INA_RS_WAVES 4
+#endif
+#ifndef INA_RS_ROUNDS
+#define INA_RS_ROUNDS 16
+#endif
+constexpr int kRsRounds = INA_RS_ROUNDS;
+constexpr int kRsBlock = 64 * INA_RS_WAVES;
 constexpr int kRsWaves = kRsBlock / 64;
-constexpr int kRsWaveItems = 64 * kRsRounds;            // 1024
-constexpr int kRsChunk = kRsWaves * kRsWaveItems;       // 4096 items per block
+constexpr int kRsWaveItems = 64 * kRsRounds;
+constexpr int kRsChunk = kRsWaves * kRsWaveItems;       // items per block (4096)
 
 __device__ __forceinline__ unsigned long long lanes_with_digit(uint32_t d, int bits, bool valid) {
     unsigned long long m = __ballot(valid);
