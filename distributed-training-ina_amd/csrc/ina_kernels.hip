@@ -60,8 +60,11 @@ static std::atomic<int> g_reduce_blocks{0};
 static std::atomic<int> g_unroll{4};
 // the other chunk_loop<4> streaming kernels
 static std::atomic<int> g_stream_blocks{8192};
-// PS combine kernels (W+2 streams)
-static std::atomic<int> g_combine_blocks{512};
+// PS combine kernels (W+2 streams), measured per kernel (bench_extra grid sweeps, two
+// sessions): the fp32 combine runs best at 256 workgroups (6.6-6.7 TB/s vs 6.0 at 512),
+// the INA combine (quantiser in the loop, more VGPRs) at 512 (256 drops it to 4.3 TB/s)
+static std::atomic<int> g_combine_blocks{256};
+static std::atomic<int> g_combine_ina_blocks{512};
 static std::atomic<int> g_nontemporal{1};
 
 static inline unsigned grid_for(size_t work_items, int per_thread, int cap_override = 0) {
@@ -142,13 +145,11 @@ static inline bool slot_ballot_ok(int V) {
 
 
 // Cross-lane moves by one lane as DPP row moves (measured on gfx950, tools/lab/dpp_lab.hip):
-// wave_shl:1 -> lane i reads lane i+1 (lane 63 keeps its own value); wave_shr:1 -> lane i
-// reads lane i-1 (lane 0 keeps its own).  One VALU op instead of an LDS ds_bpermute.
+// wave_shl:1 -> lane i reads lane i+1 (lane 63 keeps its own value); wave_shr:1 (0x138,
+// used inline with an explicit `old` for lane 0) -> lane i reads lane i-1.  One VALU op
+// instead of an LDS ds_bpermute.
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x130, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x138, 0xF, 0xF, false);
 }
 
 template <int W>
@@ -805,71 +806,51 @@ __device__ __forceinline__ void nga_store_header(const NgaFieldsDev& f, size_t p
     if (f.frag_id) f.frag_id[p] = bswap((w2 >> 24) | (w3 << 8));
 }
 
-// vector unpack: thread per (packet, 4 values); reads two aligned 16-byte chunks
-__global__ __launch_bounds__(kBlock) void k_unpack_nga_vec(const uint8_t* __restrict__ pkts,
-                                                           size_t npk, int V, size_t pstride,
-                                                           NgaFieldsDev f, int32_t* __restrict__ vals) {
-    const size_t gs = (size_t)gridDim.x * kBlock;
-    const uint32_t groups = (uint32_t)(V / 4);
-    const size_t total = npk * groups;
-    for (size_t g = (size_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += gs) {
-        size_t p = g / groups;
-        uint32_t j4 = (uint32_t)(g - p * groups);
-        const u32x4* src = reinterpret_cast<const u32x4*>(pkts + p * pstride + 16 * (size_t)j4);
-        u32x4 a = __builtin_nontemporal_load(src);
-        u32x4 b = __builtin_nontemporal_load(src + 1);
-        if (j4 == 0) nga_store_header(f, p, a.x, a.y, a.z, a.w);
-        if (vals) {
-            // value t starts at byte 15+4t of the 32 loaded bytes: words (3+t, 4+t)
-            u32x4 o;
-            o.x = bswap(__builtin_amdgcn_alignbyte(b.x, a.w, 3));
-            o.y = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
-            o.z = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
-            o.w = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
-            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(vals + p * (size_t)V) + j4);
-        }
-    }
-}
+// flat unpack: the packet buffer is read as one contiguous array of 16-byte chunks
+// (C = stride/16 per packet), thread per chunk, U chunks in flight per thread.  Chunk c
+// >= 1 of a packet holds dwords 4c..4c+3 and yields values 4c-4..4c-1 (value j = byte
+// 3 of dword 3+j, then bytes 0..2 of dword 4+j: one v_perm each), so the only
+// cross-lane input is the previous chunk's dword 3 (DPP wave_shr:1; lane 0 of a wave
+// loads it).  Chunk 0 is the header (SoA fields); chunks past V/4 are padding.  Reads
+// and writes are both fully contiguous streams.
+constexpr uint32_t kSelBE = 0x03040506u;   // perm(hi, lo): {lo.b3, hi.b0, hi.b1, hi.b2} as a BE word
 
-// wave-shuffle unpack (values only): L = V/4 lanes per packet (L a power of two
-// <= 64); lane j loads 16-byte chunk j once and takes chunk j+1 from its neighbour
-// (DPP wave_shl:1); the packet's last lane loads the tail chunk L itself.  Each
-// thread handles U wave-tiles per iteration (U loads in flight, as in chunk_loop).
 template <int U>
-__global__ __launch_bounds__(kBlock) void k_unpack_nga_shfl(const uint8_t* __restrict__ pkts,
-                                                            size_t npk, int log2L, size_t pstride,
-                                                            int32_t* __restrict__ vals) {
-    const size_t gs = (size_t)gridDim.x * kBlock;
-    const uint32_t L = 1u << log2L;
-    const size_t total = npk << log2L;
+__global__ __launch_bounds__(kBlock) void k_unpack_nga_flat(const uint8_t* __restrict__ pkts,
+                                                            uint32_t C, uint32_t L, uint32_t nch,
+                                                            NgaFieldsDev f, int hdr,
+                                                            int32_t* __restrict__ vals, uint32_t V) {
+    const uint32_t gs = gridDim.x * kBlock;
     const int lane = threadIdx.x & 63;
-    const size_t wave0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) & ~(size_t)63;
-    for (size_t base = wave0; base < total; base += U * gs) {
-        u32x4 a[U], t[U];
-        size_t g[U];
+    const uint32_t wave0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
+    const u32x4* ch = reinterpret_cast<const u32x4*>(pkts);
+    for (uint32_t base = wave0; base < nch; base += U * gs) {
+        u32x4 a[U];
+        uint32_t pw0[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            g[u] = base + u * gs + (size_t)lane;
-            const size_t p = g[u] >> log2L;
-            const uint32_t j = (uint32_t)(g[u] & (L - 1));
-            const u32x4* pk = reinterpret_cast<const u32x4*>(pkts + p * pstride);
-            a[u] = g[u] < total ? __builtin_nontemporal_load(pk + j) : u32x4{0u, 0u, 0u, 0u};
-            t[u] = (g[u] < total && j == L - 1) ? __builtin_nontemporal_load(pk + L)
-                                               : u32x4{0u, 0u, 0u, 0u};
+            const uint32_t t = base + u * gs + (uint32_t)lane;
+            a[u] = t < nch ? __builtin_nontemporal_load(ch + t) : u32x4{0u, 0u, 0u, 0u};
+            pw0[u] = 0u;
+            if (lane == 0 && t > 0 && t < nch) pw0[u] = reinterpret_cast<const uint32_t*>(ch + t)[-1];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            u32x4 b;
-            b.x = from_next_lane(a[u].x); b.y = from_next_lane(a[u].y);
-            b.z = from_next_lane(a[u].z); b.w = from_next_lane(a[u].w);
-            if ((g[u] & (L - 1)) == L - 1) b = t[u];
-            if (g[u] < total) {
+            const uint32_t t = base + u * gs + (uint32_t)lane;
+            const uint32_t pw = (uint32_t)__builtin_amdgcn_update_dpp((int)pw0[u], (int)a[u].w, 0x138,
+                                                                      0xF, 0xF, false);
+            if (t >= nch) continue;
+            const uint32_t p = t / C, c = t - p * C;
+            if (c == 0) {
+                if (hdr) nga_store_header(f, p, a[u].x, a[u].y, a[u].z, a[u].w);
+            } else if (c <= L && vals) {
                 u32x4 o;
-                o.x = bswap(__builtin_amdgcn_alignbyte(b.x, a[u].w, 3));
-                o.y = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
-                o.z = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
-                o.w = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
-                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(vals) + g[u]);
+                o.x = __builtin_amdgcn_perm(a[u].x, pw, kSelBE);
+                o.y = __builtin_amdgcn_perm(a[u].y, a[u].x, kSelBE);
+                o.z = __builtin_amdgcn_perm(a[u].z, a[u].y, kSelBE);
+                o.w = __builtin_amdgcn_perm(a[u].w, a[u].z, kSelBE);
+                __builtin_nontemporal_store(
+                    o, reinterpret_cast<u32x4*>(vals + (size_t)p * V) + (c - 1));
             }
         }
     }
@@ -880,8 +861,9 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_shfl(const uint8_t* __res
 // DataManager.py:116-130), dequantise and apply the update
 //     out[slot*V + j] = local[..] + ws * ((float)sum * 2^-k)
 // (aggregate()'s update with the switch's integer sum, launch.py:46-50), and write the
-// slot's PS ack header (is_ack=1, fragcheck.p4:26-31) into ack row `slot`.  Same lane
-// layout as k_unpack_nga_shfl: L = V/4 lanes per packet.
+// slot's PS ack header (is_ack=1, fragcheck.p4:26-31) into ack row `slot`.  L = V/4
+// lanes per packet: lane j loads 16-byte chunk j once and takes chunk j+1 from its
+// neighbour (DPP wave_shl:1); the packet's last lane loads the tail chunk L itself.
 __global__ __launch_bounds__(kBlock) void k_apply_completed_nga(
         const uint8_t* __restrict__ pkts, size_t npk, int log2L, size_t pstride,
         const uint8_t* __restrict__ actions, uint32_t seq0, size_t nslots,
@@ -936,8 +918,7 @@ __global__ __launch_bounds__(kBlock) void k_apply_completed_nga(
     }
 }
 
-// header fields, one thread per packet (coalesced SoA stores); pairs with the
-// values-only k_unpack_nga_shfl
+// header fields only (no values asked for), one thread per packet (coalesced SoA stores)
 __global__ __launch_bounds__(kBlock) void k_unpack_nga_hdr(const uint8_t* __restrict__ pkts,
                                                            size_t npk, size_t pstride,
                                                            NgaFieldsDev f) {
@@ -1092,6 +1073,7 @@ int ina_set_tuning(int key, int value) {
         case 3: if (value < 0) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
         case 4: if (value < 1) return INA_EINVAL; g_stream_blocks = value; return INA_OK;
         case 5: if (value < 1) return INA_EINVAL; g_combine_blocks = value; return INA_OK;
+        case 6: if (value < 1) return INA_EINVAL; g_combine_ina_blocks = value; return INA_OK;
         default: return INA_EINVAL;
     }
 }
@@ -1286,7 +1268,7 @@ int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W,
     if (int rc = fill_pack(pk, paras, W, al)) return rc;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = al && aligned16(local) && aligned16(out);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_combine_blocks);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_combine_ina_blocks);
     hipStream_t s = hs(stream);
     float sc = ldexpf(1.0f, k), inv = ldexpf(1.0f, -k), ws = (float)weight_step;
     switch (W) {
@@ -1324,19 +1306,28 @@ int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
     if (fields) f = NgaFieldsDev{fields->bitmap, fields->count, fields->flags, fields->index,
                                  fields->switch_id, fields->frag_id};
     hipStream_t s = hs(stream);
-    int log2L = -1;
-    if (V % 4 == 0 && V / 4 <= 64 && ((V / 4) & (V / 4 - 1)) == 0)
-        for (log2L = 0; (1 << log2L) < V / 4; ++log2L) {}
-    if (log2L >= 0 && pstride % 16 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
+    if (vals && V % 4 == 0 && pstride % 16 == 0 && aligned16(pkts) && aligned16(vals)) {
+        // flat chunk stream; 32-bit chunk indices, so huge batches go in packet ranges
+        const size_t C = pstride / 16;
+        const size_t per = ((size_t)1 << 31) / C;
+        for (size_t p0 = 0; p0 < npk; p0 += per) {
+            const size_t np = npk - p0 < per ? npk - p0 : per;
+            NgaFieldsDev fo = f;
+            if (fo.bitmap) fo.bitmap += p0;
+            if (fo.count) fo.count += p0;
+            if (fo.flags) fo.flags += p0;
+            if (fo.index) fo.index += p0;
+            if (fo.switch_id) fo.switch_id += p0;
+            if (fo.frag_id) fo.frag_id += p0;
+            hipLaunchKernelGGL(k_unpack_nga_flat<4>, dim3(grid_for(np * C, 4, g_stream_blocks)),
+                               dim3(kBlock), 0, s, pkts + p0 * pstride, (uint32_t)C, (uint32_t)(V / 4),
+                               (uint32_t)(np * C), fo, fields ? 1 : 0, vals + p0 * (size_t)V,
+                               (uint32_t)V);
+        }
+    } else if (!vals && pstride % 16 == 0 && aligned16(pkts)) {
         if (fields)
             hipLaunchKernelGGL(k_unpack_nga_hdr, dim3(grid_for(npk, 1)), dim3(kBlock), 0, s, pkts, npk,
                                pstride, f);
-        if (vals)
-            hipLaunchKernelGGL(k_unpack_nga_shfl<4>, dim3(grid_for(npk * (size_t)(V / 4), 4, g_stream_blocks)),
-                               dim3(kBlock), 0, s, pkts, npk, log2L, pstride, vals);
-    } else if (pstride % 16 == 0 && V % 4 == 0 && aligned16(pkts) && (!vals || aligned16(vals))) {
-        hipLaunchKernelGGL(k_unpack_nga_vec, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
-                           s, pkts, npk, V, pstride, f, vals);
     } else {
         hipLaunchKernelGGL(k_unpack_nga_scalar, dim3(grid_for(npk * ((size_t)V + 1), 1)), dim3(kBlock),
                            0, s, pkts, npk, V, pstride, f, vals);

@@ -341,11 +341,12 @@ def route_ipv4(actions: torch.Tensor, keys: torch.Tensor, ports: torch.Tensor,
 
 def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                nontemporal: bool | None = None, reduce_blocks: int | None = None,
-               stream_blocks: int | None = None, combine_blocks: int | None = None):
+               stream_blocks: int | None = None, combine_blocks: int | None = None,
+               combine_ina_blocks: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
-    measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the PS
-    combine kernels; unroll is the sum-reduce's 16-byte chunks per worker per thread."""
+    measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
+    PS combine, combine_ina_blocks the INA-semantics combine; unroll is the sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")
@@ -353,6 +354,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(4, int(stream_blocks)), "set_tuning")
     if combine_blocks is not None:
         check(lib.ina_set_tuning(5, int(combine_blocks)), "set_tuning")
+    if combine_ina_blocks is not None:
+        check(lib.ina_set_tuning(6, int(combine_ina_blocks)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

@@ -211,6 +211,67 @@ __global__ __launch_bounds__(B) void v_copy(Ptrs in, u32x4* __restrict__ out, si
     for (size_t i = tid; i < n4; i += stride) __builtin_nontemporal_store(ldnt(in.p[0] + i), out + i);
 }
 
+// v10: product form with nt loads but a default-policy store (the fp32 PS combine, which
+// streams 6.7 TB/s, stores that way); v12: nt loads, store through a buffer resource with
+// cache-policy aux bits (AUXS)
+template <int W, int U, int B>
+__global__ __launch_bounds__(B) void v_gs_plainst(Ptrs in, u32x4* __restrict__ out, size_t n4) {
+    const size_t tid = (size_t)blockIdx.x * B + threadIdx.x, stride = (size_t)gridDim.x * B;
+    size_t i = tid;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        u32x4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = ldnt(in.p[0] + i + u * stride);
+#pragma unroll
+        for (int w = 1; w < W; ++w)
+#pragma unroll
+            for (int u = 0; u < U; ++u) a[u] += ldnt(in.p[w] + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) out[i + u * stride] = a[u];
+    }
+    for (; i < n4; i += stride) {
+        u32x4 a = ldnt(in.p[0] + i);
+#pragma unroll
+        for (int w = 1; w < W; ++w) a += ldnt(in.p[w] + i);
+        out[i] = a;
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// v11: buffer loads/stores, 4 GiB windows per stream, AUXL/AUXS cache-policy bits
+template <int W, int U, int B, int AUXL, int AUXS>
+__global__ __launch_bounds__(B) void v_gs_buf(Ptrs in, u32x4* __restrict__ out, size_t n4) {
+    __amdgpu_buffer_rsrc_t r[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) r[w] = mk_rsrc(in.p[w], (uint32_t)(n4 * 16));
+    __amdgpu_buffer_rsrc_t ro = mk_rsrc(out, (uint32_t)(n4 * 16));
+    const uint32_t tid = blockIdx.x * B + threadIdx.x, stride = gridDim.x * B;
+    uint32_t i = tid;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        u32x4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r[0], (i + u * stride) * 16, 0, AUXL));
+#pragma unroll
+        for (int w = 1; w < W; ++w)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                a[u] += __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r[w], (i + u * stride) * 16, 0, AUXL));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, a[u]), ro, (i + u * stride) * 16, 0, AUXS);
+    }
+    for (; i < n4; i += stride) {
+        u32x4 a = ldnt(in.p[0] + i);
+#pragma unroll
+        for (int w = 1; w < W; ++w) a += ldnt(in.p[w] + i);
+        __builtin_nontemporal_store(a, out + i);
+    }
+}
+
 using Kfn = void (*)(Ptrs, u32x4*, size_t);
 
 template <int B>
@@ -225,6 +286,8 @@ static Kfn pick(int variant, int U) {
         case 7: return v_copy<B>;
         case 8: return U == 2 ? v_gs_sb<8, 2, B, 0> : v_gs_sb<8, 4, B, 0>;
         case 9: return U == 2 ? v_gs_sb<8, 2, B, 1> : v_gs_sb<8, 4, B, 1>;
+        case 10: return U == 2 ? v_gs_plainst<8, 2, B> : v_gs_plainst<8, 4, B>;
+        case 11: return U == 2 ? v_gs_buf<8, 4, B, 2, 2> : U == 4 ? v_gs_buf<8, 4, B, 2, 0> : U == 5 ? v_gs_buf<8, 4, B, 2, 1> : v_gs_buf<8, 4, B, 0, 2>;
     }
     return nullptr;
 }

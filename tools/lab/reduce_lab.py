@@ -46,6 +46,16 @@ if FOCUS == "sched":
         configs.append(("loads_first_schedbarrier", 9, U, B, G))
     for G in (1024, 2048):
         configs.append(("readonly8", 6, 1, 256, G))
+elif FOCUS == "store":
+    # U field: variant 11 packs the cache-policy pair: 2 = nt/nt, 4 = nt/default,
+    # 5 = nt/sc0, 6 = default/nt
+    for B, G in ((256, 512), (512, 256), (256, 1024), (512, 512)):
+        configs.append(("gridstride", 1, 4, B, G))
+        configs.append(("plainstore", 10, 4, B, G))
+        for aux in (2, 4, 5, 6):
+            configs.append((f"buf{aux}", 11, aux, B, G))
+    for G in (1024, 2048):
+        configs.append(("readonly8", 6, 1, 256, G))
 elif FOCUS == "grid":
     for U, B, G in itertools.product((2, 4, 6, 8), (128, 256, 512, 768, 1024), (128, 192, 256, 320, 384, 512, 768)):
         configs.append(("gridstride", 1, U, B, G))
