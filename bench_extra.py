@@ -167,5 +167,22 @@ def run_extra(dev):
         hout.copy_(o3, non_blocking=True)
     t = _time(e2e, reps=5, warm=1)
     rows.append(_row("end-to-end pinned H2D(8x100MiB)+reduce+D2H", t, (W3 + 1) * n3 * 4,
-                     aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2)))
+                     aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2), note="one stream, phases in sequence"))
+    # the product path: chunked, H2D / reduce / D2H pipelined (ina_sum_reduce_host_i32)
+    want = hout.clone()
+    for h2d in (1, 2):
+        for chunk in (1 << 18, 1 << 20, 1 << 22):
+            ops.set_tuning(h2d_streams=h2d)
+            scratch = torch.empty(ops.load().ina_host_reduce_scratch_bytes(W3, chunk),
+                                  dtype=torch.uint8, device=dev)
+            hp = torch.empty(n3, dtype=torch.int32).pin_memory()
+
+            def piped():
+                ops.sum_reduce_host(hosts, out=hp, chunk=chunk, scratch=scratch)
+            t = _time(piped, reps=5, warm=1)
+            rows.append(_row(f"end-to-end pipelined host reduce (h2d streams {h2d}, chunk {chunk})", t,
+                             (W3 + 1) * n3 * 4, aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2),
+                             matches=bool(torch.equal(hp, want))))
+            del scratch
+    ops.set_tuning(h2d_streams=2)
     return {"rows": rows, "sweep": sweep, "grid_sweeps": gsweep}

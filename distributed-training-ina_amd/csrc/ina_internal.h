@@ -14,6 +14,7 @@ struct PtrPack {
 };
 
 int set_error(int code, const char* fmt, const char* detail);
+int set_h2d_streams(int v);   // ina_host.cpp
 
 }  // namespace ina
 

@@ -1074,6 +1074,7 @@ int ina_set_tuning(int key, int value) {
         case 4: if (value < 1) return INA_EINVAL; g_stream_blocks = value; return INA_OK;
         case 5: if (value < 1) return INA_EINVAL; g_combine_blocks = value; return INA_OK;
         case 6: if (value < 1) return INA_EINVAL; g_combine_ina_blocks = value; return INA_OK;
+        case 7: return set_h2d_streams(value);
         default: return INA_EINVAL;
     }
 }

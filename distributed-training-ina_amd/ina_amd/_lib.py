@@ -73,13 +73,16 @@ SIGNATURES = {
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
     "ina_route_ipv4": [_vp, _vp, _u32, _sz, _vp, _vp, _i, _vp, _vp],
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],
+    "ina_host_reduce_scratch_bytes": [_i, _sz],
+    "ina_sum_reduce_host_i32": [_vp, _i, _vp, _sz, _sz, _vp, _vp],
     "send_gradients": [C.POINTER(C.c_uint32), _i, _u32, _i, _u32, _i],
     "ina_send_gradients_fd": [_i, _vp, _i, _u32, _i, _u32, _i],
     "ina_send_packets_fd": [_i, _vp, _sz, _sz, _sz, _u32],
     "ina_recv_packets_fd": [_i, _vp, _sz, _sz, _sz, _i, _vp],
 }
 _RESTYPE = {"ina_version": C.c_char_p, "ina_last_error_string": C.c_char_p,
-            "ina_switch_scratch_bytes": C.c_size_t, "send_gradients": None}
+            "ina_switch_scratch_bytes": C.c_size_t, "ina_host_reduce_scratch_bytes": C.c_size_t,
+            "send_gradients": None}
 
 _lib = None
 _lock = threading.Lock()

@@ -7,6 +7,7 @@ These are the kernels that replace the reference's CPU / switch arithmetic:
   quantize / dequantize      float_to_int / int_to_float (absent; DataManager.py:9,
                              NGAPacket.py:5) -- build-defined, see DESIGN.md
   sum_reduce                 the switch's per-slot Processor add (processor.p4:14-24)
+  sum_reduce_host            the same from/to host memory, PCIe copies pipelined (PS ingest)
   quantize_reduce            worker quantise fused with the aggregator sum
   pack_nga / unpack_nga      DataManager._send_data (DataManager.py:111-165) and the
                              PS-side parse (NGAPacket.py:62-143), headers.p4 layout
@@ -108,6 +109,37 @@ def sum_reduce(bufs, out: torch.Tensor | None = None) -> torch.Tensor:
     _req(out, torch.int32, "out")
     arr = ptr_array([b.data_ptr() for b in bufs])
     check(load().ina_sum_reduce_i32(arr, len(bufs), out.data_ptr(), n, _stream(out)), "sum_reduce")
+    return out
+
+
+def sum_reduce_host(bufs, out: torch.Tensor | None = None, chunk: int = 0,
+                    device: torch.device | str | None = None, scratch: torch.Tensor | None = None):
+    """PCIe-inclusive aggregation at the PS: W int32 buckets in HOST memory (pinned for
+    full link speed; what the worker sockets deliver) -> HBM -> the same W-way sum-reduce
+    -> the aggregate back in host memory (`out`, pinned CPU int32), chunked and pipelined
+    over H2D / reduce / D2H (ina_sum_reduce_host_i32).  Returns when `out` is complete."""
+    if isinstance(bufs, torch.Tensor):
+        bufs = list(bufs.unbind(0)) if bufs.dim() > 1 else [bufs]
+    bufs = list(bufs)
+    if not 1 <= len(bufs) <= _lib.MAX_WORKERS:
+        raise ValueError(f"need 1..{_lib.MAX_WORKERS} worker buffers, got {len(bufs)}")
+    n = bufs[0].numel()
+    for i, b in enumerate(bufs):
+        if b.is_cuda or b.dtype != torch.int32 or not b.is_contiguous() or b.numel() != n:
+            raise ValueError(f"bufs[{i}] must be a contiguous host int32 tensor of {n} values")
+    out = torch.empty(n, dtype=torch.int32).pin_memory() if out is None else out
+    if out.is_cuda or out.dtype != torch.int32 or not out.is_contiguous() or out.numel() != n:
+        raise ValueError("out must be a contiguous host int32 tensor")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    lib = load()
+    need = lib.ina_host_reduce_scratch_bytes(len(bufs), chunk)
+    if scratch is None or scratch.numel() < need:
+        scratch = torch.empty(need, dtype=torch.uint8, device=dev)
+    arr = ptr_array([b.data_ptr() for b in bufs])
+    with torch.cuda.device(dev):
+        check(lib.ina_sum_reduce_host_i32(arr, len(bufs), out.data_ptr(), n, chunk,
+                                          scratch.data_ptr(), torch.cuda.current_stream(dev).cuda_stream),
+              "sum_reduce_host")
     return out
 
 
@@ -342,11 +374,12 @@ def route_ipv4(actions: torch.Tensor, keys: torch.Tensor, ports: torch.Tensor,
 def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                nontemporal: bool | None = None, reduce_blocks: int | None = None,
                stream_blocks: int | None = None, combine_blocks: int | None = None,
-               combine_ina_blocks: int | None = None):
+               combine_ina_blocks: int | None = None, h2d_streams: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
-    PS combine, combine_ina_blocks the INA-semantics combine; unroll is the sum-reduce's 16-byte chunks per worker per thread."""
+    PS combine, combine_ina_blocks the INA-semantics combine, h2d_streams the host-ingest
+    pipeline's H2D copy streams (1 or 2); unroll is the sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")
@@ -356,6 +389,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(5, int(combine_blocks)), "set_tuning")
     if combine_ina_blocks is not None:
         check(lib.ina_set_tuning(6, int(combine_ina_blocks)), "set_tuning")
+    if h2d_streams is not None:
+        check(lib.ina_set_tuning(7, int(h2d_streams)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

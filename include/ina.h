@@ -200,6 +200,20 @@ int ina_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_
                    size_t npkts, const uint32_t* keys, const int32_t* ports, int n_entries,
                    int32_t* egress, ina_stream_t stream);
 
+/* ---- PCIe-inclusive aggregation (PS ingest) ----------------------------------------
+ * The PS side of the reference receives each worker's gradients over a socket into host
+ * memory and sums them on the CPU (worker.py:63-79, launch.py:111-130, 42-52).  This
+ * moves W HOST buckets (pinned for full speed) through HBM in chunks of chunk_values
+ * values (0 = 4 Mi; rounded up to a multiple of 64): H2D copies, the W-way sum-reduce
+ * above on `stream`, D2H of the aggregate into host_out, pipelined over a ring of 3
+ * device slots on internal copy streams so both copy directions overlap the reduce.
+ * Bit-identical to ina_sum_reduce_i32.  dev_scratch: device memory (256-byte aligned)
+ * of ina_host_reduce_scratch_bytes(W, chunk_values) bytes.  Synchronous: returns once
+ * host_out holds the aggregate (the PS sends it next). */
+size_t ina_host_reduce_scratch_bytes(int W, size_t chunk_values);
+int ina_sum_reduce_host_i32(const int32_t* const* host_bufs, int W, int32_t* host_out, size_t n,
+                            size_t chunk_values, void* dev_scratch, ina_stream_t stream);
+
 /* ---- integrity ------------------------------------------------------------------
  * *out_dev (device u32) = sum_i x[i]*(2i+1) mod 2^32 (linear in x, so the checksum
  * of a reduce equals the wrapped sum of the input checksums). */

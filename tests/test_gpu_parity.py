@@ -111,6 +111,40 @@ def test_sum_reduce_config3_full_size():
     assert cs == sum(orc.checksum_i32(b) for b in bufs) % 2**32 == orc.checksum_i32(want)
 
 
+# PCIe-inclusive path: host buckets -> HBM -> reduce -> host, chunked over a 3-slot ring
+@pytest.mark.parametrize("W,n,chunk", [(1, 1, 0), (3, 63, 64), (8, 100_003, 4096),
+                                       (8, 100_003, 0), (17, 65_537, 1000), (64, 5000, 128)])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_sum_reduce_host_matches_oracle(W, n, chunk, pinned):
+    rng = np.random.default_rng(W * 31 + n + chunk)
+    bufs = [rand_i32(rng, n) for _ in range(W)]
+    hb = [torch.from_numpy(b) for b in bufs]
+    if pinned:
+        hb = [b.pin_memory() for b in hb]
+    got = ops().sum_reduce_host(hb, chunk=chunk)
+    assert not got.is_cuda
+    assert np.array_equal(got.numpy(), orc.sum_reduce_i32(bufs))
+
+
+@pytest.mark.parametrize("h2d", [1, 2])
+def test_sum_reduce_host_ring_reuse_and_copy_streams(h2d):
+    """Many more chunks than ring slots, both copy-stream settings, called twice with
+    the same scratch: every chunk is bit-exact (slot reuse waits on the right events)."""
+    rng = np.random.default_rng(h2d)
+    W, n = 8, 64 * 1000 + 7
+    bufs = [rand_i32(rng, n) for _ in range(W)]
+    hb = [torch.from_numpy(b).pin_memory() for b in bufs]
+    o = ops()
+    scratch = torch.empty(o.load().ina_host_reduce_scratch_bytes(W, 64), dtype=torch.uint8, device=DEV)
+    try:
+        o.set_tuning(h2d_streams=h2d)
+        for _ in range(2):
+            got = o.sum_reduce_host(hb, chunk=64, scratch=scratch)
+            assert np.array_equal(got.numpy(), orc.sum_reduce_i32(bufs))
+    finally:
+        o.set_tuning(h2d_streams=2)
+
+
 # --------------------------------------------------------------------------------------
 # quantise / dequantise (build-defined; parity vs the oracle's restatement)
 # --------------------------------------------------------------------------------------
@@ -268,16 +302,18 @@ def test_ps_apply_ina_update():
 # --------------------------------------------------------------------------------------
 # packets
 # --------------------------------------------------------------------------------------
-@pytest.mark.parametrize("V", [32, 128, 256, 4, 1, 33])
+# V = 100: a multiple of 4 that is not 4 x a power of two; "wide": 3 spare 16-byte
+# chunks of padding per packet (the flat unpack must skip them)
+@pytest.mark.parametrize("V", [32, 128, 256, 4, 1, 33, 100])
 @pytest.mark.parametrize("n", [1, 31, 32, 33, 300, 8191])
-@pytest.mark.parametrize("padded", [True, False])
-def test_pack_nga_matches_oracle(V, n, padded):
+@pytest.mark.parametrize("layout", ["padded", "tight", "wide"])
+def test_pack_nga_matches_oracle(V, n, layout):
     o = ops()
     rng = np.random.default_rng(V * 7 + n)
     vals = rand_i32(rng, n)
     npk = -(-n // V)
     ovf = (rng.random(npk) < 0.3).astype(np.uint8)
-    stride = o.nga_stride(V) if padded else 15 + 4 * V
+    stride = {"padded": o.nga_stride(V), "tight": 15 + 4 * V, "wide": o.nga_stride(V) + 48}[layout]
     got = host(o.pack_nga(dev(vals), V, bitmap=0xDEADBEEF, count=8, switch_id=3, seq0=16380,
                           flags=0x11, stride=stride, overflow=dev(ovf)))
     want = orc.pack_nga(vals, V, 0xDEADBEEF, 8, 3, 16380, flags=0x11, stride=stride, ovf=ovf)
