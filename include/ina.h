@@ -14,8 +14,9 @@
  *     torch CUDA tensor) owned by the caller, borrowed for the call;
  *   - arrays of worker buffers (`bufs`) are HOST arrays of W device pointers; the
  *     array itself is copied into the kernel arguments, so it may live on the stack;
- *   - `stream` is a hipStream_t (NULL = the legacy default stream); calls are
- *     asynchronous on that stream and never synchronise, allocate or free;
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream); device calls are
+ *     asynchronous on that stream and never synchronise, allocate or free (the host
+ *     paths -- send_gradients, ina_*_fd, ina_sum_reduce_host_i32 -- are synchronous);
  *   - return 0 on success, a negative INA_E* code otherwise (no exit(), unlike
  *     communicator.cc:11-12,38-39); ina_last_error_string() describes the last error.
  * Vector fast paths need 16-byte aligned pointers; other alignments take a slower
