@@ -129,6 +129,15 @@ def run_extra(dev):
                      4 * n3 + npk * stride))
     rows.append(_row("unpack_nga V=256", _time(lambda: ops.unpack_nga(pk, V)),
                      npk * stride + 4 * n3 + npk * 15))
+    # worker side, fused: NGA-256 packets of quantise(p_w - p_global) for a ResNet-50 bucket
+    nr = 25_557_032
+    xr, br = rnd_f32(nr), rnd_f32(nr)
+    npr = (nr + V - 1) // V
+    pr = torch.empty((npr, stride), dtype=torch.uint8, device=dev)
+    rows.append(_row("quantize_pack_nga V=256 ResNet-50 delta (worker side, fused)",
+                     _time(lambda: ops.quantize_pack_nga(xr, 16, V, 1, 8, 1, 1, base=br, out=pr)),
+                     8 * nr + npr * stride))
+    del xr, br, pr
     npc = 199_665   # ResNet-50 in C-128 packets (communicator.py:10)
     g = rnd_i32(npc * 128)
     pc = torch.empty((npc, 524), dtype=torch.uint8, device=dev)
@@ -153,7 +162,16 @@ def run_extra(dev):
     rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort)",
                      _time(sw_round, reps=5, warm=1),
                      stream.numel() + stream.numel() // Ws + npk * (V * 4 + 5) + npk_all))
-    del stream
+    # PS side, fused, on the switch's output: completed slots -> dequantise -> update + acks
+    sw.process(stream, acts)
+    local3 = rnd_f32(n3)
+    out3 = torch.empty_like(local3)
+    acks = torch.empty((npk, stream.shape[1]), dtype=torch.uint8, device=dev)
+    rows.append(_row("apply_completed_nga V=256 (PS side, fused; 102,400 completed of 819,200)",
+                     _time(lambda: ops.apply_completed(stream, acts, V, 1, local3, 16, 0.1, out=out3,
+                                                       acks=acks)),
+                     npk_all + npk * stream.shape[1] + 8 * n3 + 16 * npk))   # ack rows: 16-B headers
+    del stream, local3, out3, acks
 
     # --- end to end: pinned host -> HBM -> reduce -> pinned host -------------------------------
     hosts = [b.cpu().pin_memory() for b in b3]

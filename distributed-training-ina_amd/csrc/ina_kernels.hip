@@ -16,6 +16,7 @@
 // touched exactly once.  Integer sums use uint32 arithmetic (defined wraparound).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -144,13 +145,10 @@ static inline bool slot_ballot_ok(int V) {
 }
 
 
-// Cross-lane moves by one lane as DPP row moves (measured on gfx950, tools/lab/dpp_lab.hip):
-// wave_shl:1 -> lane i reads lane i+1 (lane 63 keeps its own value); wave_shr:1 (0x138,
-// used inline with an explicit `old` for lane 0) -> lane i reads lane i-1.  One VALU op
-// instead of an LDS ds_bpermute.
-__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x130, 0xF, 0xF, false);
-}
+// Cross-lane moves by one lane are DPP row moves (measured on gfx950, tools/lab/dpp_lab.hip):
+// update_dpp(old, x, 0x130 wave_shl:1) -> lane i reads lane i+1 (lane 63 gets `old`);
+// 0x138 wave_shr:1 -> lane i reads lane i-1 (lane 0 gets `old`).  One VALU op instead of
+// an LDS ds_bpermute, and `old` supplies the value from outside the wave.
 
 template <int W>
 constexpr int kUnrW = W > 0 ? W : 1;
@@ -688,6 +686,7 @@ struct NgaHdr {
 // fused worker-side quantise + packetise (DataManager.py:37 then 111-165, one pass).
 struct SrcI32 {
     const int32_t* __restrict__ v;
+    SrcI32 shifted(size_t off) const { return SrcI32{v + off}; }
     __device__ __forceinline__ uint32_t one(size_t e) const { return (uint32_t)v[e]; }
     __device__ __forceinline__ u32x4 four(size_t e) const {
         return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + e));
@@ -697,6 +696,7 @@ struct SrcQ32 {
     const float* __restrict__ x;
     const float* __restrict__ base;   // may be null
     float s;
+    SrcQ32 shifted(size_t off) const { return SrcQ32{x + off, base ? base + off : nullptr, s}; }
     __device__ __forceinline__ uint32_t one(size_t e) const {
         return (uint32_t)q32(base ? __fsub_rn(x[e], base[e]) : x[e], s);
     }
@@ -720,48 +720,78 @@ __device__ __forceinline__ uint32_t nga_val(const Src& src, size_t n, size_t p, 
     return e < n ? src.one(e) : 0u;
 }
 
-// vector path: stride % 16 == 0, V % 4 == 0, 16-byte aligned buffers.
-// Thread per 16-byte chunk of the packet buffer.
-template <typename Src>
-__global__ __launch_bounds__(kBlock) void k_pack_nga_vec(Src src, size_t n,
-                                                         NgaHdr h, const uint8_t* __restrict__ ovf,
-                                                         uint8_t* __restrict__ pkts,
-                                                         uint32_t chunks_per_pkt, size_t nchunks) {
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    const int V = h.V;
-    for (size_t g = (size_t)blockIdx.x * kBlock + threadIdx.x; g < nchunks; g += stride) {
-        size_t p = g / chunks_per_pkt;
-        uint32_t c = (uint32_t)(g - p * chunks_per_pkt);
-        u32x4 o;
-        if (c == 0) {
-            uint32_t seq = h.seq0 + (uint32_t)p;
-            uint32_t idx = seq % h.num_slots;
-            uint32_t flags = (h.flags_count_sw >> 8) & 0xFFu;
-            if (ovf && ovf[p]) flags |= INA_FLAG_OVERFLOW;
-            uint32_t count = h.flags_count_sw & 0xFFu, sw = (h.flags_count_sw >> 16) & 0xFFu;
-            uint32_t bi = bswap(idx), bf = bswap(seq);
-            o.x = bswap(h.bitmap);
-            o.y = count | (flags << 8) | (bi << 16);
-            o.z = (bi >> 16) | (sw << 16) | (bf << 24);
-            o.w = (bf >> 8) | (bswap(nga_val(src, n, p, V, 0)) << 24);
-        } else {
-            long j0 = 4 * (long)c - 4;   // out word m=4c+t takes payload words m-4, m-3
-            uint32_t v[5];
-            size_t e0 = p * (size_t)V + (size_t)j0;
-            if (j0 + 4 < V && e0 + 5 <= n) {
-                u32x4 a = src.four(e0);
-                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-                v[4] = src.one(e0 + 4);
-            } else {
+// flat pack (stride % 16 == 0, V % 4 == 0, 16-byte aligned source and packets): the
+// packet array is written as one contiguous stream of 16-byte chunks, thread per chunk,
+// U chunks in flight per thread.  Chunk c (1 <= c <= V/4) of a packet holds wire dwords
+// 4c..4c+3 = bytes 2,1,0 of value 4c-4+t and byte 3 of value 4c-3+t (one v_perm each);
+// the chunk loads its own 4 values (one 16-byte load, quantised once when the source is
+// fp32) and takes value 4c -- the next chunk's first -- from the next lane (DPP
+// wave_shl:1; lane 63 loads it).  Chunk 0 is the header plus value 0's top byte.
+constexpr uint32_t kSelWire = 0x07000102u;   // perm(next, v): {v.b2, v.b1, v.b0, next.b3}
+
+template <typename Src, int U>
+__global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, NgaHdr h,
+                                                          const uint8_t* __restrict__ ovf,
+                                                          uint8_t* __restrict__ pkts, uint32_t C,
+                                                          uint32_t L, uint32_t nch) {
+    const uint32_t gs = gridDim.x * kBlock;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
+    const size_t V = (size_t)h.V;
+    u32x4* ch = reinterpret_cast<u32x4*>(pkts);
+    for (uint32_t base = wave0; base < nch; base += U * gs) {
+        u32x4 v[U];
+        uint32_t nx0[U];
 #pragma unroll
-                for (int t = 0; t < 5; ++t) v[t] = nga_val(src, n, p, V, j0 + t);
+        for (int u = 0; u < U; ++u) {
+            const uint32_t t = base + u * gs + (uint32_t)lane;
+            const uint32_t p = t / C, c = t - p * C;
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (t < nch && c >= 1 && c <= L) {
+                const size_t e0 = (size_t)p * V + 4 * (size_t)(c - 1);
+                if (e0 + 4 <= n) {
+                    v[u] = src.four(e0);
+                } else {                                   // last packet of the bucket: zero tail
+                    v[u].x = e0 < n ? src.one(e0) : 0u;
+                    v[u].y = e0 + 1 < n ? src.one(e0 + 1) : 0u;
+                    v[u].z = e0 + 2 < n ? src.one(e0 + 2) : 0u;
+                }
             }
-            o.x = (bswap(v[0]) >> 8) | (v[1] & 0xFF000000u);
-            o.y = (bswap(v[1]) >> 8) | (v[2] & 0xFF000000u);
-            o.z = (bswap(v[2]) >> 8) | (v[3] & 0xFF000000u);
-            o.w = (bswap(v[3]) >> 8) | (v[4] & 0xFF000000u);
+            nx0[u] = 0u;
+            if (lane == 63 && t < nch && c < L) {
+                const size_t e = (size_t)p * V + 4 * (size_t)c;
+                nx0[u] = e < n ? src.one(e) : 0u;
+            }
         }
-        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(pkts) + g);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t t = base + u * gs + (uint32_t)lane;
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)nx0[u], (int)v[u].x, 0x130,
+                                                                      0xF, 0xF, false);
+            if (t >= nch) continue;
+            const uint32_t p = t / C, c = t - p * C;
+            u32x4 o;
+            if (c == 0) {
+                const uint32_t seq = h.seq0 + p;
+                const uint32_t idx = seq % h.num_slots;
+                uint32_t flags = (h.flags_count_sw >> 8) & 0xFFu;
+                if (ovf && ovf[p]) flags |= INA_FLAG_OVERFLOW;
+                const uint32_t count = h.flags_count_sw & 0xFFu, sw = (h.flags_count_sw >> 16) & 0xFFu;
+                const uint32_t bi = bswap(idx), bf = bswap(seq);
+                o.x = bswap(h.bitmap);
+                o.y = count | (flags << 8) | (bi << 16);
+                o.z = (bi >> 16) | (sw << 16) | (bf << 24);
+                o.w = (bf >> 8) | (nx & 0xFF000000u);        // value 0's top byte at byte 15
+            } else if (c <= L) {
+                o.x = __builtin_amdgcn_perm(v[u].y, v[u].x, kSelWire);
+                o.y = __builtin_amdgcn_perm(v[u].z, v[u].y, kSelWire);
+                o.z = __builtin_amdgcn_perm(v[u].w, v[u].z, kSelWire);
+                o.w = __builtin_amdgcn_perm(nx, v[u].w, kSelWire);
+            } else {
+                o = u32x4{0u, 0u, 0u, 0u};                   // padding chunks
+            }
+            __builtin_nontemporal_store(o, ch + t);
+        }
     }
 }
 
@@ -861,59 +891,101 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_flat(const uint8_t* __res
 // DataManager.py:116-130), dequantise and apply the update
 //     out[slot*V + j] = local[..] + ws * ((float)sum * 2^-k)
 // (aggregate()'s update with the switch's integer sum, launch.py:46-50), and write the
-// slot's PS ack header (is_ack=1, fragcheck.p4:26-31) into ack row `slot`.  L = V/4
-// lanes per packet: lane j loads 16-byte chunk j once and takes chunk j+1 from its
-// neighbour (DPP wave_shl:1); the packet's last lane loads the tail chunk L itself.
+// slot's PS ack header (is_ack=1, fragcheck.p4:26-31) into ack row `slot`.
+// A wave owns windows of kApWin packets: one coalesced read of their action bytes, a
+// ballot of the completed ones (1 in W of a worker stream, all of them in a stream from
+// a hardware switch), then kApB completed packets at a time with all their loads in
+// flight: header and chunk loads, then the slots' local rows.  Lane l holds chunk l+1 of a packet and
+// decodes values 4l..4l+3 with one v_perm each (the previous chunk's last dword by DPP
+// wave_shr:1; header dword 3 for lane 0), the header comes in with a wave-uniform load.
+// batch and window measured with tools/lab/apply_lab.py (8 x NGA-256 switch output,
+// 1 in 8 packets completed): batch 4 with the local rows prefetched 56.7 us; batch 8
+// without prefetch 66.8, with prefetch 81.9 (VGPRs); 16-packet windows spread the
+// completed packets of a dense stream over more waves than 64-packet ones
+#ifndef INA_APPLY_BATCH
+#define INA_APPLY_BATCH 4
+#endif
+#ifndef INA_APPLY_WIN
+#define INA_APPLY_WIN 16
+#endif
+constexpr int kApB = INA_APPLY_BATCH;
+constexpr int kApWin = INA_APPLY_WIN;   // packets per window (<= 64)
+
 __global__ __launch_bounds__(kBlock) void k_apply_completed_nga(
-        const uint8_t* __restrict__ pkts, size_t npk, int log2L, size_t pstride,
-        const uint8_t* __restrict__ actions, uint32_t seq0, size_t nslots,
+        const uint8_t* __restrict__ pkts, uint32_t npk, uint32_t pstride,
+        const uint8_t* __restrict__ actions, uint32_t seq0, uint32_t nslots,
         const float* __restrict__ local, float inv, float ws, float* __restrict__ out, size_t n,
-        uint8_t* __restrict__ acks, size_t ack_stride) {
-    const size_t gs = (size_t)gridDim.x * kBlock;
-    const uint32_t L = 1u << log2L;
-    const size_t total = npk << log2L;
+        uint8_t* __restrict__ acks, size_t ack_stride, int V) {
     const int lane = threadIdx.x & 63;
-    const int lead = lane & ~(int)(L - 1);                   // first lane of this packet group
-    const size_t wave0 = ((size_t)blockIdx.x * kBlock + threadIdx.x) & ~(size_t)63;
-    for (size_t base = wave0; base < total; base += gs) {
-        const size_t g = base + (size_t)lane;
-        const bool in = g < total;
-        const size_t p = g >> log2L;
-        const uint32_t j = (uint32_t)(g & (L - 1));
-        const u32x4* pk = reinterpret_cast<const u32x4*>(pkts + p * pstride);
-        const bool done = in && actions[p] == INA_ACT_FWD_AGG;
-        u32x4 a = done ? __builtin_nontemporal_load(pk + j) : u32x4{0u, 0u, 0u, 0u};
-        u32x4 b;
-        b.x = from_next_lane(a.x); b.y = from_next_lane(a.y);
-        b.z = from_next_lane(a.z); b.w = from_next_lane(a.w);
-        // frag_id (header bytes 11..14) from the group's chunk 0
-        const uint32_t h2 = __shfl(a.z, lead, 64), h3 = __shfl(a.w, lead, 64);
-        if (!done) continue;
-        if (j == L - 1) b = __builtin_nontemporal_load(pk + L);
-        const size_t slot = (size_t)(uint32_t)(__builtin_bswap32((h2 >> 24) | (h3 << 8)) - seq0);
-        if (slot >= nslots) continue;                         // not from this bucket
-        if (j == 0 && acks) {
-            u32x4 hd = a;
-            hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
-            *reinterpret_cast<u32x4*>(acks + slot * ack_stride) = hd;
-        }
-        const size_t e = slot * ((size_t)L * 4) + 4 * (size_t)j;
-        uint32_t v[4];
-        v[0] = bswap(__builtin_amdgcn_alignbyte(b.x, a.w, 3));
-        v[1] = bswap(__builtin_amdgcn_alignbyte(b.y, b.x, 3));
-        v[2] = bswap(__builtin_amdgcn_alignbyte(b.z, b.y, 3));
-        v[3] = bswap(__builtin_amdgcn_alignbyte(b.w, b.z, 3));
-        if (e + 4 <= n) {
-            f32x4 l = *reinterpret_cast<const f32x4*>(local + e);
-            f32x4 r;
-            r.x = __fadd_rn(l.x, __fmul_rn(__fmul_rn((float)(int32_t)v[0], inv), ws));
-            r.y = __fadd_rn(l.y, __fmul_rn(__fmul_rn((float)(int32_t)v[1], inv), ws));
-            r.z = __fadd_rn(l.z, __fmul_rn(__fmul_rn((float)(int32_t)v[2], inv), ws));
-            r.w = __fadd_rn(l.w, __fmul_rn(__fmul_rn((float)(int32_t)v[3], inv), ws));
-            *reinterpret_cast<f32x4*>(out + e) = r;
-        } else {
-            for (int t = 0; t < 4 && e + t < n; ++t)
-                out[e + t] = __fadd_rn(local[e + t], __fmul_rn(__fmul_rn((float)(int32_t)v[t], inv), ws));
+    const int L = V >> 2;
+    const bool vl = lane < L;
+    const int chn = 1 + (vl ? lane : 0);
+    const uint32_t wave = blockIdx.x * (kBlock / 64) + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+    for (uint32_t w0 = wave * kApWin; w0 < npk; w0 += nwaves * kApWin) {
+        const uint32_t p = w0 + (uint32_t)lane;
+        unsigned long long m = __ballot(lane < kApWin && p < npk && actions[p] == INA_ACT_FWD_AGG);
+        while (m) {
+            uint32_t pid[kApB];
+            int nb = 0;
+#pragma unroll
+            for (int b = 0; b < kApB; ++b) {
+                if (m) {
+                    pid[b] = w0 + (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1;
+                    nb = b + 1;
+                } else {
+                    pid[b] = pid[0];
+                }
+            }
+            u32x4 hv[kApB], a[kApB];
+#pragma unroll
+            for (int b = 0; b < kApB; ++b) {
+                const u32x4* pk = reinterpret_cast<const u32x4*>(pkts + (size_t)pid[b] * pstride);
+                hv[b] = pk[0];
+                a[b] = __builtin_nontemporal_load(pk + chn);
+            }
+            // slots from the headers, then every local row of the batch in flight at once
+            uint32_t slot[kApB];
+            f32x4 l[kApB];
+#pragma unroll
+            for (int b = 0; b < kApB; ++b) {
+                const uint32_t h2 = __builtin_amdgcn_readfirstlane(hv[b].z);
+                const uint32_t h3 = __builtin_amdgcn_readfirstlane(hv[b].w);
+                slot[b] = b < nb ? bswap((h2 >> 24) | (h3 << 8)) - seq0 : 0xFFFFFFFFu;
+                const size_t e = (size_t)slot[b] * (size_t)V + 4 * (size_t)lane;
+                l[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (slot[b] < nslots && vl && e + 4 <= n) l[b] = *reinterpret_cast<const f32x4*>(local + e);
+            }
+#pragma unroll
+            for (int b = 0; b < kApB; ++b) {
+                if (slot[b] >= nslots) continue;               // past the batch, or not this bucket
+                if (lane == 0 && acks) {
+                    u32x4 hd = hv[b];
+                    hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+                    *reinterpret_cast<u32x4*>(acks + (size_t)slot[b] * ack_stride) = hd;
+                }
+                const uint32_t pw = (uint32_t)__builtin_amdgcn_update_dpp((int)hv[b].w, (int)a[b].w,
+                                                                          0x138, 0xF, 0xF, false);
+                uint32_t v[4];
+                v[0] = __builtin_amdgcn_perm(a[b].x, pw, kSelBE);
+                v[1] = __builtin_amdgcn_perm(a[b].y, a[b].x, kSelBE);
+                v[2] = __builtin_amdgcn_perm(a[b].z, a[b].y, kSelBE);
+                v[3] = __builtin_amdgcn_perm(a[b].w, a[b].z, kSelBE);
+                if (!vl) continue;
+                const size_t e = (size_t)slot[b] * (size_t)V + 4 * (size_t)lane;
+                if (e + 4 <= n) {
+                    f32x4 r;
+                    r.x = __fadd_rn(l[b].x, __fmul_rn(__fmul_rn((float)(int32_t)v[0], inv), ws));
+                    r.y = __fadd_rn(l[b].y, __fmul_rn(__fmul_rn((float)(int32_t)v[1], inv), ws));
+                    r.z = __fadd_rn(l[b].z, __fmul_rn(__fmul_rn((float)(int32_t)v[2], inv), ws));
+                    r.w = __fadd_rn(l[b].w, __fmul_rn(__fmul_rn((float)(int32_t)v[3], inv), ws));
+                    *reinterpret_cast<f32x4*>(out + e) = r;
+                } else {
+                    for (int t = 0; t < 4 && e + t < n; ++t)
+                        out[e + t] = __fadd_rn(local[e + t], __fmul_rn(__fmul_rn((float)(int32_t)v[t], inv), ws));
+                }
+            }
         }
     }
 }
@@ -1048,10 +1120,18 @@ static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina
     NgaHdr h{prm->bitmap, prm->seq0, prm->num_slots,
              (uint32_t)prm->count | ((uint32_t)prm->flags << 8) | ((uint32_t)prm->switch_id << 16), V};
     if (pstride % 16 == 0 && V % 4 == 0 && src_aligned && aligned16(pkts)) {
-        uint32_t cpp = (uint32_t)(pstride / 16);
-        size_t nchunks = npk * cpp;
-        hipLaunchKernelGGL(k_pack_nga_vec<Src>, dim3(grid_for(nchunks, 1)), dim3(kBlock), 0, s, src, n, h,
-                           ovf, pkts, cpp, nchunks);
+        // 32-bit chunk indices: huge buckets go in packet ranges
+        const size_t C = pstride / 16;
+        const size_t per = ((size_t)1 << 31) / C;
+        for (size_t p0 = 0; p0 < npk; p0 += per) {
+            const size_t np = npk - p0 < per ? npk - p0 : per;
+            const size_t v0 = p0 * (size_t)V;
+            NgaHdr hp = h;
+            hp.seq0 = h.seq0 + (uint32_t)p0;
+            hipLaunchKernelGGL((k_pack_nga_flat<Src, 4>), dim3(grid_for(np * C, 4, g_stream_blocks)),
+                               dim3(kBlock), 0, s, src.shifted(v0), n - v0, hp, ovf ? ovf + p0 : nullptr,
+                               pkts + p0 * pstride, (uint32_t)C, (uint32_t)(V / 4), (uint32_t)(np * C));
+        }
     } else {
         size_t nbytes = npk * pstride;
         hipLaunchKernelGGL(k_pack_nga_bytes<Src>, dim3(grid_for(nbytes, 1)), dim3(kBlock), 0, s, src, n,
@@ -1341,21 +1421,22 @@ int ina_apply_completed_nga(const uint8_t* pkts, size_t npk, int V, size_t pstri
                             double weight_step, float* out, size_t n, uint8_t* acks,
                             size_t ack_stride, ina_stream_t stream) {
     if (int rc = check_k(k)) return rc;
-    int log2L = -1;
-    if (V > 0 && V % 4 == 0 && V / 4 <= 64 && ((V / 4) & (V / 4 - 1)) == 0)
-        for (log2L = 0; (1 << log2L) < V / 4; ++log2L) {}
-    if (log2L < 0) return set_error(INA_EINVAL, "V must be 4 x a power of two <= 256%s", "");
+    if (V <= 0 || V % 4 || V > 256) return set_error(INA_EINVAL, "V must be a multiple of 4 <= 256%s", "");
     if (pstride % 16 || pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V || !aligned16(pkts))
         return set_error(INA_EINVAL, "packets must be 16-byte aligned rows of stride %% 16 == 0%s", "");
     if (acks && (ack_stride % 16 || !aligned16(acks)))
         return set_error(INA_EINVAL, "ack rows must be 16-byte aligned%s", "");
     if (npk == 0 || n == 0) return INA_OK;
+    if (npk > 0x7FFFFFFFu || pstride > 0xFFFFFFFFu) return set_error(INA_EINVAL, "too many packets%s", "");
     if (!actions || !local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     if (!aligned16(local) || !aligned16(out)) return set_error(INA_EINVAL, "local/out must be 16-byte aligned%s", "");
-    size_t nslots = (n + (size_t)V - 1) / (size_t)V;
-    hipLaunchKernelGGL(k_apply_completed_nga, dim3(grid_for(npk * (size_t)(V / 4), 1)), dim3(kBlock), 0,
-                       hs(stream), pkts, npk, log2L, pstride, actions, seq0, nslots, local,
-                       ldexpf(1.0f, -k), (float)weight_step, out, n, acks, ack_stride);
+    const size_t nslots = (n + (size_t)V - 1) / (size_t)V;
+    const uint32_t ns32 = nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots;
+    const size_t windows = (npk + kApWin - 1) / kApWin;
+    unsigned g = (unsigned)std::min<size_t>((windows + 3) / 4, 2048);
+    hipLaunchKernelGGL(k_apply_completed_nga, dim3(g), dim3(kBlock), 0, hs(stream), pkts,
+                       (uint32_t)npk, (uint32_t)pstride, actions, seq0, ns32, local,
+                       ldexpf(1.0f, -k), (float)weight_step, out, n, acks, ack_stride, V);
     return check_launch("apply_completed_nga");
 }
 

@@ -446,7 +446,7 @@ def test_switch_collision_free_equals_bulk_reduce():
     assert np.array_equal(got, host(o.sum_reduce([dev(b) for b in bufs])))
 
 
-@pytest.mark.parametrize("V", [32, 256, 33])
+@pytest.mark.parametrize("V", [32, 256, 33, 100, 4])
 @pytest.mark.parametrize("with_base", [False, True])
 @pytest.mark.parametrize("padded", [True, False])
 def test_quantize_pack_fused_matches_oracle(V, with_base, padded):
@@ -464,7 +464,7 @@ def test_quantize_pack_fused_matches_oracle(V, with_base, padded):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("V,W", [(256, 8), (32, 3), (128, 4)])
+@pytest.mark.parametrize("V,W", [(256, 8), (32, 3), (128, 4), (100, 5), (4, 2)])
 def test_switch_then_fused_apply_matches_oracle(V, W):
     """PS side: device switch over W worker streams, then one fused kernel places,
     dequantises and applies the completed slots; its ack rows free every slot."""
