@@ -73,6 +73,7 @@ constexpr int kRsBlock = 64 * INA_RS_WAVES;
 constexpr int kRsWaves = kRsBlock / 64;
 constexpr int kRsWaveItems = 64 * kRsRounds;
 constexpr int kRsChunk = kRsWaves * kRsWaveItems;       // items per block (4096)
+static_assert(kRsBins % kRsBlock == 0, "digits split evenly over the block's threads");
 
 __device__ __forceinline__ unsigned long long lanes_with_digit(uint32_t d, int bits, bool valid) {
     unsigned long long m = __ballot(valid);
@@ -180,12 +181,23 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_colscan(uint32_t* __restrict__ 
     if (d >= nb) return;
     uint32_t* row = hist + d * nch;
     uint32_t run = 0;
-    for (size_t c0 = 0; c0 < nch; c0 += 64) {
-        const size_t c = c0 + (size_t)lane;
-        const uint32_t x = c < nch ? row[c] : 0u;
-        const uint32_t inc = wave_incl_scan(x);
-        if (c < nch) row[c] = run + inc - x;
-        run += __builtin_amdgcn_readlane(inc, 63);
+    // 8 x 64 chunks per step (one step up to 2 M packets): the step's loads are all
+    // issued before its scans
+    constexpr int kCs = 8;
+    for (size_t c0 = 0; c0 < nch; c0 += 64 * kCs) {
+        uint32_t x[kCs];
+#pragma unroll
+        for (int q = 0; q < kCs; ++q) {
+            const size_t c = c0 + 64 * q + (size_t)lane;
+            x[q] = c < nch ? row[c] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < kCs; ++q) {
+            const size_t c = c0 + 64 * q + (size_t)lane;
+            const uint32_t inc = wave_incl_scan(x[q]);
+            if (c < nch) row[c] = run + inc - x[q];
+            run += __builtin_amdgcn_readlane(inc, 63);
+        }
     }
     if (lane == 0) totals[d] = run;
 }
@@ -214,23 +226,41 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
         k[r] = i < n ? kin[i] : 0u;
         v[r] = kIds ? (i < n ? vin[i] : 0u) : (uint32_t)i;
     }
+    // digit totals and this chunk's column prefixes: loaded with the keys, one round trip
+    constexpr int kDPT = kRsBins / kRsBlock;         // digits per thread
+    uint32_t tot[kDPT], cpf[kDPT];
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        tot[j] = d < nb ? totals[d] : 0u;
+        cpf[j] = d < nb ? colpref[d * nch + c] : 0u;
+    }
     for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
-    if (wv == 0) {                                   // digit bases: scan of the totals
-        uint32_t carry = 0;
-        for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
-            const uint32_t d = d0 + (uint32_t)lane;
-            const uint32_t t = d < nb ? totals[d] : 0u;
-            const uint32_t inc = wave_incl_scan(t);
-            if (d < nb) dbase[d] = carry + inc - t;
-            carry += __builtin_amdgcn_readlane(inc, 63);
-        }
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        if (d < nb) dbase[d] = tot[j];
     }
 #pragma unroll
     for (int r = 0; r < kRsRounds; ++r)              // this wave's digit counts
         if (i0 + (size_t)r * 64 < n) atomicAdd(&base[wv][(k[r] >> shift) & (nb - 1)], 1u);
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) {
-        uint32_t b = dbase[d] + colpref[d * nch + c];
+    if (wv == 0) {                                   // digit bases: exclusive scan of the totals
+        uint32_t carry = 0;
+        for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
+            const uint32_t d = d0 + (uint32_t)lane;
+            const uint32_t t = d < nb ? dbase[d] : 0u;
+            const uint32_t inc = wave_incl_scan(t);
+            if (d < nb) dbase[d] = carry + inc - t;
+            carry += __builtin_amdgcn_readlane(inc, 63);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        if (d >= nb) continue;
+        uint32_t b = dbase[d] + cpf[j];
 #pragma unroll
         for (int w = 0; w < kRsWaves; ++w) {
             const uint32_t cw = base[w][d];
