@@ -171,7 +171,33 @@ def run_extra(dev):
                      _time(lambda: ops.apply_completed(stream, acts, V, 1, local3, 16, 0.1, out=out3,
                                                        acks=acks)),
                      npk_all + npk * stream.shape[1] + 8 * n3 + 16 * npk))   # ack rows: 16-B headers
-    del stream, local3, out3, acks
+    del local3, out3, acks
+
+    # the whole INA packet path on one GPU, one step: 8 workers quantise+packetise their
+    # deltas (p_w - p_global) into one arrival stream, the switch aggregates it, the PS
+    # applies the completed slots and its acks go back through the switch to free them
+    xs = [rnd_f32(n3) for _ in range(Ws)]
+    glob_p = rnd_f32(n3)
+    upd = torch.empty_like(glob_p)
+    acks = torch.empty((npk, stream.shape[1]), dtype=torch.uint8, device=dev)
+    ack_acts = torch.empty(npk, dtype=torch.uint8, device=dev)
+    rows_w = stream.view(Ws, npk, stream.shape[1])
+
+    def ina_step():
+        for w in range(Ws):
+            ops.quantize_pack_nga(xs[w], 16, V, w + 1, Ws, 1, 1, base=glob_p, num_slots=1 << 17,
+                                  out=rows_w[w])
+        sw.process(stream, acts)
+        ops.apply_completed(stream, acts, V, 1, glob_p, 16, 1.0 / (Ws + 1), out=upd, acks=acks)
+        sw.process(acks, ack_acts)
+    t = _time(ina_step, reps=5, warm=1)
+    ina_step()
+    torch.cuda.synchronize()
+    ok = bool((acts == 1).sum() == npk) and bool((ack_acts == 3).all()) and not bool(sw.frag.any())
+    rows.append(_row("INA packet path step: 8 x quantise+pack -> switch -> apply -> acks (8 x 100 MiB fp32)",
+                     t, Ws * n3 * 4, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2), slots_freed=ok,
+                     note="GB/s column = worker fp32 bytes aggregated per second through the packet path"))
+    del xs, glob_p, upd, acks, ack_acts, rows_w, stream
 
     # --- end to end: pinned host -> HBM -> reduce -> pinned host -------------------------------
     hosts = [b.cpu().pin_memory() for b in b3]
