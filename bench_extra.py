@@ -125,18 +125,20 @@ def run_extra(dev):
     stride = ops.nga_stride(V)
     npk = (n3 + V - 1) // V
     pk = torch.empty((npk, stride), dtype=torch.uint8, device=dev)
-    rows.append(_row("pack_nga V=256", _time(lambda: ops.pack_nga(o3, V, 1, 8, 1, 1, out=pk)),
-                     4 * n3 + npk * stride))
-    rows.append(_row("unpack_nga V=256", _time(lambda: ops.unpack_nga(pk, V)),
-                     npk * stride + 4 * n3 + npk * 15))
+    grids = (256, 512, 1024, 2048, 8192)
+    _sweep(ops, rows, gsweep, "pack_nga V=256", "stream_blocks", grids,
+           lambda: ops.pack_nga(o3, V, 1, 8, 1, 1, out=pk), 4 * n3 + npk * stride)
+    _sweep(ops, rows, gsweep, "unpack_nga V=256", "stream_blocks", grids,
+           lambda: ops.unpack_nga(pk, V), npk * stride + 4 * n3 + npk * 15)
     # worker side, fused: NGA-256 packets of quantise(p_w - p_global) for a ResNet-50 bucket
     nr = 25_557_032
     xr, br = rnd_f32(nr), rnd_f32(nr)
     npr = (nr + V - 1) // V
     pr = torch.empty((npr, stride), dtype=torch.uint8, device=dev)
-    rows.append(_row("quantize_pack_nga V=256 ResNet-50 delta (worker side, fused)",
-                     _time(lambda: ops.quantize_pack_nga(xr, 16, V, 1, 8, 1, 1, base=br, out=pr)),
-                     8 * nr + npr * stride))
+    _sweep(ops, rows, gsweep, "quantize_pack_nga V=256 ResNet-50 delta (worker side, fused)",
+           "stream_blocks", grids, lambda: ops.quantize_pack_nga(xr, 16, V, 1, 8, 1, 1, base=br, out=pr),
+           8 * nr + npr * stride)
+    rows.append(_row("absmax_f32 ResNet-50 delta (dynamic scale)", _time(lambda: ops.absmax(xr, br)), 8 * nr))
     del xr, br, pr
     npc = 199_665   # ResNet-50 in C-128 packets (communicator.py:10)
     g = rnd_i32(npc * 128)

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -1078,6 +1079,51 @@ __global__ __launch_bounds__(kBlock) void k_checksum_i32(const int32_t* __restri
     }
 }
 
+// ===========================================================================
+// 8. per-bucket absmax for a dynamic scale: max_i |x[i] - base[i]| over finite and
+//    infinite values (NaN ignored: the quantiser maps it to 0).  Non-negative floats
+//    order like their bit patterns, so blocks combine with one atomicMax on the bits.
+// ===========================================================================
+__device__ __forceinline__ float absdiff(float x, const float* base, size_t i) {
+    return fabsf(base ? __fsub_rn(x, base[i]) : x);
+}
+
+__global__ __launch_bounds__(kBlock) void k_absmax_f32(const float* __restrict__ x,
+                                                       const float* __restrict__ base, size_t n,
+                                                       int vec, uint32_t* __restrict__ out) {
+    __shared__ float part[kBlock / 64];
+    const size_t n4 = vec ? n / 4 : 0;
+    float m = 0.0f;
+    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+        f32x4 a[UU], b[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            a[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x) + i + u * st);
+            b[u] = base ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base) + i + u * st)
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            m = fmaxf(m, fabsf(__fsub_rn(a[u].x, b[u].x)));
+            m = fmaxf(m, fabsf(__fsub_rn(a[u].y, b[u].y)));
+            m = fmaxf(m, fabsf(__fsub_rn(a[u].z, b[u].z)));
+            m = fmaxf(m, fabsf(__fsub_rn(a[u].w, b[u].w)));
+        }
+    });
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        m = fmaxf(m, absdiff(x[i], base, i));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = part[0];
+        for (int w = 1; w < kBlock / 64; ++w) r = fmaxf(r, part[w]);
+        atomicMax(out, __float_as_uint(r));
+    }
+}
+
 }  // namespace ina
 
 // ===========================================================================
@@ -1453,6 +1499,40 @@ int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id, uint3
                        (size_t)packet_num, bitmap, aggregator_index, tensor_index,
                        reinterpret_cast<uint32_t*>(pkts));
     return check_launch("pack_c128");
+}
+
+int ina_absmax_f32(const float* x, const float* base, size_t n, float* out_dev, ina_stream_t stream) {
+    if (!out_dev) return set_error(INA_EINVAL, "null out%s", "");
+    hipStream_t s = hs(stream);
+    if (hipMemsetAsync(out_dev, 0, sizeof(float), s) != hipSuccess)
+        return set_error(INA_EHIP, "memset absmax%s", "");
+    if (n == 0) return INA_OK;
+    if (!x) return set_error(INA_EINVAL, "null pointer%s", "");
+    const int vec = aligned16(x) && (!base || aligned16(base));
+    hipLaunchKernelGGL(k_absmax_f32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks)), dim3(kBlock), 0,
+                       s, x, base, n, vec, reinterpret_cast<uint32_t*>(out_dev));
+    return check_launch("absmax_f32");
+}
+
+int ina_scale_for(float absmax, int W, int bits, int* k_out) {
+    // largest k with W * (absmax * 2^k + 1/2) <= 2^(bits-1) - 1: no worker value and no
+    // W-way sum saturates (each quantised value rounds by at most 1/2)
+    if (!k_out) return set_error(INA_EINVAL, "null k_out%s", "");
+    if (W < 1 || (bits != 16 && bits != 32)) return set_error(INA_EINVAL, "W >= 1, bits 16 or 32%s", "");
+    if (!(absmax >= 0.0f) || std::isinf(absmax))
+        return set_error(INA_EINVAL, "absmax must be finite and >= 0%s", "");
+    const double lim = (bits == 32 ? 2147483647.0 : 32767.0) / (double)W - 0.5;
+    if (lim <= 0.0) return set_error(INA_EINVAL, "too many workers for this width%s", "");
+    if (absmax == 0.0f) {
+        *k_out = 127;
+        return INA_OK;
+    }
+    int k = (int)std::floor(std::log2(lim / (double)absmax));
+    k = k < -126 ? -126 : (k > 127 ? 127 : k);
+    while (k > -126 && (double)absmax * std::ldexp(1.0, k) > lim) --k;       // guard log2 rounding
+    while (k < 127 && (double)absmax * std::ldexp(1.0, k + 1) <= lim) ++k;
+    *k_out = k;
+    return INA_OK;
 }
 
 int ina_checksum_i32(const int32_t* x, size_t n, uint32_t* out_dev, ina_stream_t stream) {

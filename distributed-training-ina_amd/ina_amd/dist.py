@@ -77,6 +77,9 @@ class ShardedAggregator:
         n = self.plan.n
         if grad.numel() != n:
             raise ValueError("bucket size changed")
+        if self.world == 1:      # the collectives are identities: quantise -> dequantise
+            ops.quantize(grad.reshape(-1), self.k, out=self.q[:n])
+            return ops.dequantize(self.q[:n], self.k, out=self.full[:n])
         ops.quantize(grad.reshape(-1), self.k, out=self.q[:n])
         reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
         ops.dequantize(self.sum_shard, self.k, out=self.f_shard)

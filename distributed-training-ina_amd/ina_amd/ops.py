@@ -13,6 +13,7 @@ These are the kernels that replace the reference's CPU / switch arithmetic:
                              PS-side parse (NGAPacket.py:62-143), headers.p4 layout
   pack_c128                  send_gradients' packet loop (communicator.cc:23-37)
   ps_combine                 aggregate() (launch.py:42-52)
+  absmax / scale_for         per-bucket dynamic scale for the quantiser (build-defined)
 """
 from __future__ import annotations
 
@@ -311,6 +312,38 @@ def checksum(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(1, dtype=torch.int32, device=x.device)
     check(load().ina_checksum_i32(x.data_ptr(), x.numel(), out.data_ptr(), _stream(x)), "checksum")
     return out
+
+
+# -- dynamic scale ---------------------------------------------------------------------------
+def absmax(x: torch.Tensor, base: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    """Device float32 [1] = max_i |x[i] - base[i]| (base optional; NaN ignored)."""
+    _req(x, torch.float32, "x")
+    if base is not None:
+        _req(base, torch.float32, "base")
+        if base.numel() != x.numel():
+            raise ValueError("base and x differ in length")
+        _same_device(x, base)
+    out = torch.empty(1, dtype=torch.float32, device=x.device) if out is None else out
+    _req(out, torch.float32, "out")
+    check(load().ina_absmax_f32(x.data_ptr(), base.data_ptr() if base is not None else None,
+                                x.numel(), out.data_ptr(), _stream(x)), "absmax")
+    return out
+
+
+def scale_for(amax: float, W: int, bits: int = 32) -> int:
+    """Largest k in [-126, 127] such that no worker value and no W-way sum of 2^k fixed
+    point values with |x| <= amax saturates at `bits` (32, or 16 for the int16 wire)."""
+    k = C.c_int(0)
+    check(load().ina_scale_for(float(amax), int(W), int(bits), C.byref(k)), "scale_for")
+    return k.value
+
+
+def scale_for_workers(xs, base: torch.Tensor | None = None, bits: int = 32) -> int:
+    """k for W device buckets (deltas against `base` when given): one absmax kernel per
+    bucket, one host read of the maximum."""
+    xs = list(xs)
+    m = torch.cat([absmax(x, base) for x in xs]).max()
+    return scale_for(float(m.item()), len(xs), bits)
 
 
 # -- device packet-stream switch ---------------------------------------------------------------

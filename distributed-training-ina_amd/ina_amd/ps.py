@@ -9,7 +9,9 @@ and meaning of launch.py:42-52 (sync: weight 1/(W+1)) and launch_async.py:42-57
   mode="ina"             the in-network semantics: each worker's delta p_w - local
                          is quantised (2^k fixed point), summed as wrapping int32 --
                          the switch's Processor add -- and dequantised into the
-                         update (ina_ps_combine_ina_f32), one pass over HBM.
+                         update (ina_ps_combine_ina_f32), one pass over HBM;
+                         k="auto" picks the largest non-saturating scale from the
+                         deltas' absmax (ops.scale_for_workers).
 
 Worker.updated_paras may be CPU tensors (unpickled from the worker socket,
 worker.py:78) or device tensors; CPU ones are staged through pinned memory.
@@ -45,7 +47,7 @@ def _staged(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
 
 
 def aggregate(global_model, worker_list, step_size, worker_num: int | None = None,
-              mode: str = "fp32", k: int = 16):
+              mode: str = "fp32", k: int | str = 16):
     dev = _device_of(global_model)
     if dev.type != "cuda":
         raise ValueError("aggregate: global_model must live on the GPU (global_model.to('cuda'))")
@@ -67,11 +69,15 @@ def aggregate(global_model, worker_list, step_size, worker_num: int | None = Non
     return out
 
 
-def combine_ina(local: torch.Tensor, paras, k: int, weight_step: float, out=None):
-    """local + float(weight_step) * dequant(sum_w q(paras[w] - local)) on the GPU."""
+def combine_ina(local: torch.Tensor, paras, k, weight_step: float, out=None):
+    """local + float(weight_step) * dequant(sum_w q(paras[w] - local)) on the GPU.
+    k="auto": the largest scale at which no delta and no W-way sum saturates
+    (ops.scale_for_workers over the deltas; one host read)."""
     from . import _lib
     ops._req(local, torch.float32, "local")
     paras, n = ops._bufs(paras, torch.float32, "paras")
+    if k == "auto":
+        k = ops.scale_for_workers(paras, base=local)
     out = torch.empty_like(local) if out is None else out
     arr = _lib.ptr_array([p.data_ptr() for p in paras])
     _lib.check(_lib.load().ina_ps_combine_ina_f32(local.data_ptr(), arr, len(paras), k,

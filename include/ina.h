@@ -75,6 +75,15 @@ int ina_quantize_f32_i16_sat(const float* x, int16_t* q, size_t n, int k, int V,
 int ina_dequantize_i32_f32(const int32_t* s, float* y, size_t n, int k, ina_stream_t stream);
 int ina_dequantize_i16_f32(const int16_t* s, float* y, size_t n, int k, ina_stream_t stream);
 
+/* Dynamic scale (build-defined, like the quantiser): *out_dev (device float) =
+ * max_i |x[i] - base[i]| (base may be NULL; NaN ignored, as the quantiser maps it to 0).
+ * ina_scale_for turns the max over all W workers into the largest k in [-126, 127] with
+ * W * (absmax * 2^k + 1/2) <= 2^(bits-1) - 1, so neither a worker value nor the W-way
+ * sum saturates (bits = 32, or 16 for the int16 wire); absmax 0 gives 127.  *k_out gets
+ * k; INA_EINVAL for absmax negative, NaN or infinite, W < 1, or W too large for the width. */
+int ina_absmax_f32(const float* x, const float* base, size_t n, float* out_dev, ina_stream_t stream);
+int ina_scale_for(float absmax, int W, int bits, int* k_out);
+
 /* ---- the aggregator ------------------------------------------------------------
  * Replaces the switch's per-slot Processor add (processor.p4:14-24, x32 at
  * ngaa.p4:87-168): out[i] = sum_w bufs[w][i] mod 2^32, bit-identical to the

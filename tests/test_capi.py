@@ -72,3 +72,41 @@ def test_ops_refuse_cpu_tensors():
 def test_nga_stride():
     from ina_amd import ops
     assert ops.nga_stride(32) == 144 and ops.nga_stride(256) == 1040 and ops.nga_stride(128) == 528
+
+
+@pytest.mark.parametrize("bits", [32, 16])
+@pytest.mark.parametrize("W", [1, 2, 8, 16, 64])
+def test_scale_for_is_the_largest_non_saturating_k(W, bits):
+    """ina_scale_for (host-only): W * (amax * 2^k + 1/2) fits the width at k and not at
+    k + 1 (unless k is already 127); checked in exact rational arithmetic."""
+    from fractions import Fraction
+    from ina_amd import ops
+    lim = Fraction(2**(bits - 1) - 1, W) - Fraction(1, 2)
+    if lim <= 0:
+        return
+    rng = np.random.default_rng(W * bits)
+    amaxes = np.concatenate([rng.uniform(0, 1, 50), 10.0 ** rng.uniform(-30, 30, 50),
+                             [1e-38, 1.0, 0.5, 2.0, 3.0e38]]).astype(np.float32)
+    for a in amaxes:
+        k = ops.scale_for(float(a), W, bits)
+        af = Fraction(float(a))
+        scaled = lambda kk: af * (Fraction(2) ** kk)                     # noqa: E731
+        assert -126 <= k <= 127
+        if k > -126:
+            assert scaled(k) <= lim, (a, k)
+        if k < 127:
+            assert scaled(k + 1) > lim, (a, k)
+
+
+def test_scale_for_edges():
+    from ina_amd import _lib, ops
+    assert ops.scale_for(0.0, 8) == 127
+    for bad in (-1.0, float("nan"), float("inf")):
+        with pytest.raises(_lib.InaError):
+            ops.scale_for(bad, 8)
+    with pytest.raises(_lib.InaError):
+        ops.scale_for(1.0, 0)
+    with pytest.raises(_lib.InaError):
+        ops.scale_for(1.0, 8, bits=8)
+    with pytest.raises(_lib.InaError):
+        ops.scale_for(1.0, 70000, bits=16)      # W/2 alone exceeds 32767

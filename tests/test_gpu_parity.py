@@ -283,6 +283,53 @@ def test_ps_combine_random_vs_oracle():
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 1023, 100_003])
+@pytest.mark.parametrize("with_base", [False, True])
+def test_absmax_matches_numpy(n, with_base):
+    """Dynamic-scale absmax: max |x - base| with NaN ignored (the quantiser maps NaN to 0),
+    +-inf counted, over aligned and tail elements."""
+    rng = np.random.default_rng(n + 7 * with_base)
+    x = mixed_floats(rng, n)
+    base = (rng.standard_normal(n) * 3).astype(np.float32) if with_base else None
+    d = (x - base).astype(np.float32) if with_base else x
+    a = np.abs(d[~np.isnan(d)])
+    want = np.float32(a.max()) if a.size else np.float32(0)
+    got = host(ops().absmax(dev(x), dev(base) if with_base else None))[0]
+    assert got.view(np.uint32) == want.view(np.uint32)
+
+
+def test_absmax_unaligned_view_and_finite_pick():
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal(10_001) * 5).astype(np.float32)
+    x[5000] = -123.25
+    got = host(ops().absmax(dev(x)[1:]))[0]
+    assert got == np.float32(123.25)
+
+
+@pytest.mark.parametrize("W", [2, 8])
+def test_combine_ina_auto_scale_never_saturates(W):
+    """k="auto": the scale from the deltas' absmax keeps every quantised delta and the W-way
+    integer sum inside int32, and the update equals the oracle's at that k."""
+    from ina_amd import ps
+    rng = np.random.default_rng(W)
+    n = 40_000
+    local = rng.standard_normal(n).astype(np.float32)
+    paras = [(local + rng.standard_normal(n).astype(np.float32) * 10.0 ** rng.uniform(-4, 4)).astype(np.float32)
+             for _ in range(W)]
+    deltas = [(p - local).astype(np.float32) for p in paras]
+    amax = max(float(np.abs(d).max()) for d in deltas)
+    k = ops().scale_for(amax, W)
+    qs = [orc.quantize_i32(d, k) for d in deltas]
+    wide = np.sum([q.astype(np.int64) for q in qs], axis=0)
+    assert np.abs(wide).max() <= 2**31 - 1                      # no wrap at this k
+    assert all(np.abs(q.astype(np.int64)).max() < 2**31 - 1 for q in qs)
+    got = host(ps.combine_ina(dev(local), [dev(p) for p in paras], "auto", 1.0 / (W + 1)))
+    d = orc.dequantize_i32(orc.sum_reduce_i32(qs), k)
+    want = (local + (d * np.float32(1.0 / (W + 1))).astype(np.float32)).astype(np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert k == ops().scale_for_workers([dev(p) for p in paras], base=dev(local))
+
+
 def test_ps_apply_ina_update():
     rng = np.random.default_rng(12)
     n, W, k = 50_001, 4, 16
