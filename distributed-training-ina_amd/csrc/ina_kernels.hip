@@ -68,6 +68,9 @@ static std::atomic<int> g_stream_blocks{8192};
 static std::atomic<int> g_combine_blocks{256};
 static std::atomic<int> g_combine_ina_blocks{512};
 static std::atomic<int> g_nontemporal{1};
+// flat packet kernels index 16-byte chunks in 32 bits: a launch covers at most this many
+// chunks and longer batches go in packet ranges (tunable so tests reach the split path)
+static std::atomic<int64_t> g_launch_chunks{0x7FFFFFFF};
 
 static inline unsigned grid_for(size_t work_items, int per_thread, int cap_override = 0) {
     size_t per_block = (size_t)kBlock * (size_t)per_thread;
@@ -1168,7 +1171,7 @@ static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina
     if (pstride % 16 == 0 && V % 4 == 0 && src_aligned && aligned16(pkts)) {
         // 32-bit chunk indices: huge buckets go in packet ranges
         const size_t C = pstride / 16;
-        const size_t per = ((size_t)1 << 31) / C;
+        const size_t per = std::max<size_t>(1, (size_t)g_launch_chunks.load() / C);
         for (size_t p0 = 0; p0 < npk; p0 += per) {
             const size_t np = npk - p0 < per ? npk - p0 : per;
             const size_t v0 = p0 * (size_t)V;
@@ -1201,6 +1204,7 @@ int ina_set_tuning(int key, int value) {
         case 5: if (value < 1) return INA_EINVAL; g_combine_blocks = value; return INA_OK;
         case 6: if (value < 1) return INA_EINVAL; g_combine_ina_blocks = value; return INA_OK;
         case 7: return set_h2d_streams(value);
+        case 8: if (value < 1) return INA_EINVAL; g_launch_chunks = value; return INA_OK;
         default: return INA_EINVAL;
     }
 }
@@ -1436,7 +1440,7 @@ int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
     if (vals && V % 4 == 0 && pstride % 16 == 0 && aligned16(pkts) && aligned16(vals)) {
         // flat chunk stream; 32-bit chunk indices, so huge batches go in packet ranges
         const size_t C = pstride / 16;
-        const size_t per = ((size_t)1 << 31) / C;
+        const size_t per = std::max<size_t>(1, (size_t)g_launch_chunks.load() / C);
         for (size_t p0 = 0; p0 < npk; p0 += per) {
             const size_t np = npk - p0 < per ? npk - p0 : per;
             NgaFieldsDev fo = f;

@@ -372,6 +372,35 @@ def test_pack_nga_matches_oracle(V, n, layout):
         assert np.array_equal(host(f[key]).view(fo[key].dtype), fo[key]), key
 
 
+@pytest.mark.parametrize("chunks", [65, 100, 7 * 65])
+def test_flat_packet_kernels_split_launches(chunks):
+    """Batches longer than one launch's chunk range (2^31 16-byte chunks) go in packet
+    ranges; a small range forces the split here: pack, fused quantise+pack and unpack
+    stay byte-exact with ragged last ranges and header sequence numbers carried over."""
+    o = ops()
+    rng = np.random.default_rng(chunks)
+    V, n = 256, 256 * 37 + 19
+    vals = rand_i32(rng, n)
+    x = mixed_floats(rng, n)
+    npk = -(-n // V)
+    ovf = (rng.random(npk) < 0.5).astype(np.uint8)
+    try:
+        o.set_tuning(launch_chunks=chunks)
+        pk = host(o.pack_nga(dev(vals), V, 5, 8, 1, 4000, overflow=dev(ovf)))
+        qp = host(o.quantize_pack_nga(dev(x), 12, V, 5, 8, 1, 4000))
+        f, v = o.unpack_nga(dev(pk), V)
+        v = host(v)
+    finally:
+        o.set_tuning(launch_chunks=2**31 - 1)
+    st = o.nga_stride(V)
+    assert np.array_equal(pk, orc.pack_nga(vals, V, 5, 8, 1, 4000, ovf=ovf, stride=st))
+    assert np.array_equal(qp, orc.pack_nga(orc.quantize_i32(x, 12), V, 5, 8, 1, 4000, stride=st))
+    assert np.array_equal(v, np.concatenate([vals, np.zeros(npk * V - n, np.int32)]))
+    fo, _ = orc.unpack_nga(pk, V, stride=st)
+    for key in fo:
+        assert np.array_equal(host(f[key]).view(fo[key].dtype), fo[key]), key
+
+
 @pytest.mark.parametrize("case", manifest("nga_cases.json"), ids=lambda c: c["name"])
 def test_pack_nga_matches_reference_datagrams(case):
     """Device packets == the datagrams DataManager._send_data emitted (same int payload)."""
