@@ -2,7 +2,11 @@
 
 Each row: median device time of one launch (HIP events on the launch stream,
 20 launches after 3 warm-ups) and the algorithmic HBM bytes of that launch
-(SURVEY.md 8d), so GB/s = bytes / time and frac = GB/s / 8000.
+(SURVEY.md 8d), so GB/s = bytes / time and frac = GB/s / 8000.  Cold caches: a
+512 MiB buffer is READ before every timed launch (outside its events), so working
+sets below the 256 MB Infinity Cache do not replay from it ("cache
+flush between iterations").  The flush only reads: a written flush buffer would leave
+up to 256 MB of dirty lines whose write-back lands inside the next timed launch.
 """
 from __future__ import annotations
 
@@ -13,12 +17,25 @@ import torch
 HBM = 8000.0
 
 
-def _time(fn, reps=20, warm=3):
+_FLUSH = []
+
+
+def _flush():
+    from ina_amd import ops
+    if not _FLUSH:
+        _FLUSH.append(torch.ones(128 << 20, dtype=torch.int32, device="cuda"))   # 512 MiB
+        torch.cuda.synchronize()
+    ops.checksum(_FLUSH[0])          # streams 512 MiB in, writes 4 bytes
+
+
+def _time(fn, reps=20, warm=3, cold=True):
     s = torch.cuda.current_stream()
     for _ in range(warm):
         fn()
     ts = []
     for _ in range(reps):
+        if cold:
+            _flush()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
         fn()

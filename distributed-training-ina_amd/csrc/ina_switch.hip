@@ -414,6 +414,20 @@ constexpr int kB = INA_SWITCH_BATCH;         // packets of a segment loaded at o
 #define INA_SWITCH_WAVES 4
 #endif
 
+// packet chunk loads of the run kernel carry the streaming (nt) hint: 294 -> 276 us for
+// 819,200 NGA-256 packets (tools/lab/switch_lab.py, r01 session log switch_lab_nt.log);
+// nt on the forwarded-packet stores or on the key pass's header loads cost 10 us each
+#ifndef INA_SWITCH_NT
+#define INA_SWITCH_NT 1
+#endif
+__device__ __forceinline__ u32x4s sw_ld(const u32x4s* p) {
+#if INA_SWITCH_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 __device__ __forceinline__ uint32_t enc_lo(uint32_t prev, uint32_t v) {
     // LE dword: BE bytes 1..3 of prev followed by BE byte 0 of v
     return (__builtin_bswap32(prev) >> 8) | (v & 0xFF000000u);
@@ -500,12 +514,12 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                 uint32_t mypid = pid[0];
 #pragma unroll
                 for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
-                tl = reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride)[64];
+                tl = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
                 const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[b] * stride);
-                a[b] = pk[lane <= L ? lane : 0];
+                a[b] = sw_ld(pk + (lane <= L ? lane : 0));
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {

@@ -272,6 +272,24 @@ __global__ __launch_bounds__(B) void v_gs_buf(Ptrs in, u32x4* __restrict__ out, 
     }
 }
 
+// copy-class policy variants (LD/ST: 1 = nt, 0 = default), 4 chunks in flight per thread
+template <int B, int LD, int ST>
+__global__ __launch_bounds__(B) void v_copy_pol(Ptrs in, u32x4* __restrict__ out, size_t n4) {
+    const size_t tid = (size_t)blockIdx.x * B + threadIdx.x, stride = (size_t)gridDim.x * B;
+    size_t i = tid;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        u32x4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = LD ? ldnt(in.p[0] + i + u * stride) : in.p[0][i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (ST) __builtin_nontemporal_store(a[u], out + i + u * stride);
+            else out[i + u * stride] = a[u];
+        }
+    }
+    for (; i < n4; i += stride) out[i] = in.p[0][i];
+}
+
 using Kfn = void (*)(Ptrs, u32x4*, size_t);
 
 template <int B>
@@ -287,6 +305,7 @@ static Kfn pick(int variant, int U) {
         case 8: return U == 2 ? v_gs_sb<8, 2, B, 0> : v_gs_sb<8, 4, B, 0>;
         case 9: return U == 2 ? v_gs_sb<8, 2, B, 1> : v_gs_sb<8, 4, B, 1>;
         case 10: return U == 2 ? v_gs_plainst<8, 2, B> : v_gs_plainst<8, 4, B>;
+        case 12: return U == 0 ? v_copy_pol<B, 0, 0> : U == 1 ? v_copy_pol<B, 0, 1> : U == 2 ? v_copy_pol<B, 1, 0> : v_copy_pol<B, 1, 1>;
         case 11: return U == 2 ? v_gs_buf<8, 4, B, 2, 2> : U == 4 ? v_gs_buf<8, 4, B, 2, 0> : U == 5 ? v_gs_buf<8, 4, B, 2, 1> : v_gs_buf<8, 4, B, 0, 2>;
     }
     return nullptr;

@@ -46,6 +46,13 @@ if FOCUS == "sched":
         configs.append(("loads_first_schedbarrier", 9, U, B, G))
     for G in (1024, 2048):
         configs.append(("readonly8", 6, 1, 256, G))
+elif FOCUS == "copy":
+    # U field of variant 12: load/store policy (0 plain/plain, 1 plain/nt, 2 nt/plain, 3 nt/nt)
+    for pol in (0, 1, 2, 3):
+        for G in (512, 1024, 2048, 4096, 8192):
+            configs.append((f"copy_pol{pol}", 12, pol, 256, G))
+    for G in (4096, 16384):
+        configs.append(("copy", 7, 1, 256, G))
 elif FOCUS == "store":
     # U field: variant 11 packs the cache-policy pair: 2 = nt/nt, 4 = nt/default,
     # 5 = nt/sc0, 6 = default/nt
@@ -78,18 +85,24 @@ else:
 
 
 def nbytes(v):
-    return {6: W * N * 4, 7: 2 * N * 4}.get(v, (W + 1) * N * 4)
+    return {6: W * N * 4, 7: 2 * N * 4, 12: 2 * N * 4}.get(v, (W + 1) * N * 4)
+
+
+# copy variants read buffer k % 16 (1.7 GB rotation, never resident in the 256 MB MALL)
+flat = [b for st in sets for b in st]
+carrs = [(C.c_void_p * W)(*([flat[j].data_ptr()] * W)) for j in range(len(flat))]
 
 
 def launch(cfg, k):
     name, v, U, B, G = cfg
-    rc = lab.lab_launch(v, W, U, B, G, arrs[k % 2], outs[k % 2].data_ptr(), N // 4, stream)
+    arr = carrs[k % len(carrs)] if v in (7, 12) else arrs[k % 2]
+    rc = lab.lab_launch(v, W, U, B, G, arr, outs[k % 2].data_ptr(), N // 4, stream)
     assert rc == 0, (cfg, rc)
 
 
 bad = []
 for cfg in configs:
-    if cfg[1] in (6, 7):
+    if cfg[1] in (6, 7, 12):
         continue
     outs[0].zero_()
     launch(cfg, 0)
