@@ -149,7 +149,7 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
         "kind": "port",
         "sample": (f"{W} workers x {n} int32 (first {n * 4 // (1 << 20)} MiB of each config-3 "
                    f"bucket): NGA-{V_SLOT} packetise (header + memcpy + htonl per packet, "
-                   f"communicator.cc:51-63) -> P4 aggregator restatement (count/frag/Processor "
+                   f"communicator.cc:23-37) -> P4 aggregator restatement (count/frag/Processor "
                    f"registers, ngaa.p4:120-196) -> PS ack, median of 3, {threads} threads split "
                    f"as communicator.py:133-157"),
         "value_1core": round(W * n * 4 / t1 / 1e9, 3),

@@ -369,7 +369,7 @@ int orc_switch_packet(orc_switch_t* sw, uint8_t* pk) {
 
 /* ------------------------------------------------------------------------- */
 /* CPU baseline: the reference's CPU packetise + aggregate path, end to end.   */
-/* Per slot and worker: build the packet the way communicator.cc:51-63 does    */
+/* Per slot and worker: build the packet the way communicator.cc:23-37 does    */
 /* (header + memcpy + htonl) into a per-packet buffer that stands in for the   */
 /* sendto() sink, run it through the P4 aggregator restated above; the PS      */
 /* unpacks the completed packet (ntohl) and acks the slot (fragcheck.p4:26).   */

@@ -2,7 +2,8 @@
 # GPU-box session: parity tests -> bench -> rocprofv3 kernel trace -> PMC passes.
 # Every GPU step has its own time limit; the script stops at the first crash,
 # abort or timeout (only an ordinary pytest failure, rc 1, lets it continue).
-# usage: tools/gpu_session.sh TAG [stages...]   stages: test bench prof pmc extra smoke
+# usage: tools/gpu_session.sh TAG [stages...]   stages: smoke test bench prof pmc extra swprof
+#        config1 rehearse sharded
 set -u
 TAG=${1:-r01}; shift || true
 STAGES=${*:-"smoke test bench prof pmc extra"}
@@ -31,6 +32,15 @@ for st in $STAGES; do
         timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o run -- \
           python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
         rc=$?; tail -2 "$OUT/pmc_$c.err"; [ $rc -ne 0 ] && fatal "pmc $c" $rc
+      done ;;
+    swprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/swprof" -o run -- \
+        python3 tools/prof_switch.py > "$OUT/swprof.log" 2>&1
+      rc=$?; tail -2 "$OUT/swprof.log"; [ $rc -ne 0 ] && fatal swprof $rc
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/swpmc_$c" -o run -- \
+          python3 tools/prof_switch.py > "$OUT/swpmc_$c.log" 2>&1
+        rc=$?; tail -2 "$OUT/swpmc_$c.log"; [ $rc -ne 0 ] && fatal "swpmc $c" $rc
       done ;;
     config1)
       timeout -k 10 600 python examples/config1_loopback.py --epochs 3 --local-steps 5 > "$OUT/config1.log" 2>&1
