@@ -304,6 +304,9 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
     const int V = st.V;
     uint8_t* lds = stage[wv];
     const bool vec = (stride % 16 == 0) && (((uintptr_t)pkts & 15u) == 0);
+    // the program reads and rewrites header + payload only (15 + 4V <= 1039 bytes); row
+    // padding past kMaxStride is never staged
+    const size_t span = stride < (size_t)kMaxStride ? stride : (size_t)kMaxStride;
 
     // slot state into registers: count, frag (scalar) and V registers (<= 4 per lane)
     uint32_t cnt = st.count[slot];
@@ -320,10 +323,10 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
         uint8_t* pk = pkts + (size_t)pid * stride;
         // stage the packet in LDS
         if (vec) {
-            for (size_t b = 16 * (size_t)lane; b < stride; b += 64 * 16)
+            for (size_t b = 16 * (size_t)lane; b < span; b += 64 * 16)
                 *reinterpret_cast<u32x4s*>(lds + b) = *reinterpret_cast<const u32x4s*>(pk + b);
         } else {
-            for (size_t b = lane; b < stride; b += 64) lds[b] = pk[b];
+            for (size_t b = lane; b < span; b += 64) lds[b] = pk[b];
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -374,10 +377,10 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         if (rewrite) {
             if (vec) {
-                for (size_t b = 16 * (size_t)lane; b < stride; b += 64 * 16)
+                for (size_t b = 16 * (size_t)lane; b < span; b += 64 * 16)
                     *reinterpret_cast<u32x4s*>(pk + b) = *reinterpret_cast<const u32x4s*>(lds + b);
             } else {
-                for (size_t b = lane; b < stride; b += 64) pk[b] = lds[b];
+                for (size_t b = lane; b < span; b += 64) pk[b] = lds[b];
             }
         }
         if (lane == 0) actions[pid] = act;
@@ -694,8 +697,9 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
                        uint8_t* actions, void* scratch, ina_stream_t stream) {
     if (!st || st->V <= 0 || st->V > kMaxV || st->num_slots == 0)
         return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
-    if (stride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)st->V || stride > (size_t)kMaxStride)
-        return set_error(INA_EINVAL, "stride must be in [15+4V, 1040]%s", "");
+    if (stride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)st->V)
+        return set_error(INA_EINVAL, "stride must be >= 15+4V%s", "");
+    if (stride > 0xFFFFFFFFu) return set_error(INA_EINVAL, "stride too large%s", "");
     if (npk == 0) return INA_OK;
     if (npk > 0x7FFFFFFFu) return set_error(INA_EINVAL, "too many packets%s", "");
     if (!pkts || !actions || !scratch || !st->count || !st->frag || !st->regs)

@@ -1,0 +1,106 @@
+// capi_check.cpp -- a C/C++ caller of libina.so with no Python and no torch: links the
+// library through include/ina.h only, allocates device memory with the HIP runtime,
+// runs quantise -> W-way sum-reduce -> NGA-256 pack -> unpack -> dequantise and checks
+// every step against a host computation.  Built by `make -C examples`; run by
+// tests/test_gpu_capi_binary.py on the GPU box.  Exit status 0 = all checks passed.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "ina.h"
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        int rc_ = (x);                                                           \
+        if (rc_ != 0) {                                                          \
+            std::fprintf(stderr, "%s failed: %d (%s)\n", #x, rc_, ina_last_error_string()); \
+            return 1;                                                            \
+        }                                                                        \
+    } while (0)
+#define HK(x)                                                                    \
+    do {                                                                         \
+        if ((x) != hipSuccess) {                                                 \
+            std::fprintf(stderr, "%s failed\n", #x);                             \
+            return 1;                                                            \
+        }                                                                        \
+    } while (0)
+
+static int32_t q_host(float x, int k) {   // the build-defined quantiser (include/ina.h)
+    if (x != x) return 0;
+    const double y = std::nearbyint((double)x * std::ldexp(1.0, k));   // RNE (default mode)
+    if (y >= 2147483647.0) return INT32_MAX;
+    if (y <= -2147483648.0) return INT32_MIN;
+    return (int32_t)y;
+}
+
+int main() {
+    const int W = 8, k = 16, V = 256;
+    const size_t n = 1000003;
+    std::printf("%s\n", ina_version());
+    std::vector<std::vector<float>> g(W, std::vector<float>(n));
+    uint32_t seed = 12345;
+    for (int w = 0; w < W; ++w)
+        for (size_t i = 0; i < n; ++i) {
+            seed = seed * 1664525u + 1013904223u;
+            g[w][i] = ((int32_t)seed >> 8) * 1e-9f;
+        }
+    float* d_g[W];
+    int32_t* d_q[W];
+    for (int w = 0; w < W; ++w) {
+        HK(hipMalloc(&d_g[w], n * 4));
+        HK(hipMalloc(&d_q[w], n * 4));
+        HK(hipMemcpy(d_g[w], g[w].data(), n * 4, hipMemcpyHostToDevice));
+    }
+    int32_t* d_sum;
+    HK(hipMalloc(&d_sum, n * 4));
+    hipStream_t s;
+    HK(hipStreamCreate(&s));
+    for (int w = 0; w < W; ++w) CK(ina_quantize_f32_i32(d_g[w], d_q[w], n, k, s));
+    CK(ina_sum_reduce_i32((const int32_t* const*)d_q, W, d_sum, n, s));
+
+    const size_t stride = (15 + 4 * V + 15) / 16 * 16, npk = (n + V - 1) / V;
+    uint8_t* d_pk;
+    HK(hipMalloc(&d_pk, npk * stride));
+    ina_nga_params_t prm;
+    std::memset(&prm, 0, sizeof prm);
+    prm.bitmap = 1; prm.count = W; prm.switch_id = 1; prm.seq0 = 1;
+    prm.num_slots = INA_NUM_REGISTER; prm.V = V;
+    CK(ina_pack_nga(d_sum, n, &prm, nullptr, d_pk, stride, s));
+    int32_t* d_back;
+    HK(hipMalloc(&d_back, npk * V * 4));
+    CK(ina_unpack_nga(d_pk, npk, V, stride, nullptr, d_back, s));
+    float* d_f;
+    HK(hipMalloc(&d_f, n * 4));
+    CK(ina_dequantize_i32_f32(d_back, d_f, n, k, s));
+    HK(hipStreamSynchronize(s));
+
+    std::vector<int32_t> sum(n), back(npk * V);
+    std::vector<float> f(n);
+    std::vector<uint8_t> pk(npk * stride);
+    HK(hipMemcpy(sum.data(), d_sum, n * 4, hipMemcpyDeviceToHost));
+    HK(hipMemcpy(back.data(), d_back, npk * V * 4, hipMemcpyDeviceToHost));
+    HK(hipMemcpy(f.data(), d_f, n * 4, hipMemcpyDeviceToHost));
+    HK(hipMemcpy(pk.data(), d_pk, npk * stride, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t want = 0;
+        for (int w = 0; w < W; ++w) want += (uint32_t)q_host(g[w][i], k);
+        if ((uint32_t)sum[i] != want || back[i] != sum[i] ||
+            f[i] != (float)sum[i] * std::ldexp(1.0f, -k))
+            ++bad;
+        // wire bytes: value i of packet i / V at 15 + 4 (i % V), big-endian
+        const uint8_t* b = &pk[(i / V) * stride + 15 + 4 * (i % V)];
+        const uint32_t be = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+        if (be != want) ++bad;
+    }
+    for (size_t i = n; i < npk * V; ++i) bad += back[i] != 0;   // zero-padded tail
+    // the error path: a bad argument returns a code, sets a message, never exits
+    const int rc = ina_sum_reduce_i32((const int32_t* const*)d_q, 0, d_sum, n, s);
+    if (rc != INA_EINVAL || std::strlen(ina_last_error_string()) == 0) ++bad;
+    std::printf("capi_check: %zu values x %d workers, %zu mismatches\n", n, W, bad);
+    return bad ? 1 : 0;
+}

@@ -504,6 +504,44 @@ def test_switch_stream_matches_oracle(V, num_slots, W, used, stride, write_dropp
         assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_switch_fuzz_vs_oracle(seed):
+    """Randomised configurations: V (incl. the LDS-staged path for V % 4 != 0 or unaligned
+    strides), pool size (1..2^18 slots: 1-3 sort passes, long segments in small pools),
+    worker count, collision / ack / foreign-switch rates, write_dropped, 2-4 batches with
+    the switch state carried over -- bit-exact actions, packets and registers."""
+    rng = np.random.default_rng(90_000 + seed)
+    o = ops()
+    V = int(rng.choice([4, 8, 32, 64, 100, 128, 256, 33, 7]))
+    num_slots = int(rng.choice([1, 3, 64, 1000, 16384, 1 << 17, (1 << 18) - 5]))
+    W = int(rng.integers(1, 21))
+    used = int(rng.integers(1, 120))
+    layout = rng.choice(["padded", "tight", "wide"])
+    stride = {"padded": o.nga_stride(V), "tight": 15 + 4 * V, "wide": o.nga_stride(V) + 32}[layout]
+    wd = bool(rng.integers(0, 2))
+    sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=wd)
+    sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+    for rnd in range(int(rng.integers(2, 5))):
+        stream = make_stream(rng, V, used, W, num_slots, collide=float(rng.uniform(0, 0.3)),
+                             ack=float(rng.uniform(0, 0.3)), other=float(rng.uniform(0, 0.2)),
+                             stride=stride)
+        want_pk, want_act = sw_orc.run(stream, stride=stride)
+        d = dev(stream)
+        act = sw_dev.process(d)
+        assert np.array_equal(host(act), want_act), (seed, rnd)
+        got_pk = host(d)
+        if wd:
+            assert np.array_equal(got_pk, want_pk), (seed, rnd)
+        else:
+            fwd = want_act != orc.ACT_DROP
+            assert np.array_equal(got_pk[fwd], want_pk[fwd]), (seed, rnd)
+            assert np.array_equal(got_pk[~fwd], stream[~fwd]), (seed, rnd)
+    cnt, frag, regs = sw_orc.registers()
+    assert np.array_equal(host(sw_dev.count), cnt)
+    assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+    assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+
+
 def test_switch_collision_free_equals_bulk_reduce():
     """Stateful device switch over a full W-worker stream == the bulk sum-reduce."""
     rng = np.random.default_rng(77)
