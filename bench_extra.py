@@ -218,6 +218,18 @@ def run_extra(dev):
                      note="GB/s column = worker fp32 bytes aggregated per second through the packet path"))
     del xs, glob_p, upd, acks, ack_acts, rows_w, stream
 
+    # small batches through the switch (P4 format: NGA-32, 16,384-slot pool): latency of
+    # one ina_switch_process call, the stand-in's per-batch cost when packets arrive in
+    # recvmmsg-sized batches
+    for nb in (64, 1024, 16384):
+        sw32 = ops.Switch(32, num_slots=16384, switch_id=1, device=dev)
+        small = torch.cat([ops.pack_nga(rnd_i32(32 * nb // 8), 32, w + 1, 8, 1, 1) for w in range(8)])
+        a32 = torch.empty(small.shape[0], dtype=torch.uint8, device=dev)
+        rows.append(_row(f"switch_process small batch: {small.shape[0]} NGA-32 packets",
+                         _time(lambda: sw32.process(small, a32), reps=20, warm=3),
+                         small.numel(), note="latency row; bytes = packet bytes read"))
+        del sw32, small, a32
+
     # --- end to end: pinned host -> HBM -> reduce -> pinned host -------------------------------
     hosts = [b.cpu().pin_memory() for b in b3]
     hout = torch.empty(n3, dtype=torch.int32).pin_memory()

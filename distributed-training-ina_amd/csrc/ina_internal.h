@@ -15,6 +15,7 @@ struct PtrPack {
 
 int set_error(int code, const char* fmt, const char* detail);
 int set_h2d_streams(int v);   // ina_host.cpp
+int set_small_sort(int v);    // ina_switch.hip
 
 }  // namespace ina
 

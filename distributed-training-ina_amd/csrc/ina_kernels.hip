@@ -1208,6 +1208,7 @@ int ina_set_tuning(int key, int value) {
         case 6: if (value < 1) return INA_EINVAL; g_combine_ina_blocks = value; return INA_OK;
         case 7: return set_h2d_streams(value);
         case 8: if (value < 1) return INA_EINVAL; g_launch_chunks = value; return INA_OK;
+        case 9: return set_small_sort(value);
         default: return INA_EINVAL;
     }
 }

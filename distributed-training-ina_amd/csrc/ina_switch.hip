@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "ina.h"
 #include "ina_internal.h"
@@ -150,6 +151,86 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
+}
+
+// 1b. batches of at most kSmallBatch packets (recvmmsg-sized, where launch latency and not
+//     bandwidth is the cost): keys and the whole sort in ONE workgroup.  The (slot, packet
+//     id) pairs are unique 64-bit values, so sorting them -- a bitonic network in LDS --
+//     gives the stable slot order with no rank bookkeeping; then the run kernel: two
+//     launches instead of seven.
+constexpr int kSmallBatch = 4096;                 // LDS capacity of the one-workgroup sort
+#ifndef INA_SWITCH_SMALL_MAX
+#define INA_SWITCH_SMALL_MAX 2048
+#endif
+static_assert(INA_SWITCH_SMALL_MAX <= kSmallBatch, "small path limited by its LDS");
+constexpr int kSmallBlock = 1024;
+static std::atomic<int> g_small_sort{1};   // ina_set_tuning key 9 (0: always the radix path)
+int set_small_sort(int v) {
+    g_small_sort = v ? 1 : 0;
+    return INA_OK;
+}
+
+// T = uint32_t packs (slot << 12 | id) when num_slots + 1 <= 2^20, else uint64_t (slot << 32
+// | id).  Compare-exchange stages with j < 64 pair elements inside one wave's 64-element
+// groups, so they need only a wave barrier; the 21 stages with j >= 64 (M = 4096) need
+// the workgroup's.
+template <typename T, int kIdBits>
+__global__ __launch_bounds__(kSmallBlock) void k_switch_sort_small(
+        const uint8_t* __restrict__ pkts, uint32_t npk, size_t stride, uint32_t num_slots,
+        int switch_id, uint8_t* __restrict__ actions, uint32_t* __restrict__ keys,
+        uint32_t* __restrict__ ids) {
+    __shared__ T v[kSmallBatch];
+    uint32_t M = 1;
+    while (M < npk) M <<= 1;
+    const bool al4 = (stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0;
+    for (uint32_t p = threadIdx.x; p < M; p += kSmallBlock) {
+        T c = ~(T)0;                                        // padding sorts last
+        if (p < npk) {
+            const uint8_t* pk = pkts + (size_t)p * stride;
+            uint32_t idx, sid;
+            if (al4) {                                      // header bytes 4..11
+                const uint32_t w1 = reinterpret_cast<const uint32_t*>(pk)[1];
+                const uint32_t w2 = reinterpret_cast<const uint32_t*>(pk)[2];
+                idx = __builtin_bswap32((w1 >> 16) | (w2 << 16));
+                sid = (w2 >> 16) & 0xFFu;
+            } else {
+                idx = rd_be32(pk + 6);
+                sid = pk[10];
+            }
+            const bool mine = switch_id >= 0 && sid == (uint32_t)(uint8_t)switch_id;
+            const uint32_t key = mine ? idx % num_slots : num_slots;
+            if (!mine) actions[p] = INA_ACT_FWD_OTHER;      // switch_check miss, ngaa.p4:184-186
+            c = ((T)key << kIdBits) | (T)p;
+        }
+        v[p] = c;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= M; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < M; i += kSmallBlock) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const T a = v[i], b = v[l];
+                    if ((a > b) == ((i & k) == 0)) {
+                        v[i] = b;
+                        v[l] = a;
+                    }
+                }
+            }
+            if (j > 32) {
+                __syncthreads();
+            } else {                                        // partners in the same wave
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t p = threadIdx.x; p < npk; p += kSmallBlock) {
+        keys[p] = (uint32_t)(v[p] >> kIdBits);
+        ids[p] = (uint32_t)(v[p] & (((T)1 << kIdBits) - 1));
+    }
 }
 
 // later passes: chunk histogram of digit (key >> shift)
@@ -412,6 +493,17 @@ __global__ __launch_bounds__(kSwBlock) void k_switch_run(ina_switch_state_t st,
 #define INA_SWITCH_BATCH 8
 #endif
 constexpr int kB = INA_SWITCH_BATCH;         // packets of a segment loaded at once
+#ifndef INA_SWITCH_WIN_SMALL
+#define INA_SWITCH_WIN_SMALL 8
+#endif
+#ifndef INA_SWITCH_WIN_LARGE
+#define INA_SWITCH_WIN_LARGE 16
+#endif
+#ifndef INA_SWITCH_GRID
+#define INA_SWITCH_GRID (1 << 20)
+#endif
+static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWITCH_WIN_LARGE >= 1 &&
+              INA_SWITCH_WIN_LARGE <= 64, "a window is at most one wave of keys");
 // occupancy target of k_switch_run2 (waves per SIMD); 4 fits its registers, 5 spills 4
 #ifndef INA_SWITCH_WAVES
 #define INA_SWITCH_WAVES 4
@@ -441,7 +533,8 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                                                           size_t stride,
                                                           const uint32_t* __restrict__ keys,
                                                           const uint32_t* __restrict__ ids,
-                                                          uint8_t* __restrict__ actions) {
+                                                          uint8_t* __restrict__ actions,
+                                                          uint32_t win) {
     const int lane = threadIdx.x & 63;
     const int V = st.V;
     const int L = V >> 2;                       // lanes holding values
@@ -452,12 +545,12 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
     const uint32_t NS = st.num_slots;
     // each wave takes windows of 64 sorted positions and processes the segments that
     // START in its window (a segment may run past the window's end)
-    for (size_t w0 = wave * 64; w0 < npk; w0 += nwaves * 64) {
+    for (size_t w0 = wave * win; w0 < npk; w0 += nwaves * win) {
         const size_t i = w0 + (size_t)lane;
         const uint32_t ki = i < npk ? keys[i] : NS;
         const uint32_t idw = i < npk ? ids[i] : 0u;     // packet ids of the window, one load
         const uint32_t kp = (i > 0 && i <= npk) ? keys[i - 1] : 0xFFFFFFFFu;
-        unsigned long long hm = __ballot(i < npk && ki < NS && (i == 0 || kp != ki));
+        unsigned long long hm = __ballot((uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki));
         while (hm) {
         const int hl = __builtin_ctzll(hm);
         hm &= hm - 1;
@@ -718,12 +811,23 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
     const uint32_t nb = 1u << sp.bits;
     const unsigned gd = (nb + kRsWaves - 1) / kRsWaves;
 
-    hipLaunchKernelGGL(k_switch_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts, npk, stride,
-                       st->num_slots, st->switch_id, k_in, actions, sp.bits, hist, sp.nch);
-    if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
-    // digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
     uint32_t *kc = k_in, *vc = v_in, *kn = k_out, *vn = v_out;
-    for (int pass = 0; pass < sp.passes; ++pass) {
+    const bool small = npk <= (size_t)INA_SWITCH_SMALL_MAX && g_small_sort.load();
+    if (small) {
+        if ((uint64_t)st->num_slots + 1 <= (1u << 20))
+            hipLaunchKernelGGL((k_switch_sort_small<uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, pkts,
+                               (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
+        else
+            hipLaunchKernelGGL((k_switch_sort_small<unsigned long long, 32>), dim3(1), dim3(kSmallBlock), 0,
+                               s, pkts, (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
+        if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
+    } else {
+        hipLaunchKernelGGL(k_switch_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts, npk, stride,
+                           st->num_slots, st->switch_id, k_in, actions, sp.bits, hist, sp.nch);
+        if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
+    }
+    // digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
+    for (int pass = 0; pass < (small ? 0 : sp.passes); ++pass) {
         const int shift = pass * sp.bits;
         if (pass > 0)
             hipLaunchKernelGGL(k_rs_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits,
@@ -742,9 +846,16 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
     const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
                       st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
     if (fast) {
-        unsigned gr = (unsigned)std::min<size_t>((npk + kSwBlock - 1) / kSwBlock, 2048);
+        // a wave runs the segments that start in its window of `win` sorted positions: a
+        // segment is a chain of dependent round trips, so small windows (more waves) win
+        // at every size -- tools/lab/switch_lab.py, profiles/r01/lab/switch_lab_win.log:
+        // 1,024 packets 52.9 -> 27.7 us (64 -> 8 positions), 819,200 packets 277 -> 266 us
+        // (64 -> 16 positions, one pass of the grid)
+        const uint32_t win = npk <= 65536 ? (uint32_t)INA_SWITCH_WIN_SMALL : (uint32_t)INA_SWITCH_WIN_LARGE;
+        const size_t per_block = (size_t)win * (kSwBlock / 64);
+        unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         hipLaunchKernelGGL(k_switch_run2, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,
-                           vc, actions);
+                           vc, actions, win);
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
         hipLaunchKernelGGL(k_switch_run, dim3(gw), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,

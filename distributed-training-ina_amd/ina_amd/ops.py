@@ -408,13 +408,14 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                nontemporal: bool | None = None, reduce_blocks: int | None = None,
                stream_blocks: int | None = None, combine_blocks: int | None = None,
                combine_ina_blocks: int | None = None, h2d_streams: int | None = None,
-               launch_chunks: int | None = None):
+               launch_chunks: int | None = None, switch_small_sort: bool | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
     PS combine, combine_ina_blocks the INA-semantics combine, h2d_streams the host-ingest
     pipeline's H2D copy streams (1 or 2), launch_chunks the 16-byte chunks one flat packet
-    kernel launch covers (default 2^31 - 1; smaller values only split launches); unroll is the sum-reduce's 16-byte chunks per worker per thread."""
+    kernel launch covers (default 2^31 - 1; smaller values only split launches),
+    switch_small_sort the one-workgroup key+sort path for switch batches <= 4096 packets; unroll is the sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")
@@ -428,6 +429,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(7, int(h2d_streams)), "set_tuning")
     if launch_chunks is not None:
         check(lib.ina_set_tuning(8, int(launch_chunks)), "set_tuning")
+    if switch_small_sort is not None:
+        check(lib.ina_set_tuning(9, int(bool(switch_small_sort))), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

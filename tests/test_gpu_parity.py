@@ -542,6 +542,35 @@ def test_switch_fuzz_vs_oracle(seed):
     assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_switch_small_batch_paths_agree(seed):
+    """Batches of <= 4096 packets take the one-workgroup key+bitonic-sort path; the same
+    batches through the chunked radix path give identical actions, packets and registers
+    (and both equal the P4 restatement)."""
+    rng = np.random.default_rng(70_000 + seed)
+    o = ops()
+    V = int(rng.choice([32, 256, 33]))
+    num_slots = int(rng.choice([3, 64, 16384, 1 << 17]))
+    W = int(rng.integers(1, 17))
+    used = int(rng.integers(1, 4096 // W + 1))
+    stream = make_stream(rng, V, used, W, num_slots, stride=o.nga_stride(V))
+    assert stream.shape[0] <= 4096
+    want_pk, want_act = orc.Switch(V, num_slots=num_slots, switch_id=1).run(stream, stride=o.nga_stride(V))
+    outs = []
+    for small in (True, False):
+        sw = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
+        d = dev(stream)
+        try:
+            o.set_tuning(switch_small_sort=small)
+            act = sw.process(d)
+        finally:
+            o.set_tuning(switch_small_sort=True)
+        outs.append((host(act), host(d), host(sw.regs)))
+    for act, pk, regs in outs:
+        assert np.array_equal(act, want_act) and np.array_equal(pk, want_pk)
+    assert np.array_equal(outs[0][2], outs[1][2])
+
+
 def test_switch_collision_free_equals_bulk_reduce():
     """Stateful device switch over a full W-worker stream == the bulk sum-reduce."""
     rng = np.random.default_rng(77)

@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
 from ina_amd import _lib, ops  # noqa: E402
 
-n, W, V = int(os.environ.get("N", 26_214_400)), 8, 256
+n, W, V = int(os.environ.get("N", 26_214_400)), 8, int(os.environ.get("V", 256))
 slots = 1 << 17
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(1)
