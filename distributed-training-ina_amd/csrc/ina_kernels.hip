@@ -735,6 +735,15 @@ __device__ __forceinline__ uint32_t nga_val(const Src& src, size_t n, size_t p, 
 // fp32) and takes value 4c -- the next chunk's first -- from the next lane (DPP
 // wave_shl:1; lane 63 loads it).  Chunk 0 is the header plus value 0's top byte.
 constexpr uint32_t kSelWire = 0x07000102u;   // perm(next, v): {v.b2, v.b1, v.b0, next.b3}
+// 16-byte chunks in flight per thread in the flat packet kernels: one (with the 8192-
+// workgroup grid striding over the rest) beat 2, 4 and 8 -- fused worker pack 57.7 -> 54.2
+// us, pack 37.5 -> 36.5, unpack 40.4 -> 39.1 (tools/lab/apply_lab.py, lab/pack_u_lab.log)
+#ifndef INA_PACK_U
+#define INA_PACK_U 1
+#endif
+#ifndef INA_UNPACK_U
+#define INA_UNPACK_U 1
+#endif
 
 template <typename Src, int U>
 __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, NgaHdr h,
@@ -1180,7 +1189,7 @@ static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina
             const size_t v0 = p0 * (size_t)V;
             NgaHdr hp = h;
             hp.seq0 = h.seq0 + (uint32_t)p0;
-            hipLaunchKernelGGL((k_pack_nga_flat<Src, 4>), dim3(grid_for(np * C, 4, g_stream_blocks)),
+            hipLaunchKernelGGL((k_pack_nga_flat<Src, INA_PACK_U>), dim3(grid_for(np * C, INA_PACK_U, g_stream_blocks)),
                                dim3(kBlock), 0, s, src.shifted(v0), n - v0, hp, ovf ? ovf + p0 : nullptr,
                                pkts + p0 * pstride, (uint32_t)C, (uint32_t)(V / 4), (uint32_t)(np * C));
         }
@@ -1454,7 +1463,7 @@ int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,
             if (fo.index) fo.index += p0;
             if (fo.switch_id) fo.switch_id += p0;
             if (fo.frag_id) fo.frag_id += p0;
-            hipLaunchKernelGGL(k_unpack_nga_flat<4>, dim3(grid_for(np * C, 4, g_stream_blocks)),
+            hipLaunchKernelGGL(k_unpack_nga_flat<INA_UNPACK_U>, dim3(grid_for(np * C, INA_UNPACK_U, g_stream_blocks)),
                                dim3(kBlock), 0, s, pkts + p0 * pstride, (uint32_t)C, (uint32_t)(V / 4),
                                (uint32_t)(np * C), fo, fields ? 1 : 0, vals + p0 * (size_t)V,
                                (uint32_t)V);

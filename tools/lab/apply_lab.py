@@ -31,24 +31,37 @@ nr = 25_557_032
 xr = torch.randn(nr, device=dev, generator=g) * 1e-2
 br = torch.randn(nr, device=dev, generator=g) * 1e-2
 st = torch.cuda.current_stream().cuda_stream
+src_i32 = torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
+flush = torch.ones(128 << 20, dtype=torch.int32, device=dev)
 
 
 class Variant:
     def __init__(self, path):
         self.name = os.path.basename(path)
         self.lib = C.CDLL(path)
-        for nm in ("ina_apply_completed_nga", "ina_quantize_pack_nga"):
+        if os.environ.get("STREAM_BLOCKS"):
+            self.lib.ina_set_tuning(4, int(os.environ["STREAM_BLOCKS"]))
+        for nm in ("ina_apply_completed_nga", "ina_quantize_pack_nga", "ina_pack_nga", "ina_unpack_nga"):
             getattr(self.lib, nm).argtypes = _lib.SIGNATURES[nm]
         self.out = torch.empty_like(local)
         self.acks = torch.empty((nslot, stride), dtype=torch.uint8, device=dev)
         self.pk = torch.empty(((nr + V - 1) // V, stride), dtype=torch.uint8, device=dev)
         self.prm = _lib.NgaParams(1, 8, 0, 1, 0, 1, 16384, V)
-        self.t = {"apply": [], "qpack": []}
+        self.t = {"apply": [], "qpack": [], "pack": [], "unpack": []}
+        self.pk3 = torch.empty((n // V, stride), dtype=torch.uint8, device=dev)
+        self.vals = torch.empty(n, dtype=torch.int32, device=dev)
 
     def apply(self):
         return self.lib.ina_apply_completed_nga(stream.data_ptr(), npk_all, V, stride, acts.data_ptr(), 1,
                                                 local.data_ptr(), 16, 0.1, self.out.data_ptr(), n,
                                                 self.acks.data_ptr(), stride, st)
+
+    def pack(self):
+        return self.lib.ina_pack_nga(src_i32.data_ptr(), n, C.byref(self.prm), None, self.pk3.data_ptr(),
+                                     stride, st)
+
+    def unpack(self):
+        return self.lib.ina_unpack_nga(self.pk3.data_ptr(), n // V, V, stride, None, self.vals.data_ptr(), st)
 
     def qpack(self):
         return self.lib.ina_quantize_pack_nga(xr.data_ptr(), br.data_ptr(), nr, 16, C.byref(self.prm),
@@ -58,10 +71,13 @@ class Variant:
 vs = [Variant(p) for p in sys.argv[1:]]
 for v in vs:
     v.out.fill_(float("nan"))
-    assert v.apply() == 0 and v.qpack() == 0
+    assert v.apply() == 0 and v.qpack() == 0 and v.pack() == 0 and v.unpack() == 0
 torch.cuda.synchronize()
 bad = False
 for v in vs[1:]:
+    if not (torch.equal(v.pk3, vs[0].pk3) and torch.equal(v.vals, vs[0].vals)):
+        print("pack/unpack differ:", v.name)
+        bad = True
     if not torch.equal(v.pk, vs[0].pk):
         print("qpack differs:", v.name, int((v.pk != vs[0].pk).sum()))
         bad = True
@@ -76,9 +92,10 @@ if bad:
     sys.exit(1)
 for r in range(int(os.environ.get("ROUNDS", 8))):
     for v in vs:
-        for op in ("apply", "qpack"):
+        for op in ("apply", "qpack", "pack", "unpack"):
             evs = []
             for _ in range(4):
+                ops.checksum(flush)                  # cold caches (read-only flush)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 assert getattr(v, op)() == 0
@@ -87,4 +104,4 @@ for r in range(int(os.environ.get("ROUNDS", 8))):
             torch.cuda.synchronize()
             v.t[op] += [a.elapsed_time(b) * 1e3 for a, b in evs[1:]]
 for v in vs:
-    print(f"{v.name:22s} apply {statistics.median(v.t['apply']):7.1f} us   qpack {statistics.median(v.t['qpack']):7.1f} us")
+    print(f"{v.name:22s} " + "  ".join(f"{op} {statistics.median(v.t[op]):6.1f} us" for op in v.t))
