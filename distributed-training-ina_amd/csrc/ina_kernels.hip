@@ -60,6 +60,16 @@ static std::atomic<int> g_max_blocks{8192};   // elementwise kernels (kern_lab: 
 // workgroups (W = 2, 4: 256; W = 8: 512; W = 16: 1024).  0 = that rule; >0 overrides.
 static std::atomic<int> g_reduce_blocks{0};
 static std::atomic<int> g_unroll{4};
+// 16-byte chunks in flight per thread in the one-in one-out elementwise kernels
+// (quantise, dequantise, PS apply): one, with the 8192-workgroup grid striding, beat 2
+// and 4 -- quantise 40.9 -> 37.6 us, dequantise 41.2 -> 36.8 (tools/lab/ew_lab.py)
+#ifndef INA_EW_U
+#define INA_EW_U 1
+#endif
+constexpr int kEwU = INA_EW_U;
+#ifndef INA_QR_U
+#define INA_QR_U 1     // fused quantise + reduce, W <= 8: C2 91.8 -> 86.7 us (ew_lab)
+#endif
 // the other chunk_loop<4> streaming kernels
 static std::atomic<int> g_stream_blocks{8192};
 // PS combine kernels (W+2 streams), measured per kernel (bench_extra grid sweeps, two
@@ -284,7 +294,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize_i32(const float* __restrict
     size_t n4 = vec ? n / 4 : 0;
     const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
     u32x4* q4 = reinterpret_cast<u32x4*>(q);
-    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+    chunk_loop<kEwU>(n4, [&]<int UU>(size_t i, size_t st) {
         f32x4 v[UU];
 #pragma unroll
         for (int u = 0; u < UU; ++u) v[u] = __builtin_nontemporal_load(x4 + i + u * st);
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_i32(const int32_t* __rest
     size_t n4 = vec ? n / 4 : 0;
     const u32x4* s4 = reinterpret_cast<const u32x4*>(sv);
     f32x4* y4 = reinterpret_cast<f32x4*>(y);
-    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+    chunk_loop<kEwU>(n4, [&]<int UU>(size_t i, size_t st) {
         u32x4 v[UU];
 #pragma unroll
         for (int u = 0; u < UU; ++u) v[u] = __builtin_nontemporal_load(s4 + i + u * st);
@@ -393,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i32(PtrPack<float> in, 
     size_t n4 = vec ? n / 4 : 0;
     u32x4* o4 = reinterpret_cast<u32x4*>(out);
     if constexpr (W > 0) {
-        chunk_loop<(W <= 8 ? 4 : 2)>(n4, [&]<int UU>(size_t i, size_t st) {
+        chunk_loop<(W <= 8 ? INA_QR_U : 2)>(n4, [&]<int UU>(size_t i, size_t st) {
             f32x4 v[W][UU];
 #pragma unroll
             for (int w = 0; w < W; ++w)
@@ -603,7 +613,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_apply_i32(const float* __restrict
                                                          float inv, float ws,
                                                          float* __restrict__ out, size_t n, int vec) {
     size_t n4 = vec ? n / 4 : 0;
-    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+    chunk_loop<kEwU>(n4, [&]<int UU>(size_t i, size_t st) {
         f32x4 l[UU];
         u32x4 q[UU];
 #pragma unroll
@@ -1254,7 +1264,7 @@ int ina_quantize_f32_i32(const float* x, int32_t* q, size_t n, int k, ina_stream
     if (n == 0) return INA_OK;
     if (!x || !q) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(x) && aligned16(q);
-    hipLaunchKernelGGL(k_quantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_quantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)), dim3(kBlock), 0,
                        hs(stream), x, q, n, ldexpf(1.0f, k), vec);
     return check_launch("quantize_i32");
 }
@@ -1285,7 +1295,7 @@ int ina_dequantize_i32_f32(const int32_t* sv, float* y, size_t n, int k, ina_str
     if (n == 0) return INA_OK;
     if (!sv || !y) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(sv) && aligned16(y);
-    hipLaunchKernelGGL(k_dequantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_dequantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)), dim3(kBlock), 0,
                        hs(stream), sv, y, n, ldexpf(1.0f, -k), vec);
     return check_launch("dequantize_i32");
 }
@@ -1331,7 +1341,7 @@ int ina_quantize_reduce_f32_i32(const float* const* bufs, int W, int32_t* out, s
     if (!out) return set_error(INA_EINVAL, "null out%s", "");
     int vec = al && aligned16(out);
     float sc = ldexpf(1.0f, k);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, W <= 8 ? INA_QR_U : 2, g_stream_blocks);
     hipStream_t s = hs(stream);
     switch (W) {
         case 2: hipLaunchKernelGGL(k_quant_reduce_i32<2>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec); break;
@@ -1398,7 +1408,7 @@ int ina_ps_apply_i32(const float* local, const int32_t* sum_int, int k, double w
     if (n == 0) return INA_OK;
     if (!local || !sum_int || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(local) && aligned16(sum_int) && aligned16(out);
-    hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, g_stream_blocks)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)), dim3(kBlock), 0,
                        hs(stream), local, sum_int, ldexpf(1.0f, -k), (float)weight_step, out, n, vec);
     return check_launch("ps_apply_i32");
 }
