@@ -54,7 +54,7 @@ def _row(name, secs, nbytes, **kw):
 
 
 DEFAULTS = {"max_blocks": 8192, "reduce_blocks": 0, "stream_blocks": 8192, "combine_blocks": 256,
-            "combine_ina_blocks": 512}
+            "combine_ina_blocks": 8192}
 
 
 def _sweep(ops, rows, sweeps, name, knob, values, fn, nbytes):
@@ -133,7 +133,7 @@ def run_extra(dev):
     _sweep(ops, rows, gsweep, "ps_combine_f32 W=4", "combine_blocks", (256, 512, 1024, 2048),
            lambda: ops.ps_combine(local, b2[:4], 0.2, out=oc), (4 + 2) * 4 * n2)
     from ina_amd import ps as ps_mod
-    _sweep(ops, rows, gsweep, "ps_combine_ina_f32 W=4", "combine_ina_blocks", (256, 512, 1024, 2048),
+    _sweep(ops, rows, gsweep, "ps_combine_ina_f32 W=4", "combine_ina_blocks", (256, 512, 2048, 8192),
            lambda: ps_mod.combine_ina(local, b2[:4], 16, 0.2, out=oc), (4 + 2) * 4 * n2)
     del b4, b2, local, oc, o4
 

@@ -67,16 +67,24 @@ static std::atomic<int> g_unroll{4};
 #define INA_EW_U 1
 #endif
 constexpr int kEwU = INA_EW_U;
+// PS combine kernels, W <= 4 (tools/lab/ew_lab.py, C2 size): one chunk in flight --
+// fp32 combine 94.3 -> 91.9 us at 256 workgroups, INA combine 106.4 -> 93.2 us at 8192
+#ifndef INA_COMB_U
+#define INA_COMB_U 1
+#endif
+#ifndef INA_COMBI_U
+#define INA_COMBI_U 1
+#endif
 #ifndef INA_QR_U
 #define INA_QR_U 1     // fused quantise + reduce, W <= 8: C2 91.8 -> 86.7 us (ew_lab)
 #endif
 // the other chunk_loop<4> streaming kernels
 static std::atomic<int> g_stream_blocks{8192};
-// PS combine kernels (W+2 streams), measured per kernel (bench_extra grid sweeps, two
-// sessions): the fp32 combine runs best at 256 workgroups (6.6-6.7 TB/s vs 6.0 at 512),
-// the INA combine (quantiser in the loop, more VGPRs) at 512 (256 drops it to 4.3 TB/s)
+// PS combine kernels (W+2 streams), measured per kernel (bench_extra grid sweeps and
+// ew_lab): the fp32 combine runs best at 256 workgroups (6.6-6.7 TB/s vs 6.0 at 512),
+// the INA combine (quantiser in the loop) with one chunk in flight at 8192
 static std::atomic<int> g_combine_blocks{256};
-static std::atomic<int> g_combine_ina_blocks{512};
+static std::atomic<int> g_combine_ina_blocks{8192};
 static std::atomic<int> g_nontemporal{1};
 // flat packet kernels index 16-byte chunks in 32 bits: a launch covers at most this many
 // chunks and longer batches go in packet ranges (tunable so tests reach the split path)
@@ -573,7 +581,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_combine_f32(const float* __restri
     size_t n4 = vec ? n / 4 : 0;
     const f32x4* l4 = reinterpret_cast<const f32x4*>(local);
     f32x4* o4 = reinterpret_cast<f32x4*>(out);
-    chunk_loop<(W > 0 && W <= 4) ? 4 : 2>(n4, [&]<int UU>(size_t i, size_t st) {
+    chunk_loop<(W > 0 && W <= 4) ? INA_COMB_U : 2>(n4, [&]<int UU>(size_t i, size_t st) {
         f32x4 l[UU], acc[UU];
 #pragma unroll
         for (int u = 0; u < UU; ++u) { l[u] = l4[i + u * st]; acc[u] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -647,7 +655,7 @@ __global__ __launch_bounds__(kBlock) void k_ps_combine_ina(const float* __restri
                                                            int vec) {
     const int nw = W > 0 ? W : Wd;
     size_t n4 = vec ? n / 4 : 0;
-    chunk_loop<(W > 0 && W <= 4) ? 4 : 2>(n4, [&]<int UU>(size_t i, size_t st) {
+    chunk_loop<(W > 0 && W <= 4) ? INA_COMBI_U : 2>(n4, [&]<int UU>(size_t i, size_t st) {
         f32x4 l[UU];
         u32x4 acc[UU];
 #pragma unroll
@@ -1390,7 +1398,7 @@ int ina_ps_combine_f32(const float* local, const float* const* paras, int W, dou
     if (int rc = fill_pack(pk, paras, W, al)) return rc;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = al && aligned16(local) && aligned16(out);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_combine_blocks);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, W <= 4 ? INA_COMB_U : 2, g_combine_blocks);
     hipStream_t s = hs(stream);
     float ws = (float)weight_step;
     switch (W) {
@@ -1422,7 +1430,7 @@ int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W,
     if (int rc = fill_pack(pk, paras, W, al)) return rc;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = al && aligned16(local) && aligned16(out);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, 4, g_combine_ina_blocks);
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, W <= 4 ? INA_COMBI_U : 2, g_combine_ina_blocks);
     hipStream_t s = hs(stream);
     float sc = ldexpf(1.0f, k), inv = ldexpf(1.0f, -k), ws = (float)weight_step;
     switch (W) {
