@@ -132,14 +132,24 @@ __device__ __forceinline__ int32_t q32(float x, float s) {
 }
 
 // returns the int16 value widened to int32; *sat |= clamped-or-NaN
+#ifndef INA_Q16_MED3
+#define INA_Q16_MED3 1
+#endif
 __device__ __forceinline__ int32_t q16(float x, float s, bool& sat) {
     float y = __builtin_rintf(x * s);
+#if INA_Q16_MED3
+    // one v_med3_f32 clamps; a clamped value, +-inf or NaN differs from y
+    const float c = __builtin_amdgcn_fmed3f(y, -32768.0f, 32767.0f);
+    sat |= !(c == y);
+    return (y != y) ? 0 : (int32_t)c;
+#else
     bool in = (y <= 32767.0f) && (y >= -32768.0f);  // false for NaN
     sat |= !in;
     int32_t r = in ? (int32_t)y : 0;
     r = (y > 32767.0f) ? 32767 : r;
     r = (y < -32768.0f) ? -32768 : r;
     return r;
+#endif
 }
 
 __device__ __forceinline__ int32_t sat16(int32_t a, bool& sat) {

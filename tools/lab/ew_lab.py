@@ -23,6 +23,8 @@ n2 = 25_557_032                                   # config 2: ResNet-50 fp32, W 
 b4 = [torch.randn(n2, device=dev, generator=g) * 1e-2 for _ in range(4)]
 arr4 = (C.c_void_p * 4)(*[b.data_ptr() for b in b4])
 loc2 = torch.randn(n2, device=dev, generator=g)
+b16 = b4 + [torch.randn(n2, device=dev, generator=g) * 1e-2 for _ in range(12)]
+arr16 = (C.c_void_p * 16)(*[b.data_ptr() for b in b16])
 st = torch.cuda.current_stream().cuda_stream
 
 
@@ -31,7 +33,8 @@ class Variant:
         self.name = os.path.basename(path)
         self.lib = C.CDLL(path)
         for nm in ("ina_quantize_f32_i32", "ina_dequantize_i32_f32", "ina_ps_apply_i32",
-                   "ina_quantize_reduce_f32_i32", "ina_ps_combine_f32", "ina_ps_combine_ina_f32"):
+                   "ina_quantize_reduce_f32_i32", "ina_ps_combine_f32", "ina_ps_combine_ina_f32",
+                   "ina_quantize_reduce_f32_i16_sat"):
             getattr(self.lib, nm).argtypes = _lib.SIGNATURES[nm]
         self.oq = torch.empty(n, dtype=torch.int32, device=dev)
         self.of = torch.empty(n, device=dev)
@@ -39,8 +42,10 @@ class Variant:
         self.oqr = torch.empty(n2, dtype=torch.int32, device=dev)
         self.oc = torch.empty(n2, device=dev)
         self.oci = torch.empty(n2, device=dev)
+        self.o16 = torch.empty(n2, dtype=torch.int16, device=dev)
+        self.f16 = torch.empty((n2 + 255) // 256, dtype=torch.uint8, device=dev)
         self.t = {"quantize": [], "dequantize": [], "ps_apply": [], "qreduce_C2": [], "combine": [],
-                  "combine_ina": []}
+                  "combine_ina": [], "qreduce_C4": []}
         for key, env in ((5, "COMBINE_BLOCKS"), (6, "COMBINE_INA_BLOCKS")):
             if os.environ.get(env):
                 self.lib.ina_set_tuning(key, int(os.environ[env]))
@@ -60,6 +65,10 @@ class Variant:
     def combine_ina(self):
         return self.lib.ina_ps_combine_ina_f32(loc2.data_ptr(), arr4, 4, 16, 0.2, self.oci.data_ptr(), n2, st)
 
+    def qreduce_C4(self):
+        return self.lib.ina_quantize_reduce_f32_i16_sat(arr16, 16, self.o16.data_ptr(), n2, 13, 256,
+                                                        self.f16.data_ptr(), st)
+
     def ps_apply(self):
         return self.lib.ina_ps_apply_i32(local.data_ptr(), q.data_ptr(), 16, 0.1, self.oa.data_ptr(), n, st)
 
@@ -67,12 +76,13 @@ class Variant:
 vs = [Variant(p) for p in sys.argv[1:]]
 for v in vs:
     assert v.quantize() == 0 and v.dequantize() == 0 and v.ps_apply() == 0 and v.qreduce_C2() == 0
-    assert v.combine() == 0 and v.combine_ina() == 0
+    assert v.combine() == 0 and v.combine_ina() == 0 and v.qreduce_C4() == 0
 torch.cuda.synchronize()
 for v in vs[1:]:
     assert torch.equal(v.oq, vs[0].oq) and torch.equal(v.of, vs[0].of) and torch.equal(v.oa, vs[0].oa), v.name
     assert torch.equal(v.oqr, vs[0].oqr), v.name
     assert torch.equal(v.oc, vs[0].oc) and torch.equal(v.oci, vs[0].oci), v.name
+    assert torch.equal(v.o16, vs[0].o16) and torch.equal(v.f16, vs[0].f16), v.name
 for r in range(int(os.environ.get("ROUNDS", 6))):
     for v in vs:
         for op in v.t:
