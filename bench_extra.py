@@ -53,7 +53,7 @@ def _row(name, secs, nbytes, **kw):
     return r
 
 
-DEFAULTS = {"max_blocks": 8192, "reduce_blocks": 0, "stream_blocks": 8192, "combine_blocks": 256,
+DEFAULTS = {"max_blocks": 16384, "reduce_blocks": 0, "stream_blocks": 8192, "combine_blocks": 256,
             "combine_ina_blocks": 8192}
 
 
@@ -124,7 +124,7 @@ def run_extra(dev):
     o4 = torch.empty(n2, dtype=torch.int16, device=dev)
     f4 = torch.empty((n2 + 255) // 256, dtype=torch.uint8, device=dev)
     _sweep(ops, rows, gsweep, "quantize_reduce_f32_i16 W=16 V=256 (C4)", "max_blocks",
-           (2048, 8192, 16384),
+           (2048, 8192, 16384, 32768),
            lambda: ops.quantize_reduce_i16(b4, 13, 256, out=o4, overflow=f4),
            (16 * 4 + 2) * n2 + f4.numel())
     # --- PS combine (launch.py:42-52), W=4 ---------------------------------------------------
