@@ -49,8 +49,9 @@ def parse():
     ap.add_argument("--workers", type=int, default=W_WORKERS)
     ap.add_argument("--values", type=int, default=N_VALUES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 22,
-                    help="values per worker in the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=N_VALUES,
+                    help="values per worker in the CPU-baseline sample (default: the whole "
+                         "config-3 bucket, ~2-4 s of host work)")
     ap.add_argument("--extra", action="store_true")
     ap.add_argument("--mode", choices=("reduce", "sharded"), default="reduce",
                     help="reduce: the headline (config 3); sharded: config 5, one 1 GiB fp32 "
@@ -124,7 +125,7 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
     for P in sorted({1, threads}):
         ts = []
         out = None
-        for _ in range(3):
+        for _ in range(5):
             out, secs = orc.cpu_packetise_aggregate(bufs_host, V_SLOT, P)
             ts.append(secs)
         res[P] = (statistics.median(ts), out)
@@ -144,13 +145,14 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
         local += (1.0 / (W + 1)) * 1.0 * sum([p - local for p in paras])
         ta.append(time.perf_counter() - t0)
     t_agg = statistics.median(ta)
+    part = "the whole" if n == N_VALUES else f"first {n * 4 // (1 << 20)} MiB of each"
     return {
         "value": round(W * n * 4 / tP / 1e9, 3), "unit": "GB/s", "cores": threads,
         "kind": "port",
-        "sample": (f"{W} workers x {n} int32 (first {n * 4 // (1 << 20)} MiB of each config-3 "
+        "sample": (f"{W} workers x {n} int32 ({part} config-3 "
                    f"bucket): NGA-{V_SLOT} packetise (header + memcpy + htonl per packet, "
                    f"communicator.cc:23-37) -> P4 aggregator restatement (count/frag/Processor "
-                   f"registers, ngaa.p4:120-196) -> PS ack, median of 3, {threads} threads split "
+                   f"registers, ngaa.p4:120-196) -> PS ack, median of 5, {threads} threads split "
                    f"as communicator.py:133-157"),
         "value_1core": round(W * n * 4 / t1 / 1e9, 3),
         "torch_aggregate_GBps": round(W * n * 4 / t_agg / 1e9, 3),
