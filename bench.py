@@ -125,9 +125,10 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
     for P in sorted({1, threads}):
         ts = []
         out = None
-        for _ in range(5):
+        for it in range(13):             # 3 warm-up runs, median of 10
             out, secs = orc.cpu_packetise_aggregate(bufs_host, V_SLOT, P)
-            ts.append(secs)
+            if it >= 3:
+                ts.append(secs)
         res[P] = (statistics.median(ts), out)
     tP, outP = res[threads]
     t1, _ = res[1]
@@ -152,7 +153,7 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
         "sample": (f"{W} workers x {n} int32 ({part} config-3 "
                    f"bucket): NGA-{V_SLOT} packetise (header + memcpy + htonl per packet, "
                    f"communicator.cc:23-37) -> P4 aggregator restatement (count/frag/Processor "
-                   f"registers, ngaa.p4:120-196) -> PS ack, median of 5, {threads} threads split "
+                   f"registers, ngaa.p4:120-196) -> PS ack, 3 warm-up runs then median of 10, {threads} threads split "
                    f"as communicator.py:133-157"),
         "value_1core": round(W * n * 4 / t1 / 1e9, 3),
         "torch_aggregate_GBps": round(W * n * 4 / t_agg / 1e9, 3),

@@ -110,3 +110,59 @@ def test_scale_for_edges():
         ops.scale_for(1.0, 8, bits=8)
     with pytest.raises(_lib.InaError):
         ops.scale_for(1.0, 70000, bits=16)      # W/2 alone exceeds 32767
+
+
+def _einval_cases():
+    from ina_amd import _lib
+    P = _lib.ptr_array
+    prm = _lib.NgaParams(1, 2, 0, 1, 0, 1, 16384, 32)
+    st = _lib.SwitchState(16384, 32, 1, 0, None, None, None)
+    return {
+        "ina_quantize_f32_i32": (None, None, 64, 16, None),
+        "ina_quantize_f32_i16_sat": (None, None, 64, 8, 32, None, None),
+        "ina_dequantize_i32_f32": (None, None, 64, 16, None),
+        "ina_dequantize_i16_f32": (None, None, 64, 16, None),
+        "ina_sum_reduce_i32": (P([None, None]), 2, None, 64, None),
+        "ina_sum_reduce_i16_sat": (P([None, None]), 2, None, 64, 32, None, None),
+        "ina_quantize_reduce_f32_i32": (P([None, None]), 2, None, 64, 16, None),
+        "ina_quantize_reduce_f32_i16_sat": (P([None, None]), 2, None, 64, 8, 32, None, None),
+        "ina_ps_combine_f32": (None, P([None, None]), 2, 0.5, None, 64, None),
+        "ina_ps_apply_i32": (None, None, 16, 0.5, None, 64, None),
+        "ina_ps_combine_ina_f32": (None, P([None, None]), 2, 16, 0.5, None, 64, None),
+        "ina_pack_nga": (None, 64, ctypes.byref(prm), None, None, 144, None),
+        "ina_quantize_pack_nga": (None, None, 64, 16, ctypes.byref(prm), None, 144, None),
+        "ina_unpack_nga": (None, 2, 32, 144, None, None, None),
+        "ina_pack_c128": (None, 2, 1, 0, 0, None, None),
+        "ina_apply_completed_nga": (None, 2, 32, 144, None, 1, None, 16, 0.5, None, 64, None, 144,
+                                    None),
+        "ina_switch_process": (ctypes.byref(st), None, 2, 144, None, None, None),
+        "ina_route_ipv4": (None, None, 0, 4, None, None, 1, None, None),
+        "ina_checksum_i32": (None, 64, None, None),
+        "ina_absmax_f32": (None, None, 64, None, None),
+        "ina_sum_reduce_host_i32": (P([None, None]), 2, None, 64, 0, None, None),
+    }
+
+
+def test_every_device_entry_point_rejects_null_buffers():
+    """Null buffers with n > 0 come back as INA_EINVAL with a message, before any HIP
+    call (the reference's send_gradients would exit(-1), communicator.cc:11-12)."""
+    from ina_amd import _lib
+    lib = _lib.load()
+    cases = _einval_cases()
+    device_fns = {n for n in _lib.SIGNATURES if n.startswith("ina_")} - {
+        "ina_version", "ina_last_error_string", "ina_set_tuning", "ina_switch_scratch_bytes",
+        "ina_host_reduce_scratch_bytes", "ina_scale_for", "ina_send_gradients_fd",
+        "ina_send_packets_fd", "ina_recv_packets_fd"}
+    assert device_fns == set(cases)
+    for name, args in cases.items():
+        rc = getattr(lib, name)(*args)
+        assert rc == _lib.INA_EINVAL, (name, rc, lib.ina_last_error_string())
+        assert lib.ina_last_error_string(), name
+
+
+def test_socket_entry_points_reject_bad_descriptors():
+    from ina_amd import _lib
+    lib = _lib.load()
+    assert lib.ina_send_packets_fd(-1, None, 2, 144, 144, 0) < 0
+    assert lib.ina_recv_packets_fd(-1, None, 2, 144, 0, 0, None) < 0
+    assert lib.ina_send_gradients_fd(-1, None, 1, 0, 1, 0, 0) < 0
