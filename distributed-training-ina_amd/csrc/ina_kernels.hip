@@ -28,6 +28,7 @@
 namespace ina {
 
 using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+using u32x2 = uint32_t __attribute__((ext_vector_type(2)));
 using f32x4 = float __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
@@ -135,6 +136,12 @@ __device__ __forceinline__ int32_t q32(float x, float s) {
 #ifndef INA_Q16_MED3
 #define INA_Q16_MED3 1
 #endif
+// int16 kernels: a wave covers 512 values as two 256-value halves (16 B per lane per
+// load, contiguous per instruction) -- C4 fused quantise+reduce 289 -> 251 us against
+// 8 consecutive values per lane (32-B lane stride; tools/lab/ew_lab.py, lab/q16_lab.log)
+#ifndef INA_Q16_SPLIT
+#define INA_Q16_SPLIT 1
+#endif
 __device__ __forceinline__ int32_t q16(float x, float s, bool& sat) {
     float y = __builtin_rintf(x * s);
 #if INA_Q16_MED3
@@ -171,6 +178,19 @@ __device__ __forceinline__ void write_slot_flags8(unsigned long long m, bool act
     int g0 = lane & ~(lanes_per_slot - 1);
     unsigned long long gm = (lanes_per_slot == 64) ? ~0ull : (((1ull << lanes_per_slot) - 1ull) << g0);
     if (active && (lane & (lanes_per_slot - 1)) == 0) ovf[elem0 / (size_t)V] = (m & gm) ? 1 : 0;
+}
+
+// the same for the split layout (a wave owns 512 values, lane l holds 4 at 4l of each
+// 256-value half): a slot is V/4 adjacent lanes of one half, or both halves at V = 512
+__device__ __forceinline__ void write_slot_flags_split(unsigned long long ma, unsigned long long mb,
+                                                       size_t eA, size_t eB, size_t n, int V,
+                                                       uint8_t* __restrict__ ovf) {
+    if (V >= 512) {
+        write_slot_flags8(ma | mb, eA < n, eA, V, 64, ovf);
+    } else {
+        write_slot_flags8(ma, eA < n, eA, V, V / 4, ovf);
+        write_slot_flags8(mb, eB < n, eB, V, V / 4, ovf);
+    }
 }
 
 static inline bool slot_ballot_ok(int V) {
@@ -336,6 +356,32 @@ __global__ __launch_bounds__(kBlock) void k_quantize_i16_vec(const float* __rest
                                                              uint8_t* __restrict__ ovf) {
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * kBlock;
+#if INA_Q16_SPLIT
+    // a wave owns 512 consecutive values, lane l the 4 at 4l of each 256-value half (one
+    // contiguous KiB per load instruction); see k_quant_reduce_i16
+    const int lane = (int)(tid & 63);
+    const size_t nreg = (n + 511) / 512;
+    for (size_t r = tid >> 6; r < nreg; r += stride >> 6) {
+        const size_t eA = r * 512 + 4 * (size_t)lane, eB = eA + 256;
+        bool sa = false, sb = false;
+        if (r * 512 + 512 <= n) {                 // wave-uniform
+            f32x4 u = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + eA));
+            f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + eB));
+            u32x2 oa, ob;
+            oa.x = (uint32_t)(uint16_t)q16(u.x, s, sa) | ((uint32_t)q16(u.y, s, sa) << 16);
+            oa.y = (uint32_t)(uint16_t)q16(u.z, s, sa) | ((uint32_t)q16(u.w, s, sa) << 16);
+            ob.x = (uint32_t)(uint16_t)q16(v.x, s, sb) | ((uint32_t)q16(v.y, s, sb) << 16);
+            ob.y = (uint32_t)(uint16_t)q16(v.z, s, sb) | ((uint32_t)q16(v.w, s, sb) << 16);
+            __builtin_nontemporal_store(oa, reinterpret_cast<u32x2*>(q + eA));
+            __builtin_nontemporal_store(ob, reinterpret_cast<u32x2*>(q + eB));
+        } else {
+            for (size_t j = eA; j < eA + 4 && j < n; ++j) q[j] = (int16_t)q16(x[j], s, sa);
+            for (size_t j = eB; j < eB + 4 && j < n; ++j) q[j] = (int16_t)q16(x[j], s, sb);
+        }
+        const unsigned long long ma = __ballot(sa), mb = __ballot(sb);   // wave-convergent
+        if (ovf) write_slot_flags_split(ma, mb, eA, eB, n, V, ovf);
+    }
+#else
     const size_t n8 = (n + 7) / 8;
     // uniform trip count per wave so every lane reaches the ballot together
     const size_t wave0 = tid & ~(size_t)63;
@@ -363,6 +409,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize_i16_vec(const float* __rest
         unsigned long long m = __ballot(sat);   // wave-convergent: uniform trip count
         if (ovf) write_slot_flags8(m, i < n8, 8 * i, V, lanes_per_slot, ovf);
     }
+#endif
 }
 
 // generic int16 path (unaligned or V without a ballot layout): byte flags via a
@@ -470,6 +517,49 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i16(PtrPack<float> in, 
     const size_t stride = (size_t)gridDim.x * kBlock;
     const int nw = W > 0 ? W : Wd;
     constexpr int UNR = W > 0 ? W : 1;
+#if INA_Q16_SPLIT
+    // a wave owns 512 consecutive values: lane l holds 4l..4l+3 of each 256-value half, so
+    // every load instruction of the wave reads 1 KiB contiguous (16 B per lane, no 32-B
+    // lane stride); the two halves' saturation ballots give the slot flags
+    const int lane = (int)(tid & 63);
+    const size_t nreg = (n + 511) / 512;
+    for (size_t r = tid >> 6; r < nreg; r += stride >> 6) {
+        const size_t eA = r * 512 + 4 * (size_t)lane, eB = eA + 256;
+        bool sa = false, sb = false;
+        if (r * 512 + 512 <= n) {                 // wave-uniform
+            int32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll UNR
+            for (int w = 0; w < nw; ++w) {
+                f32x4 u = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w] + eA));
+                f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in.p[w] + eB));
+                a[0] += q16(u.x, s, sa); a[1] += q16(u.y, s, sa);
+                a[2] += q16(u.z, s, sa); a[3] += q16(u.w, s, sa);
+                a[4] += q16(v.x, s, sb); a[5] += q16(v.y, s, sb);
+                a[6] += q16(v.z, s, sb); a[7] += q16(v.w, s, sb);
+            }
+            u32x2 oa, ob;
+            oa.x = (uint32_t)(uint16_t)sat16(a[0], sa) | ((uint32_t)sat16(a[1], sa) << 16);
+            oa.y = (uint32_t)(uint16_t)sat16(a[2], sa) | ((uint32_t)sat16(a[3], sa) << 16);
+            ob.x = (uint32_t)(uint16_t)sat16(a[4], sb) | ((uint32_t)sat16(a[5], sb) << 16);
+            ob.y = (uint32_t)(uint16_t)sat16(a[6], sb) | ((uint32_t)sat16(a[7], sb) << 16);
+            __builtin_nontemporal_store(oa, reinterpret_cast<u32x2*>(out + eA));
+            __builtin_nontemporal_store(ob, reinterpret_cast<u32x2*>(out + eB));
+        } else {
+            for (size_t j = eA; j < eA + 4 && j < n; ++j) {
+                int32_t a = 0;
+                for (int w = 0; w < nw; ++w) a += q16(in.p[w][j], s, sa);
+                out[j] = (int16_t)sat16(a, sa);
+            }
+            for (size_t j = eB; j < eB + 4 && j < n; ++j) {
+                int32_t a = 0;
+                for (int w = 0; w < nw; ++w) a += q16(in.p[w][j], s, sb);
+                out[j] = (int16_t)sat16(a, sb);
+            }
+        }
+        const unsigned long long ma = __ballot(sa), mb = __ballot(sb);   // wave-convergent
+        if (ovf) write_slot_flags_split(ma, mb, eA, eB, n, V, ovf);
+    }
+#else
     const size_t n8 = (n + 7) / 8;
     const size_t wave0 = tid & ~(size_t)63;
     for (size_t base = wave0; base < n8; base += stride) {
@@ -505,6 +595,7 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i16(PtrPack<float> in, 
         unsigned long long m = __ballot(sat);   // wave-convergent: uniform trip count
         if (ovf) write_slot_flags8(m, i < n8, 8 * i, V, lanes_per_slot, ovf);
     }
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void k_quant_reduce_i16_scalar(PtrPack<float> in, int W,

@@ -26,6 +26,8 @@ loc2 = torch.randn(n2, device=dev, generator=g)
 b16 = b4 + [torch.randn(n2, device=dev, generator=g) * 1e-2 for _ in range(12)]
 arr16 = (C.c_void_p * 16)(*[b.data_ptr() for b in b16])
 st = torch.cuda.current_stream().cuda_stream
+K16 = int(os.environ.get("K16", 13))       # C4 scale; 20 saturates often (flag check)
+ONLY = os.environ.get("ONLY", "").split(",") if os.environ.get("ONLY") else None
 
 
 class Variant:
@@ -34,7 +36,7 @@ class Variant:
         self.lib = C.CDLL(path)
         for nm in ("ina_quantize_f32_i32", "ina_dequantize_i32_f32", "ina_ps_apply_i32",
                    "ina_quantize_reduce_f32_i32", "ina_ps_combine_f32", "ina_ps_combine_ina_f32",
-                   "ina_quantize_reduce_f32_i16_sat"):
+                   "ina_quantize_reduce_f32_i16_sat", "ina_quantize_f32_i16_sat"):
             getattr(self.lib, nm).argtypes = _lib.SIGNATURES[nm]
         self.oq = torch.empty(n, dtype=torch.int32, device=dev)
         self.of = torch.empty(n, device=dev)
@@ -44,8 +46,10 @@ class Variant:
         self.oci = torch.empty(n2, device=dev)
         self.o16 = torch.empty(n2, dtype=torch.int16, device=dev)
         self.f16 = torch.empty((n2 + 255) // 256, dtype=torch.uint8, device=dev)
+        self.q16 = torch.empty(n, dtype=torch.int16, device=dev)
+        self.fq16 = torch.empty((n + 255) // 256, dtype=torch.uint8, device=dev)
         self.t = {"quantize": [], "dequantize": [], "ps_apply": [], "qreduce_C2": [], "combine": [],
-                  "combine_ina": [], "qreduce_C4": []}
+                  "combine_ina": [], "qreduce_C4": [], "quantize16": []}
         for key, env in ((5, "COMBINE_BLOCKS"), (6, "COMBINE_INA_BLOCKS")):
             if os.environ.get(env):
                 self.lib.ina_set_tuning(key, int(os.environ[env]))
@@ -66,8 +70,12 @@ class Variant:
         return self.lib.ina_ps_combine_ina_f32(loc2.data_ptr(), arr4, 4, 16, 0.2, self.oci.data_ptr(), n2, st)
 
     def qreduce_C4(self):
-        return self.lib.ina_quantize_reduce_f32_i16_sat(arr16, 16, self.o16.data_ptr(), n2, 13, 256,
+        return self.lib.ina_quantize_reduce_f32_i16_sat(arr16, 16, self.o16.data_ptr(), n2, K16, 256,
                                                         self.f16.data_ptr(), st)
+
+    def quantize16(self):
+        return self.lib.ina_quantize_f32_i16_sat(x.data_ptr(), self.q16.data_ptr(), n, K16 + 2, 256,
+                                                 self.fq16.data_ptr(), st)
 
     def ps_apply(self):
         return self.lib.ina_ps_apply_i32(local.data_ptr(), q.data_ptr(), 16, 0.1, self.oa.data_ptr(), n, st)
@@ -76,16 +84,19 @@ class Variant:
 vs = [Variant(p) for p in sys.argv[1:]]
 for v in vs:
     assert v.quantize() == 0 and v.dequantize() == 0 and v.ps_apply() == 0 and v.qreduce_C2() == 0
-    assert v.combine() == 0 and v.combine_ina() == 0 and v.qreduce_C4() == 0
+    assert v.combine() == 0 and v.combine_ina() == 0 and v.qreduce_C4() == 0 and v.quantize16() == 0
 torch.cuda.synchronize()
 for v in vs[1:]:
     assert torch.equal(v.oq, vs[0].oq) and torch.equal(v.of, vs[0].of) and torch.equal(v.oa, vs[0].oa), v.name
     assert torch.equal(v.oqr, vs[0].oqr), v.name
     assert torch.equal(v.oc, vs[0].oc) and torch.equal(v.oci, vs[0].oci), v.name
     assert torch.equal(v.o16, vs[0].o16) and torch.equal(v.f16, vs[0].f16), v.name
+    assert torch.equal(v.q16, vs[0].q16) and torch.equal(v.fq16, vs[0].fq16), v.name
 for r in range(int(os.environ.get("ROUNDS", 6))):
     for v in vs:
         for op in v.t:
+            if ONLY and op not in ONLY:
+                continue
             evs = []
             for _ in range(4):
                 ops.checksum(flush)
@@ -97,4 +108,6 @@ for r in range(int(os.environ.get("ROUNDS", 6))):
             torch.cuda.synchronize()
             v.t[op] += [a.elapsed_time(b) * 1e3 for a, b in evs[1:]]
 for v in vs:
-    print(f"{v.name:16s} " + "  ".join(f"{op} {statistics.median(v.t[op]):6.1f} us" for op in v.t))
+    print(f"{v.name:16s} " + "  ".join(f"{op} {statistics.median(v.t[op]):6.1f} us" for op in v.t if v.t[op]))
+print("C4 slots flagged:", int(vs[0].f16.sum()), "of", vs[0].f16.numel(),
+      "| quantize16 slots flagged:", int(vs[0].fq16.sum()), "of", vs[0].fq16.numel())
