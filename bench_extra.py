@@ -127,6 +127,15 @@ def run_extra(dev):
            (2048, 8192, 16384, 32768),
            lambda: ops.quantize_reduce_i16(b4, 13, 256, out=o4, overflow=f4),
            (16 * 4 + 2) * n2 + f4.numel())
+    # the C4 worker's own quantiser and the PS's dequantise of the int16 aggregate
+    q4 = torch.empty(n2, dtype=torch.int16, device=dev)
+    rows.append(_row("quantize_f32_i16_sat V=256 (C4 worker)",
+                     _time(lambda: ops.quantize_i16(b4[0], 13, 256, out=q4, overflow=f4)),
+                     6 * n2 + f4.numel()))
+    y4 = torch.empty(n2, dtype=torch.float32, device=dev)
+    rows.append(_row("dequantize_i16_f32 (C4 aggregate)", _time(lambda: ops.dequantize(o4, 13, out=y4)),
+                     6 * n2))
+    del q4, y4
     # --- PS combine (launch.py:42-52), W=4 ---------------------------------------------------
     local = rnd_f32(n2, 1.0)
     oc = torch.empty_like(local)

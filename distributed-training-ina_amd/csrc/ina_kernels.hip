@@ -449,11 +449,28 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_i32(const int32_t* __rest
         y[i] = (float)sv[i] * inv;
 }
 
+// int16 -> fp32: lane holds 4 values (8-byte load, 16-byte store), so each instruction of
+// a wave reads 512 B and writes 1 KiB contiguous; vec = 0 for unaligned buffers
 __global__ __launch_bounds__(kBlock) void k_dequantize_i16(const int16_t* __restrict__ sv,
                                                            float* __restrict__ y, size_t n,
-                                                           float inv) {
+                                                           float inv, int vec) {
+    size_t n4 = vec ? n / 4 : 0;
+    const u32x2* s4 = reinterpret_cast<const u32x2*>(sv);
+    f32x4* y4 = reinterpret_cast<f32x4*>(y);
+    chunk_loop<kEwU>(n4, [&]<int UU>(size_t i, size_t st) {
+        u32x2 v[UU];
+#pragma unroll
+        for (int u = 0; u < UU; ++u) v[u] = __builtin_nontemporal_load(s4 + i + u * st);
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            f32x4 r;
+            r.x = (float)(int16_t)(v[u].x & 0xFFFFu) * inv; r.y = (float)((int32_t)v[u].x >> 16) * inv;
+            r.z = (float)(int16_t)(v[u].y & 0xFFFFu) * inv; r.w = (float)((int32_t)v[u].y >> 16) * inv;
+            __builtin_nontemporal_store(r, y4 + i + u * st);
+        }
+    });
     const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
         y[i] = (float)sv[i] * inv;
 }
 
@@ -1413,8 +1430,9 @@ int ina_dequantize_i16_f32(const int16_t* sv, float* y, size_t n, int k, ina_str
     if (int rc = check_k(k)) return rc;
     if (n == 0) return INA_OK;
     if (!sv || !y) return set_error(INA_EINVAL, "null pointer%s", "");
-    hipLaunchKernelGGL(k_dequantize_i16, dim3(grid_for(n, 1)), dim3(kBlock), 0, hs(stream), sv, y, n,
-                       ldexpf(1.0f, -k));
+    const int vec = ((uintptr_t)sv % 8 == 0) && aligned16(y);
+    hipLaunchKernelGGL(k_dequantize_i16, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)),
+                       dim3(kBlock), 0, hs(stream), sv, y, n, ldexpf(1.0f, -k), vec);
     return check_launch("dequantize_i16");
 }
 

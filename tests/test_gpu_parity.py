@@ -188,6 +188,20 @@ def test_dequantize(k):
     assert np.array_equal(got16.view(np.uint32), orc.dequantize_i16(s16, k).view(np.uint32))
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 257, 100003, 25_557_032])
+@pytest.mark.parametrize("off", [0, 1, 4])
+def test_dequantize_i16_sizes_and_alignment(n, off):
+    """Vector path (8-byte aligned int16, 16-byte aligned fp32, 4 values per lane) and the
+    scalar path for unaligned views; the remainder values after n/4 chunks."""
+    if n > 200_000 and off:
+        pytest.skip("alignment covered at small n")
+    rng = np.random.default_rng(n + off)
+    s16 = rng.integers(-32768, 32768, n + off).astype(np.int16)
+    d = dev(s16)[off:]
+    got = host(ops().dequantize(d, 13))
+    assert np.array_equal(got.view(np.uint32), orc.dequantize_i16(s16[off:], 13).view(np.uint32))
+
+
 def test_quantize_dequantize_round_trip_bound():
     x = (np.random.default_rng(3).standard_normal(1 << 20) * 1e-2).astype(np.float32)
     k = 16
