@@ -603,6 +603,29 @@ def test_switch_collision_free_equals_bulk_reduce():
     assert np.array_equal(got, host(o.sum_reduce([dev(b) for b in bufs])))
 
 
+def test_switch_config3_full_size_equals_bulk_reduce():
+    """Config 3 at full size through the packet path: 8 workers x 26,214,400 int32 ->
+    819,200 NGA-256 packets -> device switch (2^17-slot pool, multi-pass radix sort,
+    windowed run kernel) -> the 102,400 completed packets, unpacked and ordered by frag id,
+    equal the bulk W-way sum-reduce bit for bit (full-range values, so the sums wrap)."""
+    o = ops()
+    V, W, n = 256, 8, 26_214_400
+    g = torch.Generator(device=DEV).manual_seed(31)
+    bufs = [torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
+            for _ in range(W)]
+    want = o.sum_reduce(bufs)
+    stream = torch.cat([o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=1 << 17) for w, b in enumerate(bufs)])
+    del bufs
+    sw = o.Switch(V, num_slots=1 << 17, switch_id=1, device=DEV)
+    act = sw.process(stream)
+    npk = n // V
+    done = torch.nonzero(act == orc.ACT_FWD_AGG).flatten()
+    assert done.numel() == npk and bool((done >= (W - 1) * npk).all())
+    f, vals = o.unpack_nga(stream[done], V)
+    order = torch.argsort(f["frag_id"].to(torch.int64))
+    assert torch.equal(vals.view(npk, V)[order].reshape(-1), want)
+
+
 @pytest.mark.parametrize("V", [32, 256, 33, 100, 4])
 @pytest.mark.parametrize("with_base", [False, True])
 @pytest.mark.parametrize("padded", [True, False])
