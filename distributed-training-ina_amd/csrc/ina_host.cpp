@@ -122,6 +122,13 @@ int ina_sum_reduce_host_i32(const int32_t* const* host_bufs, int W, int32_t* hos
     auto out_buf = [&](int slot) { return base + ((size_t)slot * (W + 1) + (size_t)W) * c; };
     bool ok = true;
     auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
+    // on an error return, copies already enqueued still read host_bufs / write host_out:
+    // drain every stream first so the caller may free them
+    auto drain = [&]() {
+        for (int i = 0; i < P.n_h2d; ++i) (void)hipStreamSynchronize(P.h2d[i]);
+        (void)hipStreamSynchronize(P.d2h);
+        (void)hipStreamSynchronize(cs);
+    };
 
     // earlier work of the caller's stream on the scratch finishes before the first copy
     chk(hipEventRecord(P.start, cs));
@@ -143,7 +150,10 @@ int ina_sum_reduce_host_i32(const int32_t* const* host_bufs, int W, int32_t* hos
         if (k >= (size_t)kSlots) chk(hipStreamWaitEvent(cs, P.out_done[slot], 0));
         const int32_t* ptrs[INA_MAX_WORKERS];
         for (int w = 0; w < W; ++w) ptrs[w] = in_buf(slot, w);
-        if (int rc = ina_sum_reduce_i32(ptrs, W, out_buf(slot), len, stream)) return rc;
+        if (int rc = ina_sum_reduce_i32(ptrs, W, out_buf(slot), len, stream)) {
+            drain();
+            return rc;
+        }
         chk(hipEventRecord(P.red_done[slot], cs));
         // copy out
         chk(hipStreamWaitEvent(P.d2h, P.red_done[slot], 0));
@@ -151,7 +161,10 @@ int ina_sum_reduce_host_i32(const int32_t* const* host_bufs, int W, int32_t* hos
                            hipMemcpyDeviceToHost, P.d2h));
         chk(hipEventRecord(P.out_done[slot], P.d2h));
     }
-    if (!ok) return set_error(INA_EHIP, "host pipeline enqueue%s", "");
+    if (!ok) {
+        drain();
+        return set_error(INA_EHIP, "host pipeline enqueue%s", "");
+    }
     // synchronous: the aggregate is in host_out when this returns (the PS sends it next)
     if (hipStreamSynchronize(P.d2h) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess)
         return set_error(INA_EHIP, "host pipeline sync%s", "");

@@ -74,8 +74,10 @@ int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num
                        hipMemcpyHostToDevice, s) != hipSuccess)
         return ina::set_error(INA_EHIP, "H2D gradient copy%s", "");
     if (int rc = ina_pack_c128(g_stage.d_grad, packet_num, worker_id, aggregator_index,
-                               tensor_index, g_stage.d_pkts, s))
+                               tensor_index, g_stage.d_pkts, s)) {
+        (void)hipStreamSynchronize(s);   // the H2D copy still reads the caller's array
         return rc;
+    }
     if (hipMemcpyAsync(g_stage.h_pkts, g_stage.d_pkts, npk * INA_C128_BYTES, hipMemcpyDeviceToHost,
                        s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
