@@ -1060,6 +1060,10 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_flat(const uint8_t* __res
 #ifndef INA_APPLY_WIN
 #define INA_APPLY_WIN 16
 #endif
+#ifndef INA_APPLY_MW
+#define INA_APPLY_MW 1
+#endif
+static_assert(64 % INA_APPLY_WIN == 0, "windows tile the wave's 64 lanes");
 constexpr int kApB = INA_APPLY_BATCH;
 constexpr int kApWin = INA_APPLY_WIN;   // packets per window (<= 64)
 
@@ -1074,16 +1078,32 @@ __global__ __launch_bounds__(kBlock) void k_apply_completed_nga(
     const int chn = 1 + (vl ? lane : 0);
     const uint32_t wave = blockIdx.x * (kBlock / 64) + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+#if INA_APPLY_MW
+    // one action load covers this wave's next 64 / kApWin windows (lane l: window l /
+    // kApWin of the group, packet l % kApWin), so a stream whose completed packets sit in
+    // one region does not pay a round trip per empty window
+    constexpr uint32_t kG = 64 / kApWin;
+    const size_t S = (size_t)nwaves * kApWin;               // distance between a wave's windows
+    for (size_t w0 = (size_t)wave * kApWin; w0 < npk; w0 += kG * S) {
+        const size_t p = w0 + (size_t)(lane / kApWin) * S + (size_t)(lane % kApWin);
+        unsigned long long m = __ballot(p < npk && actions[p] == INA_ACT_FWD_AGG);
+#else
     for (uint32_t w0 = wave * kApWin; w0 < npk; w0 += nwaves * kApWin) {
         const uint32_t p = w0 + (uint32_t)lane;
         unsigned long long m = __ballot(lane < kApWin && p < npk && actions[p] == INA_ACT_FWD_AGG);
+#endif
         while (m) {
             uint32_t pid[kApB];
             int nb = 0;
 #pragma unroll
             for (int b = 0; b < kApB; ++b) {
                 if (m) {
-                    pid[b] = w0 + (uint32_t)__builtin_ctzll(m);
+                    const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+#if INA_APPLY_MW
+                    pid[b] = (uint32_t)(w0 + (size_t)(bit / kApWin) * S + (bit % kApWin));
+#else
+                    pid[b] = w0 + bit;
+#endif
                     m &= m - 1;
                     nb = b + 1;
                 } else {
