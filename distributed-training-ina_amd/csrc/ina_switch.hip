@@ -515,6 +515,14 @@ static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWI
 #ifndef INA_SWITCH_NT
 #define INA_SWITCH_NT 1
 #endif
+// the tail chunk (bytes 1024..1039 of an NGA-256 row) always lies in the 128-byte line
+// the packet shares with the next row; loading it with the default policy keeps that line
+// in L2 for the neighbour: run kernel HBM reads 975.7 -> 911.4 MB, switch 268 -> 265 us.
+// A default-policy touch of each packet's head chunk as well read 870 MB but ran 288 us
+// (profiles/r01/lab/switch_lab_tail.log)
+#ifndef INA_SWITCH_TAIL_NT
+#define INA_SWITCH_TAIL_NT 0
+#endif
 __device__ __forceinline__ u32x4s sw_ld(const u32x4s* p) {
 #if INA_SWITCH_NT
     return __builtin_nontemporal_load(p);
@@ -610,7 +618,11 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                 uint32_t mypid = pid[0];
 #pragma unroll
                 for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
+#if INA_SWITCH_TAIL_NT
                 tl = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
+#else
+                tl = *(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
+#endif
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
