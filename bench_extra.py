@@ -222,9 +222,16 @@ def run_extra(dev):
     ina_step()
     torch.cuda.synchronize()
     ok = bool((acts == 1).sum() == npk) and bool((ack_acts == 3).all()) and not bool(sw.frag.any())
+    row_b = stream.shape[1]
+    path_bytes = (Ws * (8 * n3 + npk * row_b)                                   # fused worker packs
+                  + stream.numel() + npk * row_b + npk * (V * 4 + 5) + npk_all  # switch
+                  + npk_all + npk * row_b + 8 * n3 + 16 * npk                   # PS apply + acks
+                  + npk * row_b + npk * 6)                                       # acks through the switch
     rows.append(_row("INA packet path step: 8 x quantise+pack -> switch -> apply -> acks (8 x 100 MiB fp32)",
-                     t, Ws * n3 * 4, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2), slots_freed=ok,
-                     note="GB/s column = worker fp32 bytes aggregated per second through the packet path"))
+                     t, path_bytes, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2), slots_freed=ok,
+                     note="bytes = the sum of the four stages' algorithmic HBM bytes (so frac is the "
+                          "path's roofline fraction); aggregated_GBps = worker fp32 bytes aggregated "
+                          "per second through the packet path"))
     del xs, glob_p, upd, acks, ack_acts, rows_w, stream
 
     # small batches through the switch (P4 format: NGA-32, 16,384-slot pool): latency of
