@@ -16,6 +16,8 @@ struct PtrPack {
 int set_error(int code, const char* fmt, const char* detail);
 int set_h2d_streams(int v);   // ina_host.cpp
 int set_small_sort(int v);    // ina_switch.hip
+int set_switch_win(int v);    // ina_switch.hip
+int set_ack_fast(int v);      // ina_switch.hip
 
 }  // namespace ina
 

@@ -1374,6 +1374,8 @@ int ina_set_tuning(int key, int value) {
         case 7: return set_h2d_streams(value);
         case 8: if (value < 1) return INA_EINVAL; g_launch_chunks = value; return INA_OK;
         case 9: return set_small_sort(value);
+        case 10: return set_switch_win(value);
+        case 11: return set_ack_fast(value);
         default: return INA_EINVAL;
     }
 }

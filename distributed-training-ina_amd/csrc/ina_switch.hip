@@ -50,8 +50,8 @@ __device__ __forceinline__ uint32_t rd_be32(const uint8_t* p) {
 // The P4 registers see each slot's packets in arrival order, so the batch is grouped by
 // slot with a STABLE sort.  Keys need only ceil(log2(num_slots + 1)) bits (18 at 2^17
 // slots), so the sort is 1-3 digit passes of <= 9 bits.  A block owns a chunk of 4096
-// consecutive items, its wave w the w-th 1024 of them (16 rounds of 64, in order; all
-// loads issued up front):
+// consecutive items (1024 / 2048 for smaller batches, see sort_plan), its wave w the w-th
+// quarter of them (rounds of 64, in order; all loads issued up front):
 //   hist     the chunk's digit counts (LDS) -> cnt[digit][chunk]
 //   colscan  one wave per digit: exclusive scan along the chunks (in place) + the
 //            digit's total
@@ -70,10 +70,20 @@ constexpr int kRsBins = 1 << kRsMaxBits;     // 512
 #define INA_RS_ROUNDS 16
 #endif
 constexpr int kRsRounds = INA_RS_ROUNDS;
+#ifndef INA_RS_ROUNDS_SMALL
+#define INA_RS_ROUNDS_SMALL 4
+#endif
+#ifndef INA_RS_SMALL_ITEMS
+#define INA_RS_SMALL_ITEMS 262144
+#endif
+#ifndef INA_RS_ROUNDS_MID
+#define INA_RS_ROUNDS_MID 8
+#endif
+#ifndef INA_RS_MID_ITEMS
+#define INA_RS_MID_ITEMS 524288
+#endif
 constexpr int kRsBlock = 64 * INA_RS_WAVES;
 constexpr int kRsWaves = kRsBlock / 64;
-constexpr int kRsWaveItems = 64 * kRsRounds;
-constexpr int kRsChunk = kRsWaves * kRsWaveItems;       // items per block (4096)
 static_assert(kRsBins % kRsBlock == 0, "digits split evenly over the block's threads");
 
 __device__ __forceinline__ unsigned long long lanes_with_digit(uint32_t d, int bits, bool valid) {
@@ -103,23 +113,26 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 // 1. keys: aggregator slot of each packet, or num_slots (sorts last) for packets that
 //    are not this switch's (switch_check miss, ngaa.p4:27-37,184-186); fused with the
 //    first digit pass's chunk histogram.
+constexpr uint32_t kAckBit = 0x80000000u;
+template <int R>
 __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restrict__ pkts,
                                                           size_t npk, size_t stride,
                                                           uint32_t num_slots, int switch_id,
                                                           uint32_t* __restrict__ keys,
                                                           uint8_t* __restrict__ actions, int bits,
-                                                          uint32_t* __restrict__ hist, size_t nch) {
+                                                          uint32_t* __restrict__ hist, size_t nch,
+                                                          int ack_hint) {
     __shared__ uint32_t h[kRsBins];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
     const uint32_t nb = 1u << bits;
     for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) h[d] = 0;
     __syncthreads();
-    const size_t p0 = c * kRsChunk + (size_t)wv * kRsWaveItems + (size_t)lane;
-    uint32_t idx[kRsRounds], sid[kRsRounds];
+    const size_t p0 = c * (kRsWaves * 64 * R) + (size_t)wv * (64 * R) + (size_t)lane;
+    uint32_t idx[R], sid[R], ack[R];
     if ((stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0) {   // header bytes 4..11
 #pragma unroll
-        for (int r = 0; r < kRsRounds; ++r) {
+        for (int r = 0; r < R; ++r) {
             const size_t p = p0 + (size_t)r * 64;
             uint32_t w1 = 0, w2 = 0;
             if (p < npk) {
@@ -129,22 +142,25 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
             }
             idx[r] = __builtin_bswap32((w1 >> 16) | (w2 << 16));
             sid[r] = (w2 >> 16) & 0xFFu;
+            ack[r] = (w1 >> 14) & 1u;                          // flags byte 5, bit 6
         }
     } else {
 #pragma unroll
-        for (int r = 0; r < kRsRounds; ++r) {
+        for (int r = 0; r < R; ++r) {
             const size_t p = p0 + (size_t)r * 64;
             idx[r] = p < npk ? rd_be32(pkts + p * stride + 6) : 0u;
             sid[r] = p < npk ? pkts[p * stride + 10] : 0u;
+            ack[r] = p < npk ? (pkts[p * stride + 5] >> 6) & 1u : 0u;
         }
     }
 #pragma unroll
-    for (int r = 0; r < kRsRounds; ++r) {
+    for (int r = 0; r < R; ++r) {
         const size_t p = p0 + (size_t)r * 64;
         if (p < npk) {
             const bool mine = switch_id >= 0 && sid[r] == (uint32_t)(uint8_t)switch_id;
             const uint32_t key = mine ? idx[r] % num_slots : num_slots;
-            keys[p] = key;
+            // bit 31 carries "PS ack" through the sort (the digit passes never read it)
+            keys[p] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
             if (!mine) actions[p] = INA_ACT_FWD_OTHER;
             atomicAdd(&h[key & (nb - 1)], 1u);
         }
@@ -165,6 +181,17 @@ constexpr int kSmallBatch = 4096;                 // LDS capacity of the one-wor
 static_assert(INA_SWITCH_SMALL_MAX <= kSmallBatch, "small path limited by its LDS");
 constexpr int kSmallBlock = 1024;
 static std::atomic<int> g_small_sort{1};   // ina_set_tuning key 9 (0: always the radix path)
+static std::atomic<int> g_switch_win{0};   // ina_set_tuning key 10: run-kernel window (0: auto)
+static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack lane path (0: off)
+int set_ack_fast(int v) {
+    g_ack_fast = v ? 1 : 0;
+    return INA_OK;
+}
+int set_switch_win(int v) {
+    if (v < 0 || v > 64) return INA_EINVAL;
+    g_switch_win = v;
+    return INA_OK;
+}
 int set_small_sort(int v) {
     g_small_sort = v ? 1 : 0;
     return INA_OK;
@@ -234,6 +261,7 @@ __global__ __launch_bounds__(kSmallBlock) void k_switch_sort_small(
 }
 
 // later passes: chunk histogram of digit (key >> shift)
+template <int R>
 __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const uint32_t* __restrict__ keys, size_t n,
                                                       int shift, int bits,
                                                       uint32_t* __restrict__ hist, size_t nch) {
@@ -243,12 +271,12 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const uint32_t* __restrict
     const uint32_t nb = 1u << bits;
     for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) h[d] = 0;
     __syncthreads();
-    const size_t i0 = c * kRsChunk + (size_t)wv * kRsWaveItems + (size_t)lane;
-    uint32_t k[kRsRounds];
+    const size_t i0 = c * (kRsWaves * 64 * R) + (size_t)wv * (64 * R) + (size_t)lane;
+    uint32_t k[R];
 #pragma unroll
-    for (int r = 0; r < kRsRounds; ++r) k[r] = i0 + (size_t)r * 64 < n ? keys[i0 + (size_t)r * 64] : 0u;
+    for (int r = 0; r < R; ++r) k[r] = i0 + (size_t)r * 64 < n ? keys[i0 + (size_t)r * 64] : 0u;
 #pragma unroll
-    for (int r = 0; r < kRsRounds; ++r)
+    for (int r = 0; r < R; ++r)
         if (i0 + (size_t)r * 64 < n) atomicAdd(&h[(k[r] >> shift) & (nb - 1)], 1u);
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
@@ -285,7 +313,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_colscan(uint32_t* __restrict__ 
 
 // scatter: out position = base(digit, chunk, wave) + items of that digit the wave already
 // placed + rank among this round's lanes with the same digit
-template <bool kIds>
+template <bool kIds, int R>
 __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin,
                                                          uint32_t* __restrict__ kout,
@@ -299,10 +327,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
     const uint32_t nb = 1u << bits;
-    const size_t i0 = c * kRsChunk + (size_t)wv * kRsWaveItems + (size_t)lane;
-    uint32_t k[kRsRounds], v[kRsRounds];
+    const size_t i0 = c * (kRsWaves * 64 * R) + (size_t)wv * (64 * R) + (size_t)lane;
+    uint32_t k[R], v[R];
 #pragma unroll
-    for (int r = 0; r < kRsRounds; ++r) {
+    for (int r = 0; r < R; ++r) {
         const size_t i = i0 + (size_t)r * 64;
         k[r] = i < n ? kin[i] : 0u;
         v[r] = kIds ? (i < n ? vin[i] : 0u) : (uint32_t)i;
@@ -323,7 +351,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
         if (d < nb) dbase[d] = tot[j];
     }
 #pragma unroll
-    for (int r = 0; r < kRsRounds; ++r)              // this wave's digit counts
+    for (int r = 0; r < R; ++r)              // this wave's digit counts
         if (i0 + (size_t)r * 64 < n) atomicAdd(&base[wv][(k[r] >> shift) & (nb - 1)], 1u);
     __syncthreads();
     if (wv == 0) {                                   // digit bases: exclusive scan of the totals
@@ -352,7 +380,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
     __syncthreads();
     const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int r = 0; r < kRsRounds; ++r) {
+    for (int r = 0; r < R; ++r) {
         if (i0 - (size_t)lane + (size_t)r * 64 >= n) break;      // wave-uniform
         const bool valid = i0 + (size_t)r * 64 < n;
         const uint32_t d = (k[r] >> shift) & (nb - 1);
@@ -542,7 +570,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                                                           const uint32_t* __restrict__ keys,
                                                           const uint32_t* __restrict__ ids,
                                                           uint8_t* __restrict__ actions,
-                                                          uint32_t win) {
+                                                          uint32_t win, uint32_t kmask) {
     const int lane = threadIdx.x & 63;
     const int V = st.V;
     const int L = V >> 2;                       // lanes holding values
@@ -555,10 +583,21 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
     // START in its window (a segment may run past the window's end)
     for (size_t w0 = wave * win; w0 < npk; w0 += nwaves * win) {
         const size_t i = w0 + (size_t)lane;
-        const uint32_t ki = i < npk ? keys[i] : NS;
+        const uint32_t kr = i < npk ? keys[i] : NS;
+        const uint32_t ki = kr & kmask;                   // slot (bit 31: PS-ack hint)
         const uint32_t idw = i < npk ? ids[i] : 0u;     // packet ids of the window, one load
-        const uint32_t kp = (i > 0 && i <= npk) ? keys[i - 1] : 0xFFFFFFFFu;
-        unsigned long long hm = __ballot((uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki));
+        const uint32_t kp = (i > 0 && i <= npk) ? (keys[i - 1] & kmask) : 0xFFFFFFFFu;
+        const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
+        // a PS ack alone in its segment only clears the slot's frag register and is
+        // forwarded unchanged (fragcheck.p4:26-31, ngaa.p4:130-132): every such lane of the
+        // window at once, no packet read (lane 63 never qualifies: its successor is unknown)
+        const uint32_t kn = (uint32_t)__builtin_amdgcn_update_dpp((int)ki, (int)ki, 0x130, 0xF, 0xF, false);
+        const bool lone_ack = head && (kr & ~kmask) != 0u && kn != ki;
+        if (lone_ack) {
+            st.frag[ki] = 0u;
+            actions[idw] = INA_ACT_FWD_ACK;
+        }
+        unsigned long long hm = __ballot(head && !lone_ack);
         while (hm) {
         const int hl = __builtin_ctzll(hm);
         hm &= hm - 1;
@@ -574,7 +613,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                 size_t j0 = w0 + 64;
                 for (;;) {
                     const size_t j = j0 + (size_t)lane;
-                    const bool diff = j >= npk || keys[j] != slot;
+                    const bool diff = j >= npk || (keys[j] & kmask) != slot;
                     const unsigned long long m = __ballot(diff);
                     if (m) { end = j0 + (size_t)__builtin_ctzll(m); break; }
                     j0 += 64;
@@ -732,7 +771,7 @@ static int end_bit_for(uint32_t num_slots) {
 }
 
 struct SortPlan {
-    int passes, bits;
+    int passes, bits, rounds;   // rounds: 64-item rounds per wave (chunk = 4 waves x 64 x rounds)
     size_t nch, hist_elems;
 };
 
@@ -741,7 +780,15 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     const int eb = end_bit_for(num_slots);
     p.passes = (eb + kRsMaxBits - 1) / kRsMaxBits;
     p.bits = (eb + p.passes - 1) / p.passes;
-    p.nch = (npk + kRsChunk - 1) / kRsChunk;
+    // chunk = 4 waves x 64 x rounds items: 1,024 up to 256 Ki packets (a batch of the PS's
+    // acks still spreads over more than a few dozen CUs), 2,048 up to 512 Ki, 4,096 above
+    // (switch_lab, profiles/r01/lab/switch_lab_rounds.log: 102,400 packets 77.7 -> 60.9 us,
+    // 409,600 155.5 -> 146.1, 819,200 unchanged)
+    p.rounds = npk <= (size_t)INA_RS_SMALL_ITEMS ? INA_RS_ROUNDS_SMALL
+             : npk <= (size_t)INA_RS_MID_ITEMS   ? INA_RS_ROUNDS_MID
+                                                 : kRsRounds;
+    const size_t chunk = (size_t)kRsWaves * 64 * (size_t)p.rounds;
+    p.nch = (npk + chunk - 1) / chunk;
     p.hist_elems = ((size_t)1 << p.bits) * p.nch;
     return p;
 }
@@ -817,6 +864,15 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
     uint32_t* v_in = reinterpret_cast<uint32_t*>(base + 2 * arr);
     uint32_t* v_out = reinterpret_cast<uint32_t*>(base + 3 * arr);
     const SortPlan sp = sort_plan(npk, st->num_slots);
+    // sort chunk geometry (sort_plan): one instantiation per rounds-per-wave choice
+    constexpr int kR0 = INA_RS_ROUNDS_SMALL, kR1 = INA_RS_ROUNDS_MID, kR2 = kRsRounds;
+    const int ri = sp.rounds == kR0 ? 0 : sp.rounds == kR1 ? 1 : 2;
+    auto* k_keys = ri == 0 ? &k_switch_keys<kR0> : ri == 1 ? &k_switch_keys<kR1> : &k_switch_keys<kR2>;
+    auto* k_hist = ri == 0 ? &k_rs_hist<kR0> : ri == 1 ? &k_rs_hist<kR1> : &k_rs_hist<kR2>;
+    auto* k_sc0 = ri == 0 ? &k_rs_scatter<false, kR0>
+                : ri == 1 ? &k_rs_scatter<false, kR1> : &k_rs_scatter<false, kR2>;
+    auto* k_sc1 = ri == 0 ? &k_rs_scatter<true, kR0>
+                : ri == 1 ? &k_rs_scatter<true, kR1> : &k_rs_scatter<true, kR2>;
     uint32_t* hist = reinterpret_cast<uint32_t*>(base + 4 * arr);
     uint32_t* totals = reinterpret_cast<uint32_t*>(base + 4 * arr + align_up(sp.hist_elems * 4, 256));
     const unsigned gc = (unsigned)sp.nch;
@@ -824,6 +880,10 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
     const unsigned gd = (nb + kRsWaves - 1) / kRsWaves;
 
     uint32_t *kc = k_in, *vc = v_in, *kn = k_out, *vn = v_out;
+    const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
+                      st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
+    // keys carry the PS-ack bit for the run kernel when bit 31 is free of slot bits
+    const bool ack_hint = fast && end_bit_for(st->num_slots) <= 31 && g_ack_fast.load();
     const bool small = npk <= (size_t)INA_SWITCH_SMALL_MAX && g_small_sort.load();
     if (small) {
         if ((uint64_t)st->num_slots + 1 <= (1u << 20))
@@ -834,40 +894,39 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
                                s, pkts, (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
-        hipLaunchKernelGGL(k_switch_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts, npk, stride,
-                           st->num_slots, st->switch_id, k_in, actions, sp.bits, hist, sp.nch);
+        hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts, npk, stride, st->num_slots,
+                           st->switch_id, k_in, actions, sp.bits, hist, sp.nch, ack_hint ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
     }
     // digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
     for (int pass = 0; pass < (small ? 0 : sp.passes); ++pass) {
         const int shift = pass * sp.bits;
         if (pass > 0)
-            hipLaunchKernelGGL(k_rs_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits,
-                               hist, sp.nch);
+            hipLaunchKernelGGL(k_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits, hist,
+                               sp.nch);
         hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, hist, sp.nch, nb, totals);
         if (pass == 0)
-            hipLaunchKernelGGL(k_rs_scatter<false>, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn,
-                               vn, npk, shift, sp.bits, hist, totals, sp.nch);
+            hipLaunchKernelGGL(k_sc0, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn, vn, npk, shift,
+                               sp.bits, hist, totals, sp.nch);
         else
-            hipLaunchKernelGGL(k_rs_scatter<true>, dim3(gc), dim3(kRsBlock), 0, s, kc, vc, kn, vn,
-                               npk, shift, sp.bits, hist, totals, sp.nch);
+            hipLaunchKernelGGL(k_sc1, dim3(gc), dim3(kRsBlock), 0, s, kc, vc, kn, vn, npk, shift,
+                               sp.bits, hist, totals, sp.nch);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
         std::swap(kc, kn);
         std::swap(vc, vn);
     }
-    const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
-                      st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
     if (fast) {
         // a wave runs the segments that start in its window of `win` sorted positions: a
         // segment is a chain of dependent round trips, so small windows (more waves) win
         // at every size -- tools/lab/switch_lab.py, profiles/r01/lab/switch_lab_win.log:
         // 1,024 packets 52.9 -> 27.7 us (64 -> 8 positions), 819,200 packets 277 -> 266 us
         // (64 -> 16 positions, one pass of the grid)
-        const uint32_t win = npk <= 65536 ? (uint32_t)INA_SWITCH_WIN_SMALL : (uint32_t)INA_SWITCH_WIN_LARGE;
+        uint32_t win = npk <= 65536 ? (uint32_t)INA_SWITCH_WIN_SMALL : (uint32_t)INA_SWITCH_WIN_LARGE;
+        if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
         const size_t per_block = (size_t)win * (kSwBlock / 64);
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         hipLaunchKernelGGL(k_switch_run2, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,
-                           vc, actions, win);
+                           vc, actions, win, ack_hint ? ~kAckBit : 0xFFFFFFFFu);
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
         hipLaunchKernelGGL(k_switch_run, dim3(gw), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,

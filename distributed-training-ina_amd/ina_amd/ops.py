@@ -408,14 +408,18 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                nontemporal: bool | None = None, reduce_blocks: int | None = None,
                stream_blocks: int | None = None, combine_blocks: int | None = None,
                combine_ina_blocks: int | None = None, h2d_streams: int | None = None,
-               launch_chunks: int | None = None, switch_small_sort: bool | None = None):
+               launch_chunks: int | None = None, switch_small_sort: bool | None = None,
+               switch_window: int | None = None, switch_ack_fast: bool | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
     PS combine, combine_ina_blocks the INA-semantics combine, h2d_streams the host-ingest
     pipeline's H2D copy streams (1 or 2), launch_chunks the 16-byte chunks one flat packet
     kernel launch covers (default 2^31 - 1; smaller values only split launches),
-    switch_small_sort the one-workgroup key+sort path for switch batches <= 4096 packets; unroll is the sum-reduce's 16-byte chunks per worker per thread."""
+    switch_small_sort the one-workgroup key+sort path for switch batches <= 4096 packets,
+    switch_window the sorted positions one wave of the switch run kernel owns (0 = auto,
+    1..64), switch_ack_fast the lane-parallel path for PS acks alone in their slot's
+    segment; unroll is the sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")
@@ -431,6 +435,10 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(8, int(launch_chunks)), "set_tuning")
     if switch_small_sort is not None:
         check(lib.ina_set_tuning(9, int(bool(switch_small_sort))), "set_tuning")
+    if switch_window is not None:
+        check(lib.ina_set_tuning(10, int(switch_window)), "set_tuning")
+    if switch_ack_fast is not None:
+        check(lib.ina_set_tuning(11, int(bool(switch_ack_fast))), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

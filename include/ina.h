@@ -62,6 +62,16 @@ typedef void* ina_stream_t; /* hipStream_t */
 const char* ina_version(void);
 const char* ina_last_error_string(void);
 
+/* Launch-geometry knobs (process-wide; results never change, only speed).  Keys:
+ * 0 elementwise grid cap, 1 reduce chunks per worker per thread (1/2/4), 2 reduce
+ * non-temporal loads/stores (0/1), 3 reduce grid (0 = 64*W rule), 4 chunk-loop grid,
+ * 5 fp32 PS-combine grid, 6 INA PS-combine grid, 7 host-ingest H2D streams (1/2),
+ * 8 16-byte chunks per flat packet-kernel launch, 9 switch one-workgroup small-batch
+ * path (0/1), 10 switch run-kernel window in sorted positions (0 = auto, 1..64),
+ * 11 switch lane-parallel path for PS acks alone in their slot's segment (0/1).
+ * Returns INA_EINVAL for an unknown key or value.                                 */
+int ina_set_tuning(int key, int value);
+
 /* ---- quantise / dequantise ---------------------------------------------------
  * Replaces float_to_int / int_to_float, imported at DataManager.py:9 and
  * NGAPacket.py:5 (used DataManager.py:37,168, NGAPacket.py:118) but absent from

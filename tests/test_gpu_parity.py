@@ -556,6 +556,38 @@ def test_switch_fuzz_vs_oracle(seed):
     assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
 
 
+@pytest.mark.parametrize("ack_fast", [True, False])
+@pytest.mark.parametrize("W,ack", [(1, 0.5), (1, 1.0), (2, 0.4), (5, 0.3)])
+def test_switch_lone_acks_vs_oracle(W, ack, ack_fast):
+    """Radix-path batches (> 2,048 packets) full of short segments: a PS ack alone in its
+    slot's segment takes the run kernel's lane-parallel path (its bit rides through the
+    slot sort in the key), everything else the per-segment state machine; bit-exact
+    against the oracle either way, with the switch state carried across batches."""
+    rng = np.random.default_rng(7 * W + int(ack * 10) + ack_fast)
+    o = ops()
+    V, num_slots = 32, 8192
+    stride = o.nga_stride(V)
+    o.set_tuning(switch_ack_fast=ack_fast)
+    try:
+        sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
+        sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+        for rnd in range(3):
+            stream = make_stream(rng, V, 3000 // W + 1, W, num_slots, collide=0.05,
+                                 ack=ack if rnd else 0.0, other=0.05, stride=stride)
+            assert stream.shape[0] > 2048
+            want_pk, want_act = sw_orc.run(stream, stride=stride)
+            d = dev(stream)
+            act = sw_dev.process(d)
+            assert np.array_equal(host(act), want_act), rnd
+            assert np.array_equal(host(d), want_pk), rnd
+        cnt, frag, regs = sw_orc.registers()
+        assert np.array_equal(host(sw_dev.count), cnt)
+        assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+        assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+    finally:
+        o.set_tuning(switch_ack_fast=True)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_switch_small_batch_paths_agree(seed):
     """Batches of <= 4096 packets take the one-workgroup key+bitonic-sort path; the same
@@ -603,20 +635,23 @@ def test_switch_collision_free_equals_bulk_reduce():
     assert np.array_equal(got, host(o.sum_reduce([dev(b) for b in bufs])))
 
 
-def test_switch_config3_full_size_equals_bulk_reduce():
+@pytest.mark.parametrize("V,n,pool", [(256, 26_214_400, 1 << 17), (32, 1_280_000, 1 << 16),
+                                      (64, 1_600_000, 1 << 15)])
+def test_switch_config3_full_size_equals_bulk_reduce(V, n, pool):
     """Config 3 at full size through the packet path: 8 workers x 26,214,400 int32 ->
     819,200 NGA-256 packets -> device switch (2^17-slot pool, multi-pass radix sort,
     windowed run kernel) -> the 102,400 completed packets, unpacked and ordered by frag id,
-    equal the bulk W-way sum-reduce bit for bit (full-range values, so the sums wrap)."""
+    equal the bulk W-way sum-reduce bit for bit (full-range values, so the sums wrap).
+    The smaller cases take the sort's other chunk geometries (320,000 and 200,000 packets)."""
     o = ops()
-    V, W, n = 256, 8, 26_214_400
+    W = 8
     g = torch.Generator(device=DEV).manual_seed(31)
     bufs = [torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
             for _ in range(W)]
     want = o.sum_reduce(bufs)
-    stream = torch.cat([o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=1 << 17) for w, b in enumerate(bufs)])
+    stream = torch.cat([o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=pool) for w, b in enumerate(bufs)])
     del bufs
-    sw = o.Switch(V, num_slots=1 << 17, switch_id=1, device=DEV)
+    sw = o.Switch(V, num_slots=pool, switch_id=1, device=DEV)
     act = sw.process(stream)
     npk = n // V
     done = torch.nonzero(act == orc.ACT_FWD_AGG).flatten()
