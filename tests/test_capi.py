@@ -166,3 +166,17 @@ def test_socket_entry_points_reject_bad_descriptors():
     assert lib.ina_send_packets_fd(-1, None, 2, 144, 144, 0) < 0
     assert lib.ina_recv_packets_fd(-1, None, 2, 144, 0, 0, None) < 0
     assert lib.ina_send_gradients_fd(-1, None, 1, 0, 1, 0, 0) < 0
+
+
+def test_set_tuning_rejects_unknown_keys_and_values():
+    """Launch-geometry knobs (include/ina.h ina_set_tuning): bad keys/values are refused
+    and leave the defaults alone; no device work is involved."""
+    from ina_amd import _lib
+    lib = _lib.load()
+    assert lib.ina_set_tuning(99, 1) == _lib.INA_EINVAL
+    assert lib.ina_set_tuning(-1, 1) == _lib.INA_EINVAL
+    assert lib.ina_set_tuning(1, 3) == _lib.INA_EINVAL          # reduce chunks: 1, 2 or 4
+    assert lib.ina_set_tuning(7, 3) == _lib.INA_EINVAL          # H2D streams: 1 or 2
+    assert lib.ina_set_tuning(10, 65) == _lib.INA_EINVAL        # switch window <= 64
+    assert lib.ina_set_tuning(10, 0) == _lib.INA_OK             # 0 = automatic
+    assert lib.ina_set_tuning(11, 1) == _lib.INA_OK
