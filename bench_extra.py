@@ -232,7 +232,32 @@ def run_extra(dev):
                      note="bytes = the sum of the four stages' algorithmic HBM bytes (so frac is the "
                           "path's roofline fraction); aggregated_GBps = worker fp32 bytes aggregated "
                           "per second through the packet path"))
-    del xs, glob_p, upd, acks, ack_acts, rows_w, stream
+    del acks, ack_acts, rows_w, stream
+
+    # steady state: the PS's acks for step t reach the switch in the same batch as the
+    # workers' packets for step t+1, in front of them (the ack frees the slot before the
+    # slot's next packets claim it -- arrival order is what the slot sort keeps)
+    big = torch.zeros(((Ws + 1) * npk, row_b), dtype=torch.uint8, device=dev)   # [acks | 8 workers]
+    ack_rows, rows_w2 = big[:npk], big[npk:].view(Ws, npk, row_b)
+    acts2 = torch.empty((Ws + 1) * npk, dtype=torch.uint8, device=dev)
+    sw2 = ops.Switch(V, num_slots=1 << 17, switch_id=1, device=dev)
+
+    def ina_step_steady():
+        for w in range(Ws):
+            ops.quantize_pack_nga(xs[w], 16, V, w + 1, Ws, 1, 1, base=glob_p, num_slots=1 << 17,
+                                  out=rows_w2[w])
+        sw2.process(big, acts2)
+        ops.apply_completed(big, acts2, V, 1, glob_p, 16, 1.0 / (Ws + 1), out=upd, acks=ack_rows)
+    ina_step_steady()                      # first step: the ack rows are zero (another switch's)
+    t = _time(ina_step_steady, reps=5, warm=1)
+    ina_step_steady()
+    torch.cuda.synchronize()
+    ok = bool((acts2[npk:] == 1).sum() == npk) and bool((acts2[:npk] == 3).all())
+    rows.append(_row("INA packet path step, steady state: step t's acks ride in front of step t+1's packets",
+                     t, path_bytes - npk * 6, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
+                     acks_and_slots_ok=ok,
+                     note="one switch batch per step: (W+1) x 102,400 packets; bytes as the row above"))
+    del xs, glob_p, upd, big, ack_rows, rows_w2, acts2, sw2
 
     # small batches through the switch (P4 format: NGA-32, 16,384-slot pool): latency of
     # one ina_switch_process call, the stand-in's per-batch cost when packets arrive in

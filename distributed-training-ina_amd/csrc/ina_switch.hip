@@ -588,16 +588,19 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
         const uint32_t idw = i < npk ? ids[i] : 0u;     // packet ids of the window, one load
         const uint32_t kp = (i > 0 && i <= npk) ? (keys[i - 1] & kmask) : 0xFFFFFFFFu;
         const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
-        // a PS ack alone in its segment only clears the slot's frag register and is
-        // forwarded unchanged (fragcheck.p4:26-31, ngaa.p4:130-132): every such lane of the
-        // window at once, no packet read (lane 63 never qualifies: its successor is unknown)
+        // a PS ack only clears the slot's frag register and is forwarded unchanged
+        // (fragcheck.p4:26-31, ngaa.p4:130-132), so an ack at the HEAD of its segment is
+        // done here for every such lane of the window at once, without reading the packet:
+        // alone in its segment it also stores frag = 0; otherwise its segment runs below
+        // from the next position with frag = 0 (lane 63 is never "alone": its successor is
+        // unknown)
         const uint32_t kn = (uint32_t)__builtin_amdgcn_update_dpp((int)ki, (int)ki, 0x130, 0xF, 0xF, false);
-        const bool lone_ack = head && (kr & ~kmask) != 0u && kn != ki;
-        if (lone_ack) {
-            st.frag[ki] = 0u;
-            actions[idw] = INA_ACT_FWD_ACK;
-        }
+        const bool head_ack = head && (kr & ~kmask) != 0u;
+        const bool lone_ack = head_ack && kn != ki;
+        if (head_ack) actions[idw] = INA_ACT_FWD_ACK;
+        if (lone_ack) st.frag[ki] = 0u;
         unsigned long long hm = __ballot(head && !lone_ack);
+        const unsigned long long am = __ballot(head_ack && !lone_ack);   // segments led by an ack
         while (hm) {
         const int hl = __builtin_ctzll(hm);
         hm &= hm - 1;
@@ -623,11 +626,12 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
         // slot state: count and frag are wave-uniform (SGPRs, scalar branches); the V
         // registers are loaded only if a packet adds to them before any overwrite
         // (count_reg == 1 overwrites, processor.p4:16-21), i.e. rarely
+        const bool ack_led = (am >> hl) & 1ull;
         uint32_t cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
-        uint32_t frag = __builtin_amdgcn_readfirstlane(st.frag[slot]);
+        uint32_t frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
         u32x4s reg = {0u, 0u, 0u, 0u};
         bool have_reg = false;
-        for (size_t q0 = pos; q0 < end; q0 += kB) {
+        for (size_t q0 = pos + (ack_led ? 1 : 0); q0 < end; q0 += kB) {
             const int nb = (int)((end - q0) < (size_t)kB ? (end - q0) : (size_t)kB);
             u32x4s a[kB];
             uint32_t pid[kB];

@@ -661,6 +661,39 @@ def test_switch_config3_full_size_equals_bulk_reduce(V, n, pool):
     assert torch.equal(vals.view(npk, V)[order].reshape(-1), want)
 
 
+@pytest.mark.parametrize("V,W,per", [(32, 4, 3000), (256, 8, 700)])
+def test_steady_state_acks_ride_with_next_step(V, W, per):
+    """Steady-state packet path: step t's PS acks sit in front of step t+1's worker packets
+    in ONE switch batch (the bench's steady-state row).  Every step the device switch
+    equals the oracle's P4 restatement on the same bytes (actions, packets, registers):
+    the acks free the slots (FWD_ACK) and the new packets complete them (FWD_AGG)."""
+    rng = np.random.default_rng(V + W)
+    o = ops()
+    n = V * per
+    stride = o.nga_stride(V)
+    big = torch.zeros(((W + 1) * per, stride), dtype=torch.uint8, device=DEV)
+    ack_rows, rows_w = big[:per], big[per:].view(W, per, stride)
+    sw_dev = o.Switch(V, num_slots=1 << 13, switch_id=1, device=DEV, write_dropped=True)
+    sw_orc = orc.Switch(V, num_slots=1 << 13, switch_id=1)
+    local = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(DEV)
+    for step in range(3):
+        q = [dev(rand_i32(rng, n)) for _ in range(W)]
+        for w in range(W):
+            o.pack_nga(q[w], V, w + 1, W, 1, 1, num_slots=1 << 13, out=rows_w[w])
+        stream = host(big).copy()
+        want_pk, want_act = sw_orc.run(stream, stride=stride)
+        act = sw_dev.process(big)
+        assert np.array_equal(host(act), want_act), step
+        assert np.array_equal(host(big), want_pk), step
+        assert int((want_act[per:] == orc.ACT_FWD_AGG).sum()) == per
+        assert (want_act[:per] == (orc.ACT_FWD_ACK if step else orc.ACT_FWD_OTHER)).all()
+        o.apply_completed(big, act, V, 1, local, 16, 0.2, acks=ack_rows)
+    cnt, frag, regs = sw_orc.registers()
+    assert np.array_equal(host(sw_dev.count), cnt)
+    assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+    assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+
+
 @pytest.mark.parametrize("V", [32, 256, 33, 100, 4])
 @pytest.mark.parametrize("with_base", [False, True])
 @pytest.mark.parametrize("padded", [True, False])
