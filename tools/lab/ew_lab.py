@@ -50,7 +50,7 @@ class Variant:
         self.fq16 = torch.empty((n + 255) // 256, dtype=torch.uint8, device=dev)
         self.t = {"quantize": [], "dequantize": [], "ps_apply": [], "qreduce_C2": [], "combine": [],
                   "combine_ina": [], "qreduce_C4": [], "quantize16": []}
-        for key, env in ((5, "COMBINE_BLOCKS"), (6, "COMBINE_INA_BLOCKS")):
+        for key, env in ((5, "COMBINE_BLOCKS"), (6, "COMBINE_INA_BLOCKS"), (4, "STREAM_BLOCKS")):
             if os.environ.get(env):
                 self.lib.ina_set_tuning(key, int(os.environ[env]))
 
