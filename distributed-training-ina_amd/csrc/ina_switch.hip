@@ -798,8 +798,12 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
 }
 
 static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
+    // sized for the SMALLEST chunk whatever tier npk falls in, so the scratch size is
+    // monotonic in npk: a buffer sized for a batch serves every smaller batch too
     const SortPlan p = sort_plan(npk, num_slots);
-    return align_up(p.hist_elems * 4, 256) + align_up((size_t)kRsBins * 4, 256);
+    const size_t chunk = (size_t)kRsWaves * 64 * (size_t)INA_RS_ROUNDS_SMALL;
+    const size_t hist = ((size_t)1 << p.bits) * ((npk + chunk - 1) / chunk);
+    return align_up(hist * 4, 256) + align_up((size_t)kRsBins * 4, 256);
 }
 
 }  // namespace ina

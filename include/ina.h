@@ -187,7 +187,8 @@ int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id,
  * processed in array order per slot (different slots are independent); forwarded
  * packets are rewritten in place (slot sum, collision bit; dropped ones too when
  * write_dropped) and actions[p] gets INA_ACT_*.
- * scratch: device buffer of ina_switch_scratch_bytes(npkts, num_slots) bytes.  */
+ * scratch: device buffer of ina_switch_scratch_bytes(npkts, num_slots) bytes; the size
+ * is monotonic in npkts, so one buffer sized for the largest batch serves them all. */
 typedef struct ina_switch_state {
     uint32_t num_slots;
     int32_t V;

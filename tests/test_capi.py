@@ -180,3 +180,17 @@ def test_set_tuning_rejects_unknown_keys_and_values():
     assert lib.ina_set_tuning(10, 65) == _lib.INA_EINVAL        # switch window <= 64
     assert lib.ina_set_tuning(10, 0) == _lib.INA_OK             # 0 = automatic
     assert lib.ina_set_tuning(11, 1) == _lib.INA_OK
+
+
+def test_switch_scratch_bytes_monotonic():
+    """One scratch buffer sized for the largest batch must serve every smaller one, across
+    the sort's chunk tiers (include/ina.h, ina_switch_scratch_bytes)."""
+    from ina_amd import _lib
+    lib = _lib.load()
+    for slots in (1, 64, 16384, 1 << 17, (1 << 31) - 1):
+        prev = 0
+        for npk in list(range(1, 5000, 37)) + list(range(250_000, 560_000, 1_013)) + [819_200]:
+            b = lib.ina_switch_scratch_bytes(npk, slots)
+            assert b >= prev, (slots, npk)
+            assert b >= 16 * npk
+            prev = b
