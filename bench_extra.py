@@ -257,7 +257,30 @@ def run_extra(dev):
                      t, path_bytes - npk * 6, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
                      acks_and_slots_ok=ok,
                      note="one switch batch per step: (W+1) x 102,400 packets; bytes as the row above"))
-    del xs, glob_p, upd, big, ack_rows, rows_w2, acts2, sw2
+    # the same with the PS on the switch's GPU: ina_switch_process_apply takes each completed
+    # slot's sum from the switch's registers straight into the update and the ack row (the
+    # completed packets are consumed, not written back)
+    big.zero_()
+    sw3 = ops.Switch(V, num_slots=1 << 17, switch_id=1, device=dev)
+
+    def ina_step_fused():
+        for w in range(Ws):
+            ops.quantize_pack_nga(xs[w], 16, V, w + 1, Ws, 1, 1, base=glob_p, num_slots=1 << 17,
+                                  out=rows_w2[w])
+        sw3.process_apply(big, 1, glob_p, 16, 1.0 / (Ws + 1), out=upd, acks=ack_rows,
+                          keep_forwarded=False, actions=acts2)
+    ina_step_fused()
+    t = _time(ina_step_fused, reps=5, warm=1)
+    ina_step_fused()
+    torch.cuda.synchronize()
+    ok = bool((acts2[npk:] == 1).sum() == npk) and bool((acts2[:npk] == 3).all())
+    fused_bytes = path_bytes - npk * 6 - (npk_all + npk * row_b) - npk * row_b  # no apply re-read, no fwd write
+    rows.append(_row("INA packet path step, steady state, PS fused into the switch pass",
+                     t, fused_bytes, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
+                     acks_and_slots_ok=ok,
+                     note="ina_switch_process_apply(keep_forwarded=0): bytes = the steady-state row's "
+                          "minus the PS's re-read of completed packets and their write-back"))
+    del xs, glob_p, upd, big, ack_rows, rows_w2, acts2, sw2, sw3
 
     # small batches through the switch (P4 format: NGA-32, 16,384-slot pool): latency of
     # one ina_switch_process call, the stand-in's per-batch cost when packets arrive in

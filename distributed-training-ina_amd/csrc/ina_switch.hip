@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 
 #include "ina.h"
 #include "ina_internal.h"
@@ -20,6 +21,7 @@
 namespace ina {
 
 using u32x4s = uint32_t __attribute__((ext_vector_type(4)));
+using f32x4s = float __attribute__((ext_vector_type(4)));
 
 constexpr int kSwBlock = 256;               // 4 waves, one slot segment each
 constexpr int kMaxV = 256;                  // 4 payload words per lane
@@ -564,13 +566,27 @@ __device__ __forceinline__ uint32_t enc_lo(uint32_t prev, uint32_t v) {
     return (__builtin_bswap32(prev) >> 8) | (v & 0xFF000000u);
 }
 
+// PS co-located with the switch (ina_switch_process_apply): a completed slot's sum goes
+// straight from the VGPRs into the PS update out = local + ws * (sum * 2^-k) and the PS
+// ack row -- exactly what ina_apply_completed_nga computes from the forwarded packet.
+struct PsFuse {
+    const float* local;
+    float* out;
+    size_t n;
+    float inv, ws;
+    uint32_t seq0, nslots;
+    uint8_t* acks;
+    size_t ack_stride;
+    int on, keep_fwd;   // keep_fwd = 0: completed packets are consumed, not written back
+};
+
 __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SWITCH_WAVES, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts, size_t npk,
                                                           size_t stride,
                                                           const uint32_t* __restrict__ keys,
                                                           const uint32_t* __restrict__ ids,
                                                           uint8_t* __restrict__ actions,
-                                                          uint32_t win, uint32_t kmask) {
+                                                          uint32_t win, uint32_t kmask, PsFuse ps) {
     const int lane = threadIdx.x & 63;
     const int V = st.V;
     const int L = V >> 2;                       // lanes holding values
@@ -726,7 +742,34 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                         }
                         have_reg = true;
                         act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
-                        if (act != INA_ACT_DROP || st.write_dropped) {
+                        const bool fused = ps.on && act == INA_ACT_FWD_AGG;
+                        if (fused) {                         // launch.py:46-50 with the switch's sum
+                            const uint32_t ps_slot = frag_in - ps.seq0;
+                            if (ps_slot < ps.nslots) {
+                                const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)lane;
+                                if (vl && e0 + 4 <= ps.n) {
+                                    const f32x4s l = *reinterpret_cast<const f32x4s*>(ps.local + e0);
+                                    f32x4s r;
+                                    r.x = __fadd_rn(l.x, __fmul_rn(__fmul_rn((float)(int32_t)reg.x, ps.inv), ps.ws));
+                                    r.y = __fadd_rn(l.y, __fmul_rn(__fmul_rn((float)(int32_t)reg.y, ps.inv), ps.ws));
+                                    r.z = __fadd_rn(l.z, __fmul_rn(__fmul_rn((float)(int32_t)reg.z, ps.inv), ps.ws));
+                                    r.w = __fadd_rn(l.w, __fmul_rn(__fmul_rn((float)(int32_t)reg.w, ps.inv), ps.ws));
+                                    *reinterpret_cast<f32x4s*>(ps.out + e0) = r;
+                                } else if (vl) {
+                                    const uint32_t rv[4] = {reg.x, reg.y, reg.z, reg.w};
+                                    for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
+                                        ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
+                                            __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
+                                }
+                                if (lane == 0 && ps.acks) {      // the PS ack (fragcheck.p4:26-31)
+                                    u32x4s hd = a[b];
+                                    hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+                                    hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                                    *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
+                                }
+                            }
+                        }
+                        if ((act != INA_ACT_DROP || st.write_dropped) && (!fused || ps.keep_fwd)) {
                             // out_value -> payload (processor.p4:22): chunk c from lane c-1
                             u32x4s p;
                             p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
@@ -853,8 +896,10 @@ size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots) {
     return 4 * align_up(npkts * 4, 256) + align_up(sort_temp_bytes(npkts, num_slots), 256) + 256;
 }
 
-int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                       uint8_t* actions, void* scratch, ina_stream_t stream) {
+static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                               uint8_t* actions, void* scratch, ina_stream_t stream, const PsFuse& ps,
+                               bool* fused_out) {
+    *fused_out = false;
     if (!st || st->V <= 0 || st->V > kMaxV || st->num_slots == 0)
         return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
     if (stride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)st->V)
@@ -934,7 +979,8 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
         const size_t per_block = (size_t)win * (kSwBlock / 64);
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         hipLaunchKernelGGL(k_switch_run2, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,
-                           vc, actions, win, ack_hint ? ~kAckBit : 0xFFFFFFFFu);
+                           vc, actions, win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps);
+        *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
         hipLaunchKernelGGL(k_switch_run, dim3(gw), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,
@@ -942,6 +988,37 @@ int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, 
     }
     if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch run launch%s", "");
     return INA_OK;
+}
+
+int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                       uint8_t* actions, void* scratch, ina_stream_t stream) {
+    PsFuse off{};
+    bool fused = false;
+    return switch_process_impl(st, pkts, npk, stride, actions, scratch, stream, off, &fused);
+}
+
+int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                             uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
+                             double weight_step, float* out, size_t n, uint8_t* acks,
+                             size_t ack_stride, int keep_forwarded, ina_stream_t stream) {
+    if (k < -126 || k > 127) return set_error(INA_EINVAL, "k out of range [-126,127]%s", "");
+    if (npk == 0) return INA_OK;
+    if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
+    if (((uintptr_t)local & 15u) || ((uintptr_t)out & 15u))
+        return set_error(INA_EINVAL, "local/out must be 16-byte aligned%s", "");
+    if (acks && (((uintptr_t)acks & 15u) || ack_stride % 16))
+        return set_error(INA_EINVAL, "ack rows must be 16-byte aligned%s", "");
+    if (!st || st->V <= 0) return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
+    const size_t nslots = (n + (size_t)st->V - 1) / (size_t)st->V;
+    PsFuse ps{local, out, n, ldexpf(1.0f, -k), (float)weight_step, seq0,
+              nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,
+              keep_forwarded ? 1 : 0};
+    bool fused = false;
+    if (int rc = switch_process_impl(st, pkts, npk, stride, actions, scratch, stream, ps, &fused)) return rc;
+    if (fused) return INA_OK;
+    // layouts the register-resident run kernel does not take: the two steps one by one
+    return ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,
+                                   n, acks, ack_stride, stream);
 }
 
 int ina_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_default,

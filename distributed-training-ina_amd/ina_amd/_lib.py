@@ -71,6 +71,8 @@ SIGNATURES = {
     "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],
     "ina_switch_scratch_bytes": [_sz, _u32],
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
+    "ina_switch_process_apply": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i, _d,
+                                 _vp, _sz, _vp, _sz, _i, _vp],
     "ina_route_ipv4": [_vp, _vp, _u32, _sz, _vp, _vp, _i, _vp, _vp],
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],
     "ina_absmax_f32": [_vp, _vp, _sz, _vp, _vp],

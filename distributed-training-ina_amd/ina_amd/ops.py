@@ -377,6 +377,35 @@ class Switch:
                                         _stream(pkts)), "switch_process")
         return actions
 
+    def process_apply(self, pkts: torch.Tensor, seq0: int, local: torch.Tensor, k: int,
+                      weight_step: float, out: torch.Tensor | None = None,
+                      acks: torch.Tensor | None = None, keep_forwarded: bool = True,
+                      actions: torch.Tensor | None = None):
+        """process() + apply_completed() in one pass (the PS on the switch's GPU): completed
+        slots update out = local + weight_step * sum * 2^-k and write their PS ack rows.
+        keep_forwarded=False leaves completed packets as they arrived (consumed here).
+        Returns (actions, out)."""
+        _req(pkts, torch.uint8, "pkts")
+        _req(local, torch.float32, "local")
+        npk, stride = pkts.shape
+        actions = torch.empty(npk, dtype=torch.uint8, device=pkts.device) if actions is None else actions
+        out = torch.empty_like(local) if out is None else out
+        _req(out, torch.float32, "out")
+        ack_ptr, ack_stride = None, 0
+        if acks is not None:
+            _req(acks, torch.uint8, "acks")
+            ack_ptr, ack_stride = acks.data_ptr(), acks.shape[1]
+        need = load().ina_switch_scratch_bytes(npk, self.num_slots)
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
+        check(load().ina_switch_process_apply(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                              actions.data_ptr(), self._scratch.data_ptr(),
+                                              seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
+                                              out.data_ptr(), local.numel(), ack_ptr, ack_stride,
+                                              int(keep_forwarded), _stream(pkts)),
+              "switch_process_apply")
+        return actions, out
+
 
 def route_ipv4(actions: torch.Tensor, keys: torch.Tensor, ports: torch.Tensor,
                dst_ip: torch.Tensor | None = None, dst_default: int = 0,

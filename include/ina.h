@@ -203,6 +203,18 @@ typedef struct ina_switch_state {
 size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots);
 int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
                        uint8_t* actions, void* scratch, ina_stream_t stream);
+/* The PS co-located with the switch on one GPU: ina_switch_process followed by
+ * ina_apply_completed_nga in ONE pass -- a completed slot's sum goes from the switch's
+ * registers straight into out[slot*V + j] = local + weight_step * sum * 2^-k (slot =
+ * frag_id - seq0) and its PS ack row, with the same results as the two calls.  With
+ * keep_forwarded = 0 the completed packets are consumed and their buffers left as they
+ * arrived (everything else as ina_switch_process).  Replaces the Tofino -> PS hop of
+ * ngaa.p4:170-175 + NGAPacket.py:62-143 + launch.py:42-52 when both live on the GPU. */
+int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
+                             size_t stride, uint8_t* actions, void* scratch, uint32_t seq0,
+                             const float* local, int k, double weight_step, float* out, size_t n,
+                             uint8_t* acks, size_t ack_stride, int keep_forwarded,
+                             ina_stream_t stream);
 
 /* ---- ipRoute (ngaa.p4:39-61, entries as bfrt/setup.py:85-95 installs them) -------
  * Every packet the ingress does not drop (actions FWD_AGG, FWD_COLLISION, FWD_ACK,

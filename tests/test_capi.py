@@ -136,6 +136,8 @@ def _einval_cases():
         "ina_apply_completed_nga": (None, 2, 32, 144, None, 1, None, 16, 0.5, None, 64, None, 144,
                                     None),
         "ina_switch_process": (ctypes.byref(st), None, 2, 144, None, None, None),
+        "ina_switch_process_apply": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
+                                     None, 64, None, 144, 1, None),
         "ina_route_ipv4": (None, None, 0, 4, None, None, 1, None, None),
         "ina_checksum_i32": (None, 64, None, None),
         "ina_absmax_f32": (None, None, 64, None, None),

@@ -668,6 +668,55 @@ def test_switch_config3_full_size_equals_bulk_reduce(V, n, pool):
     assert torch.equal(vals.view(npk, V)[order].reshape(-1), want)
 
 
+@pytest.mark.parametrize("keep", [True, False])
+@pytest.mark.parametrize("V,W,per,tail", [(32, 4, 60, 11), (256, 8, 700, 0), (32, 3, 3000, 5),
+                                          (64, 16, 200, 37)])
+def test_switch_process_apply_equals_two_steps(V, W, per, tail, keep):
+    """ina_switch_process_apply (the PS on the switch's GPU) == ina_switch_process then
+    ina_apply_completed_nga: same actions, switch registers, parameter update (bit for bit)
+    and PS ack rows, over two steps with the acks riding in front of the second step's
+    packets; keep_forwarded=False leaves completed packets as they arrived."""
+    rng = np.random.default_rng(V * W + per + keep)
+    o = ops()
+    n = V * per - tail
+    npk = -(-n // V)
+    stride = o.nga_stride(V)
+    local = dev(rng.standard_normal(n).astype(np.float32))
+    res = {}
+    for fused in (False, True):
+        big = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=DEV)
+        acks, rows = big[:npk], big[npk:].view(W, npk, stride)
+        sw = o.Switch(V, num_slots=1 << 13, switch_id=1, device=DEV)
+        g = np.random.default_rng(5)
+        outs = []
+        for step in range(2):
+            for w in range(W):
+                o.pack_nga(dev(rand_i32(g, n, full=False)), V, w + 1, W, 1, 7, num_slots=1 << 13,
+                           out=rows[w])
+            before = host(big).copy()
+            out = torch.full_like(local, float("nan"))
+            if fused:
+                act, _ = sw.process_apply(big, 7, local, 16, 0.25, out=out, acks=acks, keep_forwarded=keep)
+            else:
+                act = sw.process(big)
+                o.apply_completed(big, act, V, 7, local, 16, 0.25, out=out, acks=acks)
+            a = host(act)
+            pk = host(big)
+            if fused and not keep:
+                done = a == orc.ACT_FWD_AGG
+                assert done.sum() > 0 and np.array_equal(pk[done], before[done])
+            outs.append((a, pk[:npk].copy(), host(out).view(np.uint32), pk if keep or not fused else None))
+        res[fused] = (outs, host(sw.count), host(sw.frag), host(sw.regs))
+    (o0, c0, f0, r0), (o1, c1, f1, r1) = res[False], res[True]
+    for (a0, k0, u0, p0), (a1, k1, u1, p1) in zip(o0, o1):
+        assert np.array_equal(a0, a1)
+        assert np.array_equal(k0, k1)                 # PS ack rows
+        assert np.array_equal(u0, u1)                 # parameter update, bit for bit
+        if p1 is not None:
+            assert np.array_equal(p0, p1)
+    assert np.array_equal(c0, c1) and np.array_equal(f0, f1) and np.array_equal(r0, r1)
+
+
 @pytest.mark.parametrize("V,W,per", [(32, 4, 3000), (256, 8, 700)])
 def test_steady_state_acks_ride_with_next_step(V, W, per):
     """Steady-state packet path: step t's PS acks sit in front of step t+1's worker packets

@@ -76,6 +76,12 @@ def row_cells(tag):
             ", ".join(f"{k.split(': ')[1].split(' NGA')[0]} packets {r['us']:.1f} µs"
                       for k, r in ((r['kernel'], r) for r in small))
             + " (one-workgroup sort below 2,049 packets: 2 launches; radix path above)",
+        "INA packet path step, steady state, PS fused":
+            (lambda r: f"{r['us']:.0f} µs per step = {r['aggregated_GBps']:,.0f} GB/s of worker gradients; "
+                       f"{r['GB/s'] / 1e3:.1f} TB/s = {100 * r['frac']:.0f} % of peak for the path's bytes")(
+                e("INA packet path step, steady state, PS fused into the switch pass"))
+            if "INA packet path step, steady state, PS fused into the switch pass" in ex
+            else "(not in this session's bench_extra)",
         "INA packet path step, steady state":
             (lambda r: f"{r['us']:.0f} µs per step = {r['aggregated_GBps']:,.0f} GB/s of worker gradients; "
                        f"{r['GB/s'] / 1e3:.1f} TB/s = {100 * r['frac']:.0f} % of peak for the path's bytes")(
