@@ -580,6 +580,7 @@ struct PsFuse {
     int on, keep_fwd;   // keep_fwd = 0: completed packets are consumed, not written back
 };
 
+template <bool kPs>   // kPs: PS update fused (ina_switch_process_apply); false costs nothing
 __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SWITCH_WAVES, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts, size_t npk,
                                                           size_t stride,
@@ -742,7 +743,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                         }
                         have_reg = true;
                         act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
-                        const bool fused = ps.on && act == INA_ACT_FWD_AGG;
+                        const bool fused = kPs && act == INA_ACT_FWD_AGG;
                         if (fused) {                         // launch.py:46-50 with the switch's sum
                             const uint32_t ps_slot = frag_in - ps.seq0;
                             if (ps_slot < ps.nslots) {
@@ -978,8 +979,9 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
         const size_t per_block = (size_t)win * (kSwBlock / 64);
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
-        hipLaunchKernelGGL(k_switch_run2, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc,
-                           vc, actions, win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps);
+        auto* run = ps.on ? &k_switch_run2<true> : &k_switch_run2<false>;
+        hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc, vc, actions,
+                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps);
         *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
