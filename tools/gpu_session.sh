@@ -18,7 +18,7 @@ for st in $STAGES; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
       rc=$?; tail -3 "$OUT/smoke.log"; [ $rc -ne 0 ] && fatal smoke $rc ;;
     test)
-      timeout -k 10 1000 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -25 "$OUT/pytest_gpu.log"; ok_or_fail pytest $rc ;;
     bench)
       timeout -k 10 400 python bench.py --steps 50 --warmup 10 > "$OUT/bench.json" 2> "$OUT/bench.err"
