@@ -4,6 +4,7 @@ given on the command line runs ina_switch_process on the same 8-worker NGA-256 s
 (config-3 bucket), timed with HIP events; actions and forwarded packets must agree."""
 import ctypes as C
 import os
+import re
 import statistics
 import sys
 
@@ -32,6 +33,9 @@ class Variant:
         for nm in ("ina_switch_process", "ina_switch_scratch_bytes"):
             getattr(self.lib, nm).argtypes = _lib.SIGNATURES[nm]
         self.lib.ina_switch_scratch_bytes.restype = C.c_size_t
+        m = re.search(r"_w(\d+)\.so$", path)       # libina_w<N>.so: run-kernel window N (key 10)
+        if m:
+            assert self.lib.ina_set_tuning(10, int(m.group(1))) == 0
         self.count = torch.zeros(slots, dtype=torch.uint8, device=dev)
         self.frag = torch.zeros(slots, dtype=torch.int32, device=dev)
         self.regs = torch.zeros((slots, V), dtype=torch.int32, device=dev)
