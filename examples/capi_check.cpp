@@ -98,9 +98,46 @@ int main() {
         if (be != want) ++bad;
     }
     for (size_t i = n; i < npk * V; ++i) bad += back[i] != 0;   // zero-padded tail
+
+    // the packet path: every worker's quantised bucket as NGA-256 packets through the
+    // device switch with the PS update fused (local = 0, weight 1 -> out = dequantised sum)
+    const uint32_t slots = 1u << 13;
+    uint8_t* d_stream;
+    HK(hipMalloc(&d_stream, (size_t)W * npk * stride));
+    for (int w = 0; w < W; ++w) {
+        prm.bitmap = 1u << w; prm.num_slots = slots;
+        CK(ina_pack_nga(d_q[w], n, &prm, nullptr, d_stream + (size_t)w * npk * stride, stride, s));
+    }
+    uint8_t *d_count, *d_act;
+    uint32_t *d_frag, *d_regs;
+    float *d_zero, *d_out;
+    HK(hipMalloc(&d_count, slots));
+    HK(hipMalloc(&d_frag, slots * 4));
+    HK(hipMalloc(&d_regs, (size_t)slots * V * 4));
+    HK(hipMalloc(&d_act, (size_t)W * npk));
+    HK(hipMalloc(&d_zero, n * 4));
+    HK(hipMalloc(&d_out, n * 4));
+    HK(hipMemset(d_count, 0, slots));
+    HK(hipMemset(d_frag, 0, slots * 4));
+    HK(hipMemset(d_regs, 0, (size_t)slots * V * 4));
+    HK(hipMemset(d_zero, 0, n * 4));
+    ina_switch_state_t st = {slots, V, 1, 0, d_count, d_frag, d_regs};
+    void* d_scratch;
+    HK(hipMalloc(&d_scratch, ina_switch_scratch_bytes((size_t)W * npk, slots)));
+    CK(ina_switch_process_apply(&st, d_stream, (size_t)W * npk, stride, d_act, d_scratch, 1, d_zero, k,
+                                1.0, d_out, n, nullptr, 0, 0, s));
+    HK(hipStreamSynchronize(s));
+    std::vector<float> out(n);
+    std::vector<uint8_t> act((size_t)W * npk);
+    HK(hipMemcpy(out.data(), d_out, n * 4, hipMemcpyDeviceToHost));
+    HK(hipMemcpy(act.data(), d_act, act.size(), hipMemcpyDeviceToHost));
+    size_t done = 0;
+    for (uint8_t a : act) done += a == INA_ACT_FWD_AGG;
+    if (done != npk) ++bad;
+    for (size_t i = 0; i < n; ++i) bad += std::memcmp(&out[i], &f[i], 4) != 0;
     // the error path: a bad argument returns a code, sets a message, never exits
     const int rc = ina_sum_reduce_i32((const int32_t* const*)d_q, 0, d_sum, n, s);
     if (rc != INA_EINVAL || std::strlen(ina_last_error_string()) == 0) ++bad;
-    std::printf("capi_check: %zu values x %d workers, %zu mismatches\n", n, W, bad);
+    std::printf("capi_check: %zu values x %d workers (bulk reduce, NGA-256 pack/unpack, switch + fused PS step), %zu mismatches\n", n, W, bad);
     return bad ? 1 : 0;
 }
