@@ -1,7 +1,8 @@
 // capi_check.cpp -- a C/C++ caller of libina.so with no Python and no torch: links the
 // library through include/ina.h only, allocates device memory with the HIP runtime,
-// runs quantise -> W-way sum-reduce -> NGA-256 pack -> unpack -> dequantise and checks
-// every step against a host computation.  Built by `make -C examples`; run by
+// runs quantise -> W-way sum-reduce -> NGA-256 pack -> unpack -> dequantise, then the
+// workers' packets through the device switch with the PS step fused, and checks every
+// step against a host computation.  Built by `make -C examples`; run by
 // tests/test_gpu_capi_binary.py on the GPU box.  Exit status 0 = all checks passed.
 #include <hip/hip_runtime.h>
 
