@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of ina_switch_process_apply across libina builds (experiment only):
+8 workers x NGA-256 packets of a config-3 bucket, PS step fused; switch state reset
+between launches; outputs must agree."""
+import ctypes as C
+import os
+import statistics
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "distributed-training-ina_amd"))
+from ina_amd import _lib, ops  # noqa: E402
+
+dev = torch.device("cuda")
+n, W, V, slots = 26_214_400, 8, 256, 1 << 17
+g = torch.Generator(device=dev).manual_seed(2)
+bufs = [torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g) for _ in range(W)]
+stream = torch.cat([ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots) for w, b in enumerate(bufs)])
+del bufs
+npk_all, stride = stream.shape
+local = torch.randn(n, device=dev, generator=g)
+st = torch.cuda.current_stream().cuda_stream
+vs = []
+for p in sys.argv[1:]:
+    lib = C.CDLL(p)
+    for nm in ("ina_switch_process_apply", "ina_switch_scratch_bytes"):
+        getattr(lib, nm).argtypes = _lib.SIGNATURES[nm]
+    lib.ina_switch_scratch_bytes.restype = C.c_size_t
+    v = dict(name=os.path.basename(p), lib=lib, count=torch.zeros(slots, dtype=torch.uint8, device=dev),
+             frag=torch.zeros(slots, dtype=torch.int32, device=dev),
+             regs=torch.zeros((slots, V), dtype=torch.int32, device=dev),
+             acts=torch.empty(npk_all, dtype=torch.uint8, device=dev), out=torch.empty_like(local),
+             acks=torch.empty((n // V, stride), dtype=torch.uint8, device=dev), t=[])
+    v["st"] = _lib.SwitchState(slots, V, 1, 0, v["count"].data_ptr(), v["frag"].data_ptr(), v["regs"].data_ptr())
+    v["scratch"] = torch.empty(lib.ina_switch_scratch_bytes(npk_all, slots), dtype=torch.uint8, device=dev)
+    vs.append(v)
+
+
+def run(v):
+    v["count"].zero_()
+    v["frag"].zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    rc = v["lib"].ina_switch_process_apply(C.byref(v["st"]), stream.data_ptr(), npk_all, stride,
+                                           v["acts"].data_ptr(), v["scratch"].data_ptr(), 1,
+                                           local.data_ptr(), 16, 0.125, v["out"].data_ptr(), n,
+                                           v["acks"].data_ptr(), stride, 0, st)
+    e1.record()
+    assert rc == 0
+    return e0, e1
+
+
+for v in vs:
+    run(v)
+torch.cuda.synchronize()
+for v in vs[1:]:
+    assert torch.equal(v["out"].view(torch.int32), vs[0]["out"].view(torch.int32)), v["name"]
+    assert torch.equal(v["acks"][:, :16], vs[0]["acks"][:, :16]), v["name"]
+    assert torch.equal(v["acts"], vs[0]["acts"]), v["name"]
+for r in range(int(os.environ.get("ROUNDS", 6))):
+    for v in vs:
+        evs = [run(v) for _ in range(4)]
+        torch.cuda.synchronize()
+        v["t"] += [a.elapsed_time(b) * 1e3 for a, b in evs[1:]]
+for v in vs:
+    print(f"{v['name']:18s} switch+PS fused {statistics.median(v['t']):7.1f} us")
