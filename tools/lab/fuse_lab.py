@@ -66,3 +66,24 @@ for r in range(int(os.environ.get("ROUNDS", 6))):
         v["t"] += [a.elapsed_time(b) * 1e3 for a, b in evs[1:]]
 for v in vs:
     print(f"{v['name']:18s} switch+PS fused {statistics.median(v['t']):7.1f} us")
+
+# the same work as two calls (in-tree library): switch, then the PS apply kernel
+sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
+acts2 = torch.empty(npk_all, dtype=torch.uint8, device=dev)
+out2 = torch.empty_like(local)
+acks2 = torch.empty((n // V, stride), dtype=torch.uint8, device=dev)
+pk2 = stream.clone()
+t2 = []
+for r in range(int(os.environ.get("ROUNDS", 6)) * 3):
+    sw.count.zero_()
+    sw.frag.zero_()
+    pk2.copy_(stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    sw.process(pk2, acts2)
+    ops.apply_completed(pk2, acts2, V, 1, local, 16, 0.125, out=out2, acks=acks2)
+    e1.record()
+    torch.cuda.synchronize()
+    t2.append(e0.elapsed_time(e1) * 1e3)
+assert torch.equal(out2.view(torch.int32), vs[0]["out"].view(torch.int32))
+print(f"{'two calls':18s} switch, apply     {statistics.median(t2):7.1f} us")
