@@ -267,6 +267,27 @@ def unpack_nga(pkts: torch.Tensor, V: int, stride: int | None = None, with_value
     return f, vals
 
 
+def _check_apply(pkts, actions, V, local, out, acks):
+    """Sizes the C ABI cannot see (raw pointers): checked here so a short buffer is a
+    Python error, not an out-of-bounds device write."""
+    if pkts.dim() != 2:
+        raise ValueError("pkts must be [npkts, stride]")
+    if actions.numel() < pkts.shape[0]:
+        raise ValueError("actions must hold one byte per packet")
+    _req(out, torch.float32, "out")
+    if out.numel() != local.numel():
+        raise ValueError("out must have local's size")
+    tensors = [pkts, actions, local, out]
+    if acks is not None:
+        _req(acks, torch.uint8, "acks")
+        if acks.dim() != 2 or acks.shape[1] < 16:
+            raise ValueError("acks must be [rows, stride >= 16] (16-byte ack headers)")
+        if acks.shape[0] < -(-local.numel() // V):
+            raise ValueError("acks needs one row per slot: ceil(local.numel() / V) rows")
+        tensors.append(acks)
+    _same_device(*tensors)
+
+
 def apply_completed(pkts: torch.Tensor, actions: torch.Tensor, V: int, seq0: int,
                     local: torch.Tensor, k: int, weight_step: float, out=None, acks=None):
     """PS side after Switch.process: completed slots (actions == ACT_FWD_AGG) are decoded,
@@ -277,9 +298,9 @@ def apply_completed(pkts: torch.Tensor, actions: torch.Tensor, V: int, seq0: int
     _req(local, torch.float32, "local")
     npk, stride = pkts.shape
     out = torch.empty_like(local) if out is None else out
+    _check_apply(pkts, actions, V, local, out, acks)
     ack_ptr, ack_stride = None, 0
     if acks is not None:
-        _req(acks, torch.uint8, "acks")
         ack_ptr, ack_stride = acks.data_ptr(), acks.shape[1]
     check(load().ina_apply_completed_nga(pkts.data_ptr(), npk, V, stride, actions.data_ptr(),
                                          seq0 & 0xFFFFFFFF, local.data_ptr(), k, float(weight_step),
@@ -369,6 +390,10 @@ class Switch:
         _req(pkts, torch.uint8, "pkts")
         npk, stride = pkts.shape
         actions = torch.empty(npk, dtype=torch.uint8, device=pkts.device) if actions is None else actions
+        _req(actions, torch.uint8, "actions")
+        if actions.numel() < npk:
+            raise ValueError("actions must hold one byte per packet")
+        _same_device(pkts, actions)
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
@@ -389,11 +414,11 @@ class Switch:
         _req(local, torch.float32, "local")
         npk, stride = pkts.shape
         actions = torch.empty(npk, dtype=torch.uint8, device=pkts.device) if actions is None else actions
+        _req(actions, torch.uint8, "actions")
         out = torch.empty_like(local) if out is None else out
-        _req(out, torch.float32, "out")
+        _check_apply(pkts, actions, self.V, local, out, acks)
         ack_ptr, ack_stride = None, 0
         if acks is not None:
-            _req(acks, torch.uint8, "acks")
             ack_ptr, ack_stride = acks.data_ptr(), acks.shape[1]
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
         if self._scratch is None or self._scratch.numel() < need:

@@ -791,3 +791,26 @@ def test_switch_then_fused_apply_matches_oracle(V, W):
     ack_act = host(sw.process(acks))
     assert (ack_act == orc.ACT_FWD_ACK).all()
     assert not host(sw.frag).any()
+
+
+def test_apply_wrappers_refuse_short_buffers():
+    """Buffer sizes the C ABI cannot see are checked by the Python wrappers (a short ack
+    table or action array would otherwise be an out-of-bounds device write)."""
+    o = ops()
+    V, n = 32, 32 * 10
+    pk = torch.zeros((40, o.nga_stride(V)), dtype=torch.uint8, device=DEV)
+    act = torch.zeros(40, dtype=torch.uint8, device=DEV)
+    local = torch.zeros(n, device=DEV)
+    with pytest.raises(ValueError, match="one row per slot"):
+        o.apply_completed(pk, act, V, 1, local, 16, 0.5,
+                          acks=torch.zeros((9, o.nga_stride(V)), dtype=torch.uint8, device=DEV))
+    with pytest.raises(ValueError, match="one byte per packet"):
+        o.apply_completed(pk, act[:39], V, 1, local, 16, 0.5)
+    with pytest.raises(ValueError, match="local's size"):
+        o.apply_completed(pk, act, V, 1, local, 16, 0.5, out=torch.zeros(n - 1, device=DEV))
+    sw = o.Switch(V, num_slots=64, switch_id=1, device=DEV)
+    with pytest.raises(ValueError, match="one byte per packet"):
+        sw.process(pk, act[:39])
+    with pytest.raises(ValueError, match="one row per slot"):
+        sw.process_apply(pk, 1, local, 16, 0.5,
+                         acks=torch.zeros((9, o.nga_stride(V)), dtype=torch.uint8, device=DEV))
