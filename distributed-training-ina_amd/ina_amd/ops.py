@@ -40,6 +40,15 @@ def _req(t: torch.Tensor, dtype, name: str):
         raise ValueError(f"{name} must be contiguous")
 
 
+def _fits(out: torch.Tensor, numel: int, name: str = "out"):
+    """A caller-supplied output must hold what the kernel writes (the C ABI sees only a
+    pointer, so a short buffer would be an out-of-bounds device write)."""
+    if not isinstance(out, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if out.numel() < int(numel):
+        raise ValueError(f"{name} holds {out.numel()} elements, needs {int(numel)}")
+
+
 def _same_device(*ts):
     d = ts[0].device
     for t in ts[1:]:
@@ -56,6 +65,7 @@ def nga_stride(V: int) -> int:
 def quantize(x: torch.Tensor, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
     _req(x, torch.float32, "x")
     out = torch.empty(x.shape, dtype=torch.int32, device=x.device) if out is None else out
+    _fits(out, x.numel())
     _req(out, torch.int32, "out")
     check(load().ina_quantize_f32_i32(x.data_ptr(), out.data_ptr(), x.numel(), k, _stream(x)),
           "quantize")
@@ -65,8 +75,10 @@ def quantize(x: torch.Tensor, k: int, out: torch.Tensor | None = None) -> torch.
 def quantize_i16(x: torch.Tensor, k: int, V: int, out=None, overflow=None):
     _req(x, torch.float32, "x")
     out = torch.empty(x.shape, dtype=torch.int16, device=x.device) if out is None else out
+    _fits(out, x.numel())
     nslot = (x.numel() + V - 1) // V
     overflow = torch.empty(nslot, dtype=torch.uint8, device=x.device) if overflow is None else overflow
+    _fits(overflow, nslot, "overflow")
     _req(out, torch.int16, "out")
     _req(overflow, torch.uint8, "overflow")
     check(load().ina_quantize_f32_i16_sat(x.data_ptr(), out.data_ptr(), x.numel(), k, V,
@@ -76,6 +88,7 @@ def quantize_i16(x: torch.Tensor, k: int, V: int, out=None, overflow=None):
 
 def dequantize(s: torch.Tensor, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
     out = torch.empty(s.shape, dtype=torch.float32, device=s.device) if out is None else out
+    _fits(out, s.numel())
     _req(out, torch.float32, "out")
     if s.dtype == torch.int16:
         _req(s, torch.int16, "s")
@@ -107,6 +120,7 @@ def sum_reduce(bufs, out: torch.Tensor | None = None) -> torch.Tensor:
     """out[i] = sum_w bufs[w][i] mod 2^32 (int32), the switch's slot sum."""
     bufs, n = _bufs(bufs, torch.int32)
     out = torch.empty(n, dtype=torch.int32, device=bufs[0].device) if out is None else out
+    _fits(out, n)
     _req(out, torch.int32, "out")
     arr = ptr_array([b.data_ptr() for b in bufs])
     check(load().ina_sum_reduce_i32(arr, len(bufs), out.data_ptr(), n, _stream(out)), "sum_reduce")
@@ -129,6 +143,7 @@ def sum_reduce_host(bufs, out: torch.Tensor | None = None, chunk: int = 0,
         if b.is_cuda or b.dtype != torch.int32 or not b.is_contiguous() or b.numel() != n:
             raise ValueError(f"bufs[{i}] must be a contiguous host int32 tensor of {n} values")
     out = torch.empty(n, dtype=torch.int32).pin_memory() if out is None else out
+    _fits(out, n)
     if out.is_cuda or out.dtype != torch.int32 or not out.is_contiguous() or out.numel() != n:
         raise ValueError("out must be a contiguous host int32 tensor")
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -148,8 +163,12 @@ def sum_reduce_i16(bufs, V: int, out=None, overflow=None):
     bufs, n = _bufs(bufs, torch.int16)
     dev = bufs[0].device
     out = torch.empty(n, dtype=torch.int16, device=dev) if out is None else out
+    _fits(out, n)
     overflow = (torch.empty((n + V - 1) // V, dtype=torch.uint8, device=dev)
                 if overflow is None else overflow)
+    _req(out, torch.int16, "out")
+    _req(overflow, torch.uint8, "overflow")
+    _fits(overflow, (n + V - 1) // V, "overflow")
     arr = ptr_array([b.data_ptr() for b in bufs])
     check(load().ina_sum_reduce_i16_sat(arr, len(bufs), out.data_ptr(), n, V, overflow.data_ptr(),
                                         _stream(out)), "sum_reduce_i16")
@@ -159,6 +178,7 @@ def sum_reduce_i16(bufs, V: int, out=None, overflow=None):
 def quantize_reduce(bufs, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
     bufs, n = _bufs(bufs, torch.float32)
     out = torch.empty(n, dtype=torch.int32, device=bufs[0].device) if out is None else out
+    _fits(out, n)
     _req(out, torch.int32, "out")
     arr = ptr_array([b.data_ptr() for b in bufs])
     check(load().ina_quantize_reduce_f32_i32(arr, len(bufs), out.data_ptr(), n, k, _stream(out)),
@@ -170,8 +190,12 @@ def quantize_reduce_i16(bufs, k: int, V: int, out=None, overflow=None):
     bufs, n = _bufs(bufs, torch.float32)
     dev = bufs[0].device
     out = torch.empty(n, dtype=torch.int16, device=dev) if out is None else out
+    _fits(out, n)
     overflow = (torch.empty((n + V - 1) // V, dtype=torch.uint8, device=dev)
                 if overflow is None else overflow)
+    _req(out, torch.int16, "out")
+    _req(overflow, torch.uint8, "overflow")
+    _fits(overflow, (n + V - 1) // V, "overflow")
     arr = ptr_array([b.data_ptr() for b in bufs])
     check(load().ina_quantize_reduce_f32_i16_sat(arr, len(bufs), out.data_ptr(), n, k, V,
                                                  overflow.data_ptr(), _stream(out)),
@@ -187,6 +211,7 @@ def ps_combine(local: torch.Tensor, paras, weight_step: float, out=None) -> torc
     if n != local.numel():
         raise ValueError("local and paras differ in length")
     out = torch.empty_like(local) if out is None else out
+    _fits(out, local.numel())
     arr = ptr_array([p.data_ptr() for p in paras])
     check(load().ina_ps_combine_f32(local.data_ptr(), arr, len(paras), float(weight_step),
                                     out.data_ptr(), n, _stream(local)), "ps_combine")
@@ -198,6 +223,7 @@ def ps_apply(local: torch.Tensor, sum_int: torch.Tensor, k: int, weight_step: fl
     _req(local, torch.float32, "local")
     _req(sum_int, torch.int32, "sum_int")
     out = torch.empty_like(local) if out is None else out
+    _fits(out, local.numel())
     check(load().ina_ps_apply_i32(local.data_ptr(), sum_int.data_ptr(), k, float(weight_step),
                                   out.data_ptr(), local.numel(), _stream(local)), "ps_apply")
     return out
@@ -212,11 +238,13 @@ def pack_nga(vals: torch.Tensor, V: int, bitmap: int, count: int, switch_id: int
     stride = stride or nga_stride(V)
     npk = (vals.numel() + V - 1) // V
     out = torch.empty((npk, stride), dtype=torch.uint8, device=vals.device) if out is None else out
+    _fits(out, npk * stride)
     prm = _lib.NgaParams(bitmap & 0xFFFFFFFF, count & 0xFF, flags & 0xFF, switch_id & 0xFF, 0,
                          seq0 & 0xFFFFFFFF, num_slots, V)
     ovp = None
     if overflow is not None:
         _req(overflow, torch.uint8, "overflow")
+        _fits(overflow, npk, "overflow")
         ovp = overflow.data_ptr()
     check(load().ina_pack_nga(vals.data_ptr(), vals.numel(), C.byref(prm), ovp, out.data_ptr(),
                               stride, _stream(vals)), "pack_nga")
@@ -238,6 +266,7 @@ def quantize_pack_nga(x: torch.Tensor, k: int, V: int, bitmap: int, count: int, 
     stride = stride or nga_stride(V)
     npk = (x.numel() + V - 1) // V
     out = torch.empty((npk, stride), dtype=torch.uint8, device=x.device) if out is None else out
+    _fits(out, npk * stride)
     prm = _lib.NgaParams(bitmap & 0xFFFFFFFF, count & 0xFF, flags & 0xFF, switch_id & 0xFF, 0,
                          seq0 & 0xFFFFFFFF, num_slots, V)
     check(load().ina_quantize_pack_nga(x.data_ptr(), base.data_ptr() if base is not None else None,
@@ -298,6 +327,7 @@ def apply_completed(pkts: torch.Tensor, actions: torch.Tensor, V: int, seq0: int
     _req(local, torch.float32, "local")
     npk, stride = pkts.shape
     out = torch.empty_like(local) if out is None else out
+    _fits(out, local.numel())
     _check_apply(pkts, actions, V, local, out, acks)
     ack_ptr, ack_stride = None, 0
     if acks is not None:
@@ -320,6 +350,8 @@ def pack_c128(gradient: torch.Tensor, packet_num: int, worker_id: int, aggregato
         raise ValueError("gradient shorter than packet_num * 128")
     out = (torch.empty((packet_num, _lib.C128_BYTES), dtype=torch.uint8, device=gradient.device)
            if out is None else out)
+    _req(out, torch.uint8, "out")
+    _fits(out, packet_num * _lib.C128_BYTES)
     check(load().ina_pack_c128(gradient.data_ptr(), packet_num, worker_id,
                                aggregator_index & 0xFFFFFFFF, tensor_index, out.data_ptr(),
                                _stream(gradient)), "pack_c128")
@@ -345,6 +377,7 @@ def absmax(x: torch.Tensor, base: torch.Tensor | None = None, out: torch.Tensor 
             raise ValueError("base and x differ in length")
         _same_device(x, base)
     out = torch.empty(1, dtype=torch.float32, device=x.device) if out is None else out
+    _fits(out, 1)
     _req(out, torch.float32, "out")
     check(load().ina_absmax_f32(x.data_ptr(), base.data_ptr() if base is not None else None,
                                 x.numel(), out.data_ptr(), _stream(x)), "absmax")
@@ -416,6 +449,7 @@ class Switch:
         actions = torch.empty(npk, dtype=torch.uint8, device=pkts.device) if actions is None else actions
         _req(actions, torch.uint8, "actions")
         out = torch.empty_like(local) if out is None else out
+        _fits(out, local.numel())
         _check_apply(pkts, actions, self.V, local, out, acks)
         ack_ptr, ack_stride = None, 0
         if acks is not None:
@@ -449,6 +483,7 @@ def route_ipv4(actions: torch.Tensor, keys: torch.Tensor, ports: torch.Tensor,
         if dst_ip.numel() != actions.numel():
             raise ValueError("dst_ip must hold one address per packet")
     out = torch.empty(actions.numel(), dtype=torch.int32, device=actions.device) if out is None else out
+    _fits(out, actions.numel())
     _req(out, torch.int32, "out")
     _same_device(actions, keys, ports, out, *([dst_ip] if dst_ip is not None else []))
     check(load().ina_route_ipv4(actions.data_ptr(), None if dst_ip is None else dst_ip.data_ptr(),

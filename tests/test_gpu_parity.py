@@ -806,7 +806,7 @@ def test_apply_wrappers_refuse_short_buffers():
                           acks=torch.zeros((9, o.nga_stride(V)), dtype=torch.uint8, device=DEV))
     with pytest.raises(ValueError, match="one byte per packet"):
         o.apply_completed(pk, act[:39], V, 1, local, 16, 0.5)
-    with pytest.raises(ValueError, match="local's size"):
+    with pytest.raises(ValueError, match="local's size|needs"):
         o.apply_completed(pk, act, V, 1, local, 16, 0.5, out=torch.zeros(n - 1, device=DEV))
     sw = o.Switch(V, num_slots=64, switch_id=1, device=DEV)
     with pytest.raises(ValueError, match="one byte per packet"):
