@@ -96,7 +96,7 @@ def run_extra(dev):
                 t = _time(lambda: ops.sum_reduce(b3, out=o3))
                 sweep.append(_row("sum_reduce_i32 W=8", t, (W3 + 1) * n3 * 4, nt=nt, unroll=unroll,
                                   max_blocks=blocks))
-    ops.set_tuning(reduce_blocks=0, unroll=4, nontemporal=True)
+    ops.set_tuning(reduce_blocks=0, unroll=0, nontemporal=True)   # back to the automatic geometry
     rows.append(max(sweep, key=lambda r: r["GB/s"]) | {"note": "best of sweep"})
     for W in (2, 4, 16):
         bw = [rnd_i32(n3) for _ in range(W)] if W != 16 else b3 + [rnd_i32(n3) for _ in range(8)]

@@ -60,7 +60,7 @@ static std::atomic<int> g_max_blocks{16384};  // default-cap kernels (C4 int16 f
 // interleaved A/B): 4 x 16 B per worker per thread in flight and 64*W 256-thread
 // workgroups (W = 2, 4: 256; W = 8: 512; W = 16: 1024).  0 = that rule; >0 overrides.
 static std::atomic<int> g_reduce_blocks{0};
-static std::atomic<int> g_unroll{4};
+static std::atomic<int> g_unroll{0};   // 0 = per-W choice (launch_reduce_u)
 // 16-byte chunks in flight per thread in the one-in one-out elementwise kernels
 // (quantise, dequantise, PS apply): one, with the 8192-workgroup grid striding, beat 2
 // and 4 -- quantise 40.9 -> 37.6 us, dequantise 41.2 -> 36.8 (tools/lab/ew_lab.py)
@@ -305,7 +305,10 @@ template <int W, int U>
 static void launch_reduce_w(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
                             hipStream_t s) {
     int cap = g_reduce_blocks.load();
-    if (cap <= 0) cap = W * 64 < 256 ? 256 : (W * 64 > 1024 ? 1024 : W * 64);
+    // 64 workgroups per worker stream, clamped to [256, 1024] -- except W = 16 (768: 3 per
+    // CU beat 4, 278.8 vs 300.2 us) and W = 2 with one chunk (512); tools/lab/reduce_w_sweep.py
+    if (cap <= 0)
+        cap = W == 16 ? 768 : (W == 2 && U == 1) ? 512 : (W * 64 < 256 ? 256 : (W * 64 > 1024 ? 1024 : W * 64));
     unsigned g = grid_for(n4, U, cap);
     if (g_nontemporal.load())
         hipLaunchKernelGGL((k_sum_reduce_i32_vec<W, U, true>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
@@ -316,7 +319,9 @@ static void launch_reduce_w(const PtrPack<int32_t>& pk, int32_t* out, size_t n4,
 template <int W>
 static void launch_reduce_u(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
                             hipStream_t s) {
-    switch (g_unroll.load()) {
+    int u = g_unroll.load();
+    if (u == 0) u = W <= 4 ? 1 : 4;   // auto: 1 chunk per stream for W <= 4 (86.5 vs 90.4 us at W = 4)
+    switch (u) {
         case 1: launch_reduce_w<W, 1>(pk, out, n4, n, s); break;
         case 2: launch_reduce_w<W, 2>(pk, out, n4, n, s); break;
         default: launch_reduce_w<W, 4>(pk, out, n4, n, s); break;
@@ -1365,7 +1370,7 @@ const char* ina_last_error_string(void) { return g_err; }
 int ina_set_tuning(int key, int value) {
     switch (key) {
         case 0: if (value < 1) return INA_EINVAL; g_max_blocks = value; return INA_OK;
-        case 1: if (value != 1 && value != 2 && value != 4) return INA_EINVAL; g_unroll = value; return INA_OK;
+        case 1: if (value != 0 && value != 1 && value != 2 && value != 4) return INA_EINVAL; g_unroll = value; return INA_OK;
         case 2: g_nontemporal = value ? 1 : 0; return INA_OK;
         case 3: if (value < 0) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
         case 4: if (value < 1) return INA_EINVAL; g_stream_blocks = value; return INA_OK;

@@ -63,7 +63,7 @@ const char* ina_version(void);
 const char* ina_last_error_string(void);
 
 /* Launch-geometry knobs (process-wide; results never change, only speed).  Keys:
- * 0 elementwise grid cap, 1 reduce chunks per worker per thread (1/2/4), 2 reduce
+ * 0 elementwise grid cap, 1 reduce chunks per worker per thread (0 = per-W auto, 1/2/4), 2 reduce
  * non-temporal loads/stores (0/1), 3 reduce grid (0 = 64*W rule), 4 chunk-loop grid,
  * 5 fp32 PS-combine grid, 6 INA PS-combine grid, 7 host-ingest H2D streams (1/2),
  * 8 16-byte chunks per flat packet-kernel launch, 9 switch one-workgroup small-batch

@@ -84,7 +84,7 @@ def test_sum_reduce_stacked_tensor_input():
     assert np.array_equal(got, orc.sum_reduce_i32(list(stack)))
 
 
-@pytest.mark.parametrize("unroll,blocks,nt", [(1, 2048, True), (4, 512, True), (2, 4096, False)])
+@pytest.mark.parametrize("unroll,blocks,nt", [(1, 2048, True), (4, 512, True), (2, 4096, False), (0, 0, True)])
 def test_sum_reduce_tunings_identical(unroll, blocks, nt):
     rng = np.random.default_rng(8)
     bufs = [rand_i32(rng, 300007) for _ in range(8)]
@@ -93,7 +93,7 @@ def test_sum_reduce_tunings_identical(unroll, blocks, nt):
         o.set_tuning(reduce_blocks=blocks, unroll=unroll, nontemporal=nt)
         got = host(o.sum_reduce([dev(b) for b in bufs]))
     finally:
-        o.set_tuning(max_blocks=8192, unroll=4, nontemporal=True, reduce_blocks=0)
+        o.set_tuning(max_blocks=16384, unroll=0, nontemporal=True, reduce_blocks=0)   # library defaults
     assert np.array_equal(got, orc.sum_reduce_i32(bufs))
 
 
