@@ -179,6 +179,21 @@ def run_sharded(args, rank, world, dev):
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     shard_bytes = agg.plan.shard * 4
+    # spot check: the first 64 Ki aggregated values == dequantise(sum over ranks of
+    # quantise(bucket)), the per-rank quantised prefixes exchanged with an all-gather
+    from ina_amd import ops
+    m = min(n, 1 << 16)
+    out = agg(bucket)[:m]
+    qp = ops.quantize(bucket[:m].contiguous(), 16)
+    if world > 1:
+        import torch.distributed as dist
+        allq = torch.empty(world * m, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(allq, qp)
+        qsum = (allq.view(world, m).to(torch.int64).sum(0) & 0xFFFFFFFF)
+        qsum = torch.where(qsum >= (1 << 31), qsum - (1 << 32), qsum).to(torch.int32)
+    else:
+        qsum = qp
+    parity = bool(torch.equal(out, ops.dequantize(qsum.contiguous(), 16)))
     return {
         "metric": "aggregated-gradient GB/s (config 5: 1 GiB fp32 bucket per rank, sharded RCCL)",
         "value": round(world * n * 4 * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
@@ -189,6 +204,7 @@ def run_sharded(args, rank, world, dev):
                                "reduce_scatter(int32,SUM) -> dequantise -> all_gather(fp32)",
                    "values_per_worker": n, "workers": world, "shard_values": agg.plan.shard,
                    "parallelism": f"RCCL x {world}"},
+        "parity_spot_check": parity,
         "xgmi": {"rs_bytes_per_rank": (world - 1) * shard_bytes,
                  "ag_bytes_per_rank": (world - 1) * shard_bytes},
     }

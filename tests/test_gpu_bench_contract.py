@@ -32,3 +32,16 @@ def test_bench_json_line_contract():
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
     assert cb["matches_gpu"] is True
     assert "workload" in d["config"]
+
+
+@pytest.mark.gpu
+def test_bench_sharded_mode_line():
+    """Config-5 mode on one GPU (the collectives are identities): a JSON line whose
+    aggregate passes its own parity spot check."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--mode", "sharded", "--steps", "2",
+                        "--warmup", "1", "--values", str(1 << 22)],
+                       cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity_spot_check"] is True
+    assert d["config"]["values_per_worker"] == 1 << 22
