@@ -1,0 +1,33 @@
+"""Profile target: the one-GPU INA packet path in steady state with the PS step fused into
+the switch pass (8 x fused worker quantise+pack, one ina_switch_process_apply over
+[last step's acks | 8 x 102,400 NGA-256 packets]); run under rocprofv3 --kernel-trace
+--stats for the per-kernel breakdown of bench_extra's last packet-path row."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "distributed-training-ina_amd"))
+from ina_amd import ops  # noqa: E402
+
+n, W, V, slots = 26_214_400, 8, 256, 1 << 17
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(3)
+xs = [torch.randn(n, device=dev, generator=g) * 1e-2 for _ in range(W)]
+params = torch.randn(n, device=dev, generator=g)
+npk = n // V
+stride = ops.nga_stride(V)
+batch = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=dev)
+acks, rows = batch[:npk], batch[npk:].view(W, npk, stride)
+acts = torch.empty((W + 1) * npk, dtype=torch.uint8, device=dev)
+out = torch.empty_like(params)
+sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
+for step in range(int(os.environ.get("STEPS", 6))):
+    for w in range(W):
+        ops.quantize_pack_nga(xs[w], 16, V, w + 1, W, 1, 1, base=params, num_slots=slots, out=rows[w])
+    sw.process_apply(batch, 1, params, 16, 1.0 / (W + 1), out=out, acks=acks, keep_forwarded=False,
+                     actions=acts)
+torch.cuda.synchronize()
+assert int((acts[npk:] == 1).sum()) == npk and bool((acts[:npk] == 3).all())
+print("done", batch.shape)
