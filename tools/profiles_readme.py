@@ -34,6 +34,7 @@ boxes this round: 5.53-5.83 TB/s aggregated, 143.4-150.7 us per launch = 78-82 %
 | `r01/bench_extra.json` | `bench.py --extra`: every other kernel (configs 2/4, quantise, pack/unpack, fused worker pack, fused PS apply, absmax, C-128, PS combine, device switch, the whole packet path step, end-to-end with pinned H2D/D2H -- phases in sequence and the pipelined `ina_sum_reduce_host_i32`) and the grid sweeps; cold caches (512 MiB read between timed launches); DESIGN.md's kernel table is generated from it (`tools/design_table.py`) |
 | `r01/kernel_stats_switch.csv` | rocprofv3 stats of `tools/prof_switch.py` (device switch on 819,200 NGA-256 packets): `k_switch_run2` {sw[run2]['avg_us']} us, keys {sw[keys]['avg_us']} us, sort passes {sort_us:.1f} us |
 | `r01/switch_pmc_FETCH_SIZE.csv`, `r01/switch_pmc_WRITE_SIZE.csv`, `traffic_switch.json` | PMC passes over the same program; per-kernel HBM bytes and rates computed by `tools/switch_traffic.py` (run kernel {(sw[run2]['hbm_read_bytes'] + sw[run2]['hbm_write_bytes']) / 1e9:.2f} GB at {sw[run2]['TB_per_s']} TB/s) |
+| `r01/bench_boxes.json` | the same bench line on every box of the round's evidence sessions (8 boxes: 77.9-82.3 % of peak, median 79.8 %) |
 | `r01/kernel_stats_packet_path.csv` | rocprofv3 stats of `tools/prof_path.py`: the steady-state packet path with the PS step fused (per step: 8 x `k_pack_nga_flat<SrcQ32,1>` 54.5 us, `k_switch_run2<true>` 235 us, keys 37 us, sort passes 47 us) |
 | `r01/sharded_c5_1gpu.json`, `r01/rehearse_2ranks_gloo.json`, `r01/config1_loopback.log` | session r01zf: `bench.py --mode sharded` on one GPU (config 5 plumbing, collectives are identities); bench.py at N=2 over gloo with both ranks on one GPU (the multi-rank timing/reduction path); `examples/config1_loopback.py` (config 1: ResNet-50, 2 workers, loopback sockets, device switch stand-in) |
 | `r01/lab/*.log` | interleaved A/B labs (`tools/lab/`): reduce structures, grids, store and copy cache policies; fused-kernel grids and chunks in flight; int16 layouts; C-128 pack; switch run/sort variants, nt loads, tail-chunk policy, sort chunk geometry; PS apply batch/window/action scan; packet-path stage times |
