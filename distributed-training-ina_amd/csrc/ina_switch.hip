@@ -1011,6 +1011,10 @@ int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t
     if (acks && (((uintptr_t)acks & 15u) || ack_stride % 16))
         return set_error(INA_EINVAL, "ack rows must be 16-byte aligned%s", "");
     if (!st || st->V <= 0) return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
+    // the PS step needs the layout ina_apply_completed_nga takes; refuse before the switch
+    // touches its state rather than after
+    if (st->V % 4 || st->V > 256 || stride % 16 || ((uintptr_t)pkts & 15u))
+        return set_error(INA_EINVAL, "process_apply needs V %% 4 == 0 <= 256 and 16-byte aligned rows%s", "");
     const size_t nslots = (n + (size_t)st->V - 1) / (size_t)st->V;
     PsFuse ps{local, out, n, ldexpf(1.0f, -k), (float)weight_step, seq0,
               nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,
