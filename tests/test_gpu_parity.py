@@ -814,3 +814,31 @@ def test_apply_wrappers_refuse_short_buffers():
     with pytest.raises(ValueError, match="one row per slot"):
         sw.process_apply(pk, 1, local, 16, 0.5,
                          acks=torch.zeros((9, o.nga_stride(V)), dtype=torch.uint8, device=DEV))
+
+
+def test_sum_reduce_host_concurrent_threads():
+    """ina_sum_reduce_host_i32 from several host threads at once (thread-local copy
+    streams and ring events, one scratch per caller): every result exact."""
+    import threading
+    o = ops()
+    rng = np.random.default_rng(21)
+    jobs = []
+    for t in range(3):
+        W, n = 3 + t, 1_000_003 + 17 * t
+        bufs = [torch.from_numpy(rand_i32(rng, n)).pin_memory() for _ in range(W)]
+        jobs.append((bufs, orc.sum_reduce_i32([b.numpy() for b in bufs])))
+    results, errors = [None] * len(jobs), []
+
+    def work(i):
+        try:
+            results[i] = o.sum_reduce_host(jobs[i][0], chunk=1 << 18).numpy().copy()
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errors.append(e)
+    threads = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(60)
+    assert not errors, errors
+    for (bufs, want), got in zip(jobs, results):
+        assert got is not None and np.array_equal(got, want)
