@@ -9,9 +9,23 @@ aggregate -- the work the Tofino's Processor registers do per slot
 (processor.p4:14-24).  value = W * n * 4 bytes * steps * ranks / max-rank time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU; each rank
-      aggregates its own bucket: slot ranges shard with no data-path collective,
-      "scaling": "weak")
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts N ranks
+itself (torch.distributed.run, 127.0.0.1, one rank per GPU) before anything
+touches the GPU; under an external torchrun it runs as one of those ranks.  Every
+rank asserts that the process group holds exactly N ranks (backend nccl = RCCL).
+
+Multi-GPU:
+  * headline, "scaling": "weak" -- the switch aggregates every slot independently
+    (ngaa.p4:87-168), so N GPUs aggregate N config-3 slot ranges (rank r owns
+    slots [r*102400, (r+1)*102400) of an N x 100 MiB job) with no data-path
+    collective: a 100 MiB bucket never outgrows one GPU, and the north star
+    shards over xGMI only when one does;
+  * "sharded_c5" -- in the same run, every rank times config 5 through RCCL:
+    a 1 GiB fp32 bucket per rank, quantise -> reduce_scatter(int32, SUM) ->
+    dequantise -> all_gather(fp32) (ina_amd.dist.ShardedAggregator), with per-
+    phase times, the xGMI bytes per rank and a parity check of the aggregate.
+  --mode sharded makes config 5 the headline line instead.
 
 Extra rows (not the headline): --extra writes per-kernel timings of the other
 configs (fused quantise+reduce C2, int16 C4, pack/unpack, PS combine, end-to-end
@@ -22,7 +36,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -37,11 +53,12 @@ METRIC = "aggregated-gradient GB/s (device-resident), 8-worker×100 MB int32 sum
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 W_WORKERS = 8
 N_VALUES = 26_214_400        # 100 MiB of int32 per worker (config 3)
+C5_VALUES = 268_435_456      # 1 GiB of fp32 per worker (config 5)
 V_SLOT = 256
 ROTATE = 2                   # input sets alternated per step (943 MB each > 256 MB MALL)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -51,51 +68,98 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=N_VALUES,
                     help="values per worker in the CPU-baseline sample (default: the whole "
-                         "config-3 bucket, ~2-4 s of host work)")
+                         "config-3 bucket)")
     ap.add_argument("--extra", action="store_true")
     ap.add_argument("--mode", choices=("reduce", "sharded"), default="reduce",
-                    help="reduce: the headline (config 3); sharded: config 5, one 1 GiB fp32 "
-                         "bucket per rank aggregated with quantise -> RCCL reduce-scatter -> "
-                         "dequantise -> all-gather")
+                    help="reduce: the headline (config 3); sharded: config 5 as the headline, "
+                         "one 1 GiB fp32 bucket per rank aggregated with quantise -> RCCL "
+                         "reduce-scatter -> dequantise -> all-gather")
+    ap.add_argument("--c5-values", type=int, default=C5_VALUES,
+                    help="fp32 values per rank of the config-5 measurement")
+    ap.add_argument("--c5-steps", type=int, default=10)
+    ap.add_argument("--wire", choices=("i32", "i16"), default="i32",
+                    help="config-5 wire: int32, or the int16 saturating wire (config 4 rule)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 sub-measurement")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="launcher self-check: start the ranks, form the group, assert its size, "
+                         "print one JSON line; no GPU work (runs on CPU with gloo)")
     ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "traffic_sum_reduce_c3.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 BACKEND = os.environ.get("INA_BENCH_BACKEND", "nccl")   # "gloo": rehearse N>1 on one GPU
+
+
+# -- launching and the process group ----------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks with torch.distributed.run as
+    child processes.  This process never initialises the GPU (nothing above touched
+    torch.cuda), and it waits for the ranks and exits with their status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, cwd=REPO).returncode
 
 
 def init_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if BACKEND == "gloo":
-        local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    use_gpu = not args.check_launch
+    if use_gpu:
+        if BACKEND == "gloo":
+            local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+    backend = "none"
     if world > 1:
         import torch.distributed as dist
-        if BACKEND == "nccl":
+        backend = BACKEND if use_gpu else "gloo"
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
-            dist.init_process_group(BACKEND)
-    return rank, world, local
+            dist.init_process_group(backend)
+        got = dist.get_world_size()
+        if got != args.gpus:
+            raise SystemExit(f"bench.py: process group holds {got} ranks, expected {args.gpus}")
+        backend = dist.get_backend()
+    return rank, world, local, backend
 
 
-def barrier(world):
+def barrier(world, gpu=True):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
-    torch.cuda.synchronize()
+    if gpu:
+        torch.cuda.synchronize()
 
 
-def max_over_ranks(x: float, world: int) -> float:
+def reduce_over_ranks(x: float, world: int, op: str = "max") -> float:
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda" if BACKEND == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dev = "cuda" if BACKEND == "nccl" and torch.cuda.is_available() else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
     return float(t.item())
 
 
+def max_over_ranks(x: float, world: int) -> float:
+    return reduce_over_ranks(x, world, "max")
+
+
+def all_ranks_true(ok: bool, world: int) -> bool:
+    return reduce_over_ranks(1.0 if ok else 0.0, world, "min") == 1.0
+
+
+# -- inputs --------------------------------------------------------------------------------
 def make_inputs(W, n, seed_base, dev):
     g = torch.Generator(device=dev)
     bufs = []
@@ -116,115 +180,205 @@ def load_traffic(path, W, n):
     return None
 
 
+# -- CPU baseline ----------------------------------------------------------------------------
+def cgroup_cpus():
+    """CPUs the cgroup quota grants (cpu.max), or None when unlimited/unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return round(int(q) / int(p), 2)
+    except Exception:
+        pass
+    return None
+
+
+def _median_of_10(fn):
+    ts = []
+    out = None
+    for it in range(13):             # 3 warm-up runs, median of 10 (SURVEY 8d)
+        out, secs = fn()
+        if it >= 3:
+            ts.append(secs)
+    return statistics.median(ts), out
+
+
 def cpu_baseline(args, bufs_host, gpu_out_sample):
+    """the reference's CPU path (packetise + P4 aggregator restatement) on the
+    host's cores, threads split as communicator.py:133-157, at 1 thread, at every core of
+    the affinity mask, and at the CPU count the cgroup quota grants (and twice that);
+    `value` is the best of them and `cores` the thread count that reached it.  Plus torch's
+    float aggregate() (launch.py:42-52) at that thread count."""
     from oracle import oracle as orc
     n = bufs_host[0].size
-    cores = len(os.sched_getaffinity(0))
-    threads = max(1, min(cores, 16))
-    res = {}
-    for P in sorted({1, threads}):
-        ts = []
-        out = None
-        for it in range(13):             # 3 warm-up runs, median of 10
-            out, secs = orc.cpu_packetise_aggregate(bufs_host, V_SLOT, P)
-            if it >= 3:
-                ts.append(secs)
-        res[P] = (statistics.median(ts), out)
-    tP, outP = res[threads]
-    t1, _ = res[1]
     W = len(bufs_host)
-    ok = bool(np.array_equal(outP, gpu_out_sample))
-    # the PS's own float update, aggregate() as launch.py:42-52 writes it, in torch on the
-    # same host cores over fp32 buffers of the same sample size
-    torch.set_num_threads(threads)
+    cores = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    counts = {1, cores}
+    if quota:
+        q = max(1, int(quota))
+        counts |= {min(q, cores), min(2 * q, cores)}
+    counts = sorted(counts)
+    res = {}
+    for P in counts:
+        res[P] = _median_of_10(lambda: orc.cpu_packetise_aggregate(bufs_host, V_SLOT, P))
+    best = min(counts, key=lambda P: res[P][0])
+    tP, outP = res[best]
+    ok = all(bool(np.array_equal(res[P][1], gpu_out_sample)) for P in counts)
+    # the PS's own float update, aggregate() as launch.py:42-52 writes it, in torch over
+    # fp32 buffers of the same sample size
+    torch.set_num_threads(best)
     g = torch.Generator().manual_seed(7)
     paras = [torch.randn(n, generator=g) * 1e-2 for _ in range(W)]
     local = torch.randn(n, generator=g)
-    ta = []
-    for _ in range(3):
+
+    def agg_once():
+        nonlocal local
         t0 = time.perf_counter()
         local += (1.0 / (W + 1)) * 1.0 * sum([p - local for p in paras])
-        ta.append(time.perf_counter() - t0)
-    t_agg = statistics.median(ta)
+        return None, time.perf_counter() - t0
+    t_agg, _ = _median_of_10(agg_once)
     part = "the whole" if n == N_VALUES else f"first {n * 4 // (1 << 20)} MiB of each"
+    gbs = {P: round(W * n * 4 / res[P][0] / 1e9, 3) for P in counts}
     return {
-        "value": round(W * n * 4 / tP / 1e9, 3), "unit": "GB/s", "cores": threads,
+        "value": gbs[best], "unit": "GB/s", "cores": best,
         "kind": "port",
         "sample": (f"{W} workers x {n} int32 ({part} config-3 "
                    f"bucket): NGA-{V_SLOT} packetise (header + memcpy + htonl per packet, "
                    f"communicator.cc:23-37) -> P4 aggregator restatement (count/frag/Processor "
-                   f"registers, ngaa.p4:120-196) -> PS ack, 3 warm-up runs then median of 10, {threads} threads split "
-                   f"as communicator.py:133-157"),
-        "value_1core": round(W * n * 4 / t1 / 1e9, 3),
+                   f"registers, ngaa.p4:120-196) -> PS ack, 3 warm-up runs then median of 10, "
+                   f"threads split as communicator.py:133-157; timed at {counts} threads "
+                   f"(affinity mask {cores} CPUs, cgroup quota {quota} CPUs), best = {best}"),
+        "value_1core": gbs[1],
+        "value_all_affinity_cores": gbs[cores],
+        "value_by_threads": {str(P): v for P, v in gbs.items()},
+        "cgroup_cpu_quota": quota,
         "torch_aggregate_GBps": round(W * n * 4 / t_agg / 1e9, 3),
+        "torch_aggregate_threads": best,
         "affinity_cores": cores,
         "matches_gpu": ok,
     }
 
 
-def run_sharded(args, rank, world, dev):
-    """Config 5: every rank is one worker with an n-value fp32 bucket (default 1 GiB)."""
-    from ina_amd.dist import ShardedAggregator
-    n = args.values if args.values != N_VALUES else 268_435_456
+# -- config 5: sharded over RCCL --------------------------------------------------------------
+def measure_c5(args, rank, world, dev, warmup=2):
+    """quantise -> reduce_scatter(int32, SUM) -> dequantise -> all_gather(fp32) of one
+    n-value fp32 bucket per rank; per-phase HIP-event times on the launch stream."""
+    from ina_amd import ops
+    from ina_amd.dist import ShardedAggregator, all_gather_shards, reduce_scatter_sum
+    n = args.c5_values
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     bucket = torch.randn(n, device=dev, generator=g) * 1e-2
-    agg = ShardedAggregator(n, k=16, device=dev)
-    for _ in range(args.warmup):
+    k = 16 if args.wire == "i32" else 20
+    agg = ShardedAggregator(n, k=k, device=dev, wire=args.wire, V=V_SLOT)
+    for _ in range(warmup):
         agg(bucket)
+    steps = args.c5_steps
+    stream = torch.cuda.current_stream(dev)
     barrier(world)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         agg(bucket)
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    shard_bytes = agg.plan.shard * 4
-    # spot check: the first 64 Ki aggregated values == dequantise(sum over ranks of
-    # quantise(bucket)), the per-rank quantised prefixes exchanged with an all-gather
-    from ina_amd import ops
+
+    # per-phase breakdown (one more pass, events between the phases)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    barrier(world)
+    ev[0].record(stream)
+    agg._quantize(bucket)
+    ev[1].record(stream)
+    if world > 1:
+        reduce_scatter_sum(agg.q, agg.plan, agg.group, out=agg.sum_shard)
+    ev[2].record(stream)
+    src = agg.sum_shard if world > 1 else agg.q
+    dst = agg.f_shard if world > 1 else agg.full
+    ovf = (agg.ovf_shard if world > 1 else agg.ovf_full) if args.wire == "i16" else None
+    agg._decode(src, dst, ovf)
+    ev[3].record(stream)
+    if world > 1:
+        all_gather_shards(agg.f_shard, agg.plan, agg.group, out=agg.full)
+        if ovf is not None:
+            all_gather_shards(agg.ovf_shard, agg.plan, agg.group, out=agg.ovf_full)
+    ev[4].record(stream)
+    torch.cuda.synchronize()
+    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(4)]
+
+    # parity: the aggregate's first 64 Ki values == decode(sum over ranks of the
+    # per-rank wire of those values), the per-rank wires all-gathered
     m = min(n, 1 << 16)
-    out = agg(bucket)[:m]
-    qp = ops.quantize(bucket[:m].contiguous(), 16)
+    out = agg(bucket)[:m].clone()
+    head = bucket[:m].contiguous()
+    wp = ops.quantize(head, k) if args.wire == "i32" else ops.quantize_i16_wire(head, k)
     if world > 1:
         import torch.distributed as dist
-        allq = torch.empty(world * m, dtype=torch.int32, device=dev)
-        dist.all_gather_into_tensor(allq, qp)
-        qsum = (allq.view(world, m).to(torch.int64).sum(0) & 0xFFFFFFFF)
-        qsum = torch.where(qsum >= (1 << 31), qsum - (1 << 32), qsum).to(torch.int32)
+        from ina_amd.dist import ShardPlan
+        allw = all_gather_shards(wp, ShardPlan(m * world, world, align=m))
+        wsum = allw.view(world, m).to(torch.int64).sum(0)
+        wsum = ((wsum + (1 << 31)) % (1 << 32) - (1 << 31)).to(torch.int32)
     else:
-        qsum = qp
-    parity = bool(torch.equal(out, ops.dequantize(qsum.contiguous(), 16)))
+        wsum = wp
+    if args.wire == "i32":
+        want = ops.dequantize(wsum.contiguous(), k)
+    else:
+        _, want, _ = ops.i16_wire_finish(wsum.contiguous(), k, V_SLOT, want_out16=False)
+    parity = all_ranks_true(bool(torch.equal(out, want)), world)
+
+    G = world
+    S = agg.plan.padded * 4
+    xgmi = (G - 1) * S // G
+    t_step = elapsed / steps
     return {
-        "metric": "aggregated-gradient GB/s (config 5: 1 GiB fp32 bucket per rank, sharded RCCL)",
-        "value": round(world * n * 4 * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-        "config": {"workload": "C5: 1 GiB fp32 bucket per worker, quantise k=16 -> "
-                               "reduce_scatter(int32,SUM) -> dequantise -> all_gather(fp32)",
-                   "values_per_worker": n, "workers": world, "shard_values": agg.plan.shard,
-                   "parallelism": f"RCCL x {world}"},
+        "value": round(world * n * 4 * steps / elapsed / 1e9, 2), "unit": "GB/s",
+        "metric": "aggregated-gradient GB/s (config 5: fp32 bucket per rank, sharded over RCCL)",
+        "ms_per_step": round(t_step * 1e3, 3), "steps": steps, "warmup": warmup,
+        "workload": (f"C5: {n} fp32 values ({n * 4 / 2 ** 30:.2f} GiB) per rank, quantise "
+                     f"({args.wire} wire, k={k}) -> reduce_scatter(int32, SUM) -> "
+                     f"{'dequantise' if args.wire == 'i32' else 'saturate once + dequantise'}"
+                     f" -> all_gather(fp32)"),
+        "values_per_rank": n, "shard_values": agg.plan.shard, "rccl_world": world,
+        "phase_ms": {"quantize": round(phase[0] * 1e3, 3), "reduce_scatter": round(phase[1] * 1e3, 3),
+                     "decode": round(phase[2] * 1e3, 3), "all_gather": round(phase[3] * 1e3, 3)},
+        "xgmi": {"rs_send_bytes_per_rank": xgmi, "ag_recv_bytes_per_rank": xgmi,
+                 "rs_busbw_GBps": round(xgmi / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None,
+                 "ag_busbw_GBps": round(xgmi / phase[3] / 1e9, 1) if world > 1 and phase[3] > 0 else None},
         "parity_spot_check": parity,
-        "xgmi": {"rs_bytes_per_rank": (world - 1) * shard_bytes,
-                 "ag_bytes_per_rank": (world - 1) * shard_bytes},
     }
 
 
-def main():
-    args = parse()
-    rank, world, local = init_dist(args)
-    dev = torch.device(f"cuda:{local}")
-    from ina_amd import ops
-    if args.mode == "sharded":
-        line = run_sharded(args, rank, world, dev)
-        if rank == 0:
-            print(json.dumps(line), flush=True)
-        if world > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
-        return
+# -- modes ---------------------------------------------------------------------------------------
+def run_check_launch(args, rank, world, backend):
+    import torch.distributed as dist
+    ranks = [rank]
+    if world > 1:
+        got = [None] * world
+        dist.all_gather_object(got, rank)
+        ranks = got
+    if rank == 0:
+        print(json.dumps({"check_launch": True, "n_gpus": world, "rccl_world": world,
+                          "backend": backend, "ranks": ranks}), flush=True)
 
+
+def run_sharded_headline(args, rank, world, dev, backend):
+    c5 = measure_c5(args, rank, world, dev)
+    return {
+        "metric": c5["metric"], "value": c5["value"], "unit": "GB/s",
+        "n_gpus": world, "steps": c5["steps"], "warmup": c5["warmup"],
+        "ms_per_step": c5["ms_per_step"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": c5["workload"], "values_per_worker": c5["values_per_rank"],
+                   "workers": world, "shard_values": c5["shard_values"],
+                   "parallelism": f"RCCL x {world}"},
+        "rccl_world": world, "backend": backend,
+        "phase_ms": c5["phase_ms"], "xgmi": c5["xgmi"],
+        "parity_spot_check": c5["parity_spot_check"],
+    }
+
+
+def run_reduce(args, rank, world, dev, backend):
+    from ina_amd import ops
     W, n = args.workers, args.values
+    # rank r owns slot range r of an N-bucket job: its own inputs (seeds per rank)
     sets = [make_inputs(W, n, 1000 + 100 * (rank * ROTATE + r), dev) for r in range(ROTATE)]
     outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(ROTATE)]
     torch.cuda.synchronize()
@@ -252,13 +406,15 @@ def main():
     want = np.zeros(check_n, np.uint32)
     for b in sets[last]:
         want += b[:check_n].cpu().numpy().view(np.uint32)
-    parity = bool(np.array_equal(outs[last][:check_n].cpu().numpy().view(np.uint32), want))
+    parity = all_ranks_true(
+        bool(np.array_equal(outs[last][:check_n].cpu().numpy().view(np.uint32), want)), world)
 
     worker_bytes = W * n * 4
     algo_bytes = (W + 1) * n * 4
     value = worker_bytes * args.steps * world / elapsed / 1e9
     achieved = algo_bytes / avg_launch_s / 1e9
     traffic = load_traffic(args.traffic_file, W, n)
+    slots = (n + V_SLOT - 1) // V_SLOT
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -274,8 +430,13 @@ def main():
         "data": "synthetic (int32 uniform in [-2^20, 2^20), torch generator seed 1000+w per worker)",
         "config": {"workload": "C3: 8 workers x 100 MiB int32 (26,214,400 values), V=256 slots",
                    "workers": W, "values_per_worker": n, "slot_values": V_SLOT,
-                   "slots": (n + V_SLOT - 1) // V_SLOT,
-                   "parallelism": f"slot-range shards, one bucket per rank x {world}"},
+                   "slots": slots,
+                   "parallelism": (f"slot-range shards: rank r aggregates slots "
+                                   f"[r*{slots}, (r+1)*{slots}) of a {world}-bucket job, "
+                                   f"no data-path collective; {world} rank(s)")},
+        "rccl_world": world,
+        "backend": backend,
+        "devices_visible": torch.cuda.device_count(),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
@@ -288,16 +449,38 @@ def main():
         s = min(args.cpu_sample, n)
         host = [b[:s].cpu().numpy() for b in sets[last]]
         line["cpu_baseline"] = cpu_baseline(args, host, outs[last][:s].cpu().numpy())
-    if rank == 0 and args.extra:
-        from bench_extra import run_extra
-        extra = run_extra(dev)
-        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-        json.dump(extra, open(os.path.join(REPO, "gpurun_out", "bench_extra.json"), "w"), indent=1)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    del sets, outs
+    torch.cuda.empty_cache()
+    if not args.no_c5:
+        line["sharded_c5"] = measure_c5(args, rank, world, dev)
+    return line
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    rank, world, local, backend = init_dist(args)
+    try:
+        if args.check_launch:
+            run_check_launch(args, rank, world, backend)
+            return
+        dev = torch.device(f"cuda:{local}")
+        if args.mode == "sharded":
+            line = run_sharded_headline(args, rank, world, dev, backend)
+        else:
+            line = run_reduce(args, rank, world, dev, backend)
+        if rank == 0 and args.extra:
+            from bench_extra import run_extra
+            extra = run_extra(dev)
+            os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+            json.dump(extra, open(os.path.join(REPO, "gpurun_out", "bench_extra.json"), "w"), indent=1)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+    finally:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":

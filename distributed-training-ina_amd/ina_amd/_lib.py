@@ -24,6 +24,7 @@ FLAG_OVERFLOW, FLAG_ACK, FLAG_COLLISION, FLAG_RESEND = 0x80, 0x40, 0x20, 0x10
 ACT_DROP, ACT_FWD_AGG, ACT_FWD_COLLISION, ACT_FWD_ACK, ACT_FWD_OTHER = range(5)
 ROUTE_MAX = 256                    # ipRoute size, ngaa.p4:59
 PORT_DROP, PORT_NONE = -1, -2
+I16_WIRE_SHIFT, I16_WIRE_MAX_RANKS = 22, 64      # include/ina.h
 
 
 class InaError(RuntimeError):
@@ -58,6 +59,8 @@ SIGNATURES = {
     "ina_dequantize_i32_f32": [_vp, _vp, _sz, _i, _vp],
     "ina_dequantize_i16_f32": [_vp, _vp, _sz, _i, _vp],
     "ina_sum_reduce_i32": [_vp, _i, _vp, _sz, _vp],
+    "ina_quantize_f32_i16_wire": [_vp, _vp, _sz, _i, _vp],
+    "ina_i16_wire_finish": [_vp, _sz, _i, _i, _vp, _vp, _vp, _vp],
     "ina_sum_reduce_i16_sat": [_vp, _i, _vp, _sz, _i, _vp, _vp],
     "ina_quantize_reduce_f32_i32": [_vp, _i, _vp, _sz, _i, _vp],
     "ina_quantize_reduce_f32_i16_sat": [_vp, _i, _vp, _sz, _i, _i, _vp, _vp],

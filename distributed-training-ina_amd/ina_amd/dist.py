@@ -1,27 +1,41 @@
 """Multi-GPU aggregation of one bucket that outgrows a GPU (BASELINE config 5).
 
 Layout A of SURVEY.md 8e: every rank is one worker holding its full fp32
-gradient bucket.  Each rank quantises its bucket on its GPU (int32, 2^k fixed
-point), RCCL reduce-scatters the integers with SUM over xGMI -- integer addition
-mod 2^32 is associative and commutative, so the shard each rank receives is
-bit-identical to the switch's per-slot sum (processor.p4:14-24) in any ring or
-tree order -- the owner dequantises its shard, and an all-gather returns the
-full aggregate to every rank (the PS broadcast).  The int16 path never reduces
-saturated int16 through RCCL (saturation is not associative): it accumulates in
-int32 and saturates once after the reduce.
+gradient bucket.  Each rank quantises its bucket on its GPU, RCCL reduce-scatters
+the integers with SUM over xGMI, the owner of each shard decodes it, and an
+all-gather returns the full aggregate to every rank (the PS broadcast).  The
+switch aggregates every slot independently (ngaa.p4:87-168), so contiguous slot
+ranges can live on different GPUs.
 
-Shards are contiguous slot ranges padded to `align` values (default one V=256
-slot x 4 = 1024 values = 4 KiB), so no slot straddles two ranks.
-The collective plumbing (ShardPlan, reduce_scatter_sum, all_gather_shards) is
-device-agnostic and covered on CPU with gloo; the quantise/dequantise steps are
-the device kernels (no CPU path).
+Two wires:
+  "i32"  int32 fixed point (2^k).  Integer addition mod 2^32 is associative and
+         commutative, so the shard each rank receives is bit-identical to the
+         switch's per-slot sum (processor.p4:14-24) in any ring or tree order.
+  "i16"  config 4's int16 saturating quantiser.  Saturation is not associative,
+         so int16 values never go through the collective: each rank sends the
+         int32 wire q16 + (saturated << 22) (ina_quantize_f32_i16_wire), the SUM
+         carries the exact int16 sum and the count of saturating ranks together,
+         and the owner saturates once and sets the per-slot overflow flag (the
+         ngaa_h overflow bit, headers.p4:30) -- bit-identical to the single-GPU
+         ina_quantize_reduce_f32_i16_sat over the same W buckets.  The flags are
+         all-gathered next to the values.
+
+Shards are contiguous slot ranges padded to `align` values (default 1024 values =
+4 KiB, rounded up to a whole number of V-value slots), so no slot straddles two
+ranks.  The collective plumbing (ShardPlan, reduce_scatter_sum, all_gather_shards)
+is device-agnostic and covered on CPU with gloo; with a gloo group and device
+tensors the collectives stage through host memory (a test harness for several
+ranks on one GPU, never the RCCL path).  Quantise and decode are the device
+kernels (no CPU path).
 """
 from __future__ import annotations
+
+import math
 
 import torch
 import torch.distributed as dist
 
-from . import ops
+from . import _lib, ops
 
 
 class ShardPlan:
@@ -38,6 +52,10 @@ class ShardPlan:
         return lo, min(lo + self.shard, self.n)
 
 
+def _host_staged(group) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
 def reduce_scatter_sum(x_padded: torch.Tensor, plan: ShardPlan, group=None, out=None):
     """int32 [padded] -> this rank's [shard] of the element-wise sum over ranks."""
     if x_padded.numel() != plan.padded:
@@ -46,47 +64,110 @@ def reduce_scatter_sum(x_padded: torch.Tensor, plan: ShardPlan, group=None, out=
     if plan.world == 1:
         out.copy_(x_padded)
         return out
+    if x_padded.is_cuda and _host_staged(group):
+        h = torch.empty(plan.shard, dtype=x_padded.dtype)
+        dist.reduce_scatter_tensor(h, x_padded.cpu(), op=dist.ReduceOp.SUM, group=group)
+        out.copy_(h)
+        return out
     dist.reduce_scatter_tensor(out, x_padded, op=dist.ReduceOp.SUM, group=group)
     return out
 
 
 def all_gather_shards(shard: torch.Tensor, plan: ShardPlan, group=None, out=None):
-    out = torch.empty(plan.padded, dtype=shard.dtype, device=shard.device) if out is None else out
+    """[count] per rank -> [world * count] (count = plan.shard values, or its slot flags)."""
+    out = torch.empty(plan.world * shard.numel(), dtype=shard.dtype, device=shard.device) \
+        if out is None else out
     if plan.world == 1:
         out.copy_(shard)
+        return out
+    if _host_staged(group):
+        # gloo gathers bytes: an all-gather only moves data, so any dtype (gloo has no
+        # int16) goes through as its uint8 view, bit for bit
+        h = torch.empty(out.numel() * out.element_size(), dtype=torch.uint8)
+        dist.all_gather_into_tensor(h, shard.contiguous().cpu().view(torch.uint8), group=group)
+        out.copy_(h.view(out.dtype).view(out.shape))
         return out
     dist.all_gather_into_tensor(out, shard, group=group)
     return out
 
 
 class ShardedAggregator:
-    """Reusable buffers for repeated sharded aggregation of same-sized buckets."""
+    """Reusable buffers for repeated sharded aggregation of same-sized buckets.
 
-    def __init__(self, n: int, k: int = 16, group=None, device=None, align: int = 1024):
+    wire="i32": __call__ returns the dequantised fp32 sum over ranks.
+    wire="i16": the same from the int16 saturating path; `overflow` then holds the
+    per-slot flags (ceil(n / V) bytes) of the last call.
+    """
+
+    def __init__(self, n: int, k: int = 16, group=None, device=None, align: int = 1024,
+                 wire: str = "i32", V: int = 256):
+        if wire not in ("i32", "i16"):
+            raise ValueError("wire must be 'i32' or 'i16'")
+        if V <= 0:
+            raise ValueError("V must be > 0")
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if wire == "i16" and self.world > _lib.I16_WIRE_MAX_RANKS:
+            raise ValueError(f"the int16 wire sums at most {_lib.I16_WIRE_MAX_RANKS} ranks")
+        if wire == "i16":
+            align = align * V // math.gcd(align, V)        # shards hold whole slots
         self.plan = ShardPlan(n, self.world, align)
-        self.k, self.group = k, group
+        self.k, self.group, self.wire, self.V = k, group, wire, V
         dev = device or torch.device("cuda", torch.cuda.current_device())
         self.q = torch.zeros(self.plan.padded, dtype=torch.int32, device=dev)   # pad stays 0
         self.sum_shard = torch.empty(self.plan.shard, dtype=torch.int32, device=dev)
         self.f_shard = torch.empty(self.plan.shard, dtype=torch.float32, device=dev)
         self.full = torch.empty(self.plan.padded, dtype=torch.float32, device=dev)
+        if wire == "i16":
+            self.slots_per_shard = self.plan.shard // V
+            self.ovf_shard = torch.empty(self.slots_per_shard, dtype=torch.uint8, device=dev)
+            self.ovf_full = torch.empty(self.slots_per_shard * self.world, dtype=torch.uint8,
+                                        device=dev)
+
+    @property
+    def overflow(self) -> torch.Tensor:
+        """Per-slot overflow flags of the last i16 aggregation (ceil(n / V) bytes)."""
+        if self.wire != "i16":
+            raise AttributeError("overflow flags exist only on the i16 wire")
+        return self.ovf_full[: -(-self.plan.n // self.V)]
+
+    def _quantize(self, grad: torch.Tensor):
+        n = self.plan.n
+        if grad.numel() != n:
+            raise ValueError("bucket size changed")
+        x = grad.reshape(-1)
+        if self.wire == "i32":
+            ops.quantize(x, self.k, out=self.q[:n])
+        else:
+            ops.quantize_i16_wire(x, self.k, out=self.q[:n])
+
+    def _decode(self, src: torch.Tensor, y: torch.Tensor, ovf=None):
+        if self.wire == "i32":
+            ops.dequantize(src, self.k, out=y)
+        else:
+            ops.i16_wire_finish(src, self.k, self.V, y=y, overflow=ovf, want_out16=False)
 
     def __call__(self, grad: torch.Tensor) -> torch.Tensor:
         """fp32 [n] local bucket -> fp32 [n] dequantised sum over all ranks."""
         n = self.plan.n
-        if grad.numel() != n:
-            raise ValueError("bucket size changed")
-        if self.world == 1:      # the collectives are identities: quantise -> dequantise
-            ops.quantize(grad.reshape(-1), self.k, out=self.q[:n])
-            return ops.dequantize(self.q[:n], self.k, out=self.full[:n])
-        ops.quantize(grad.reshape(-1), self.k, out=self.q[:n])
+        self._quantize(grad)
+        ovf_full = self.ovf_full if self.wire == "i16" else None
+        if self.world == 1:      # the collectives are identities: quantise -> decode
+            self._decode(self.q, self.full, ovf_full)
+            return self.full[:n]
         reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
-        ops.dequantize(self.sum_shard, self.k, out=self.f_shard)
+        self._decode(self.sum_shard, self.f_shard, self.ovf_shard if ovf_full is not None else None)
         all_gather_shards(self.f_shard, self.plan, self.group, out=self.full)
+        if ovf_full is not None:
+            all_gather_shards(self.ovf_shard, self.plan, self.group, out=ovf_full)
         return self.full[:n]
 
     def aggregate_int(self, grad: torch.Tensor) -> torch.Tensor:
-        """fp32 [n] -> this rank's int32 shard of the integer aggregate (no gather)."""
-        ops.quantize(grad.reshape(-1), self.k, out=self.q[: self.plan.n])
-        return reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
+        """fp32 [n] -> this rank's integer shard of the aggregate (no gather): the
+        int32 wrapped sum, or on the i16 wire the int16 saturated sum (its slot flags
+        in `ovf_shard`)."""
+        self._quantize(grad)
+        s = reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
+        if self.wire == "i32":
+            return s
+        out16, _, _ = ops.i16_wire_finish(s, self.k, self.V, overflow=self.ovf_shard, want_y=False)
+        return out16

@@ -86,6 +86,47 @@ def quantize_i16(x: torch.Tensor, k: int, V: int, out=None, overflow=None):
     return out, overflow
 
 
+def quantize_i16_wire(x: torch.Tensor, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 -> int32 wire words q16(x) + (saturated << 22) (include/ina.h): the int16
+    quantisation widened so an int32 SUM collective carries the sum and the saturation
+    count together (the sharded int16 path, dist.ShardedAggregator(wire="i16"))."""
+    _req(x, torch.float32, "x")
+    out = torch.empty(x.shape, dtype=torch.int32, device=x.device) if out is None else out
+    _fits(out, x.numel())
+    _req(out, torch.int32, "out")
+    _same_device(x, out)
+    check(load().ina_quantize_f32_i16_wire(x.data_ptr(), out.data_ptr(), x.numel(), k, _stream(x)),
+          "quantize_i16_wire")
+    return out
+
+
+def i16_wire_finish(wire_sum: torch.Tensor, k: int, V: int, out16=None, y=None, overflow=None,
+                    want_out16: bool = True, want_y: bool = True):
+    """Summed int32 wire shard -> (int16 saturated sum, fp32 dequantised, u8 per-slot
+    overflow flags); a result is None when neither given nor wanted."""
+    _req(wire_sum, torch.int32, "wire_sum")
+    n, dev = wire_sum.numel(), wire_sum.device
+    if V <= 0:
+        raise ValueError("V must be > 0")
+    nslot = (n + V - 1) // V
+    if out16 is None and want_out16:
+        out16 = torch.empty(n, dtype=torch.int16, device=dev)
+    if y is None and want_y:
+        y = torch.empty(n, dtype=torch.float32, device=dev)
+    overflow = torch.empty(nslot, dtype=torch.uint8, device=dev) if overflow is None else overflow
+    for t, dt, cnt, name in ((out16, torch.int16, n, "out16"), (y, torch.float32, n, "y"),
+                             (overflow, torch.uint8, nslot, "overflow")):
+        if t is not None:
+            _fits(t, cnt, name)
+            _req(t, dt, name)
+            _same_device(wire_sum, t)
+    check(load().ina_i16_wire_finish(wire_sum.data_ptr(), n, k, V,
+                                     out16.data_ptr() if out16 is not None else None,
+                                     y.data_ptr() if y is not None else None, overflow.data_ptr(),
+                                     _stream(wire_sum)), "i16_wire_finish")
+    return out16, y, overflow
+
+
 def dequantize(s: torch.Tensor, k: int, out: torch.Tensor | None = None) -> torch.Tensor:
     out = torch.empty(s.shape, dtype=torch.float32, device=s.device) if out is None else out
     _fits(out, s.numel())

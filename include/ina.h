@@ -111,6 +111,24 @@ int ina_quantize_reduce_f32_i16_sat(const float* const* bufs, int W, int16_t* ou
                                     int k, int V, uint8_t* overflow_per_slot,
                                     ina_stream_t stream);
 
+/* ---- int16 wire under slot-range sharding (config-4 semantics across GPUs)
+ * Saturation is not associative, so sharded ranks never reduce int16 through the
+ * collective.  Each rank widens its int16-saturated quantisation (the quantiser of
+ * ina_quantize_f32_i16_sat) into an int32 wire word
+ *     wire[i] = q16(x[i]) + (sat_i << INA_I16_WIRE_SHIFT)     (sat_i: clamped or NaN)
+ * and the wires are summed with an ordinary int32 SUM (RCCL reduce-scatter, any order).
+ * For <= INA_I16_WIRE_MAX_RANKS ranks the low 22 bits hold sum q16 exactly and the high
+ * bits count the ranks that saturated.  ina_i16_wire_finish decodes a summed shard:
+ * out16[i] = sat16(sum q16), y[i] = out16[i] * 2^-k, overflow_per_slot[s] = 1 iff a rank
+ * saturated an element of slot s (V values) or its sum saturated (the ngaa_h overflow
+ * bit, headers.p4:30) -- bit-identical to ina_quantize_reduce_f32_i16_sat over the same
+ * buckets.  out16, y, overflow_per_slot may each be NULL; every slot flag is written.  */
+#define INA_I16_WIRE_SHIFT 22
+#define INA_I16_WIRE_MAX_RANKS 64
+int ina_quantize_f32_i16_wire(const float* x, int32_t* wire, size_t n, int k, ina_stream_t stream);
+int ina_i16_wire_finish(const int32_t* wire_sum, size_t n, int k, int V, int16_t* out16, float* y,
+                        uint8_t* overflow_per_slot, ina_stream_t stream);
+
 /* ---- PS combine ------------------------------------------------------------------
  * launch.py:42-52 / launch_async.py:42-57 aggregate(), fused, bit-exact to the
  * torch fp32 sequence: out = local + float(weight_step) * (0 + sum_w (paras[w] - local)).

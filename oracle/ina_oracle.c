@@ -177,6 +177,44 @@ int orc_quantize_reduce_f32_i16_sat(const float* const* bufs, int W, int16_t* ou
     return 0;
 }
 
+/* int16 wire under sharding (build-defined; include/ina.h): a rank
+ * sends q16 widened to int32 plus its saturation bit at 2^22, the ranks' wires are
+ * summed in int32, and the owner decodes sum q16 and the saturation count.  Written
+ * here with 64-bit floor division (the device uses shifts), so the check is not a copy
+ * of the kernel.  End to end it must equal orc_quantize_reduce_f32_i16_sat. */
+int orc_quantize_f32_i16_wire(const float* x, int32_t* wire, size_t n, int k) {
+    if (k < -126 || k > 127) return ORC_EINVAL;
+    float s = pow2f(k);
+    for (size_t i = 0; i < n; ++i) {
+        int sat = 0;
+        int32_t v = orc_q_i16(x[i], s, &sat);
+        wire[i] = (int32_t)((int64_t)v + (int64_t)sat * (1 << 22));
+    }
+    return 0;
+}
+
+int orc_i16_wire_finish(const int32_t* wsum, size_t n, int k, int V, int16_t* out16, float* y,
+                        uint8_t* ovf) {
+    if (k < -126 || k > 127 || V <= 0) return ORC_EINVAL;
+    float inv = pow2f(-k);
+    size_t slots = (n + (size_t)V - 1) / (size_t)V;
+    if (ovf) memset(ovf, 0, slots);
+    for (size_t i = 0; i < n; ++i) {
+        int64_t t = (int64_t)wsum[i] + (1 << 21);
+        int64_t c = t >= 0 ? t / (1 << 22) : -((-t + (1 << 22) - 1) / (1 << 22));   /* floor */
+        int64_t v = (int64_t)wsum[i] - c * (1 << 22);
+        int sat = c != 0;
+        int16_t r;
+        if (v > INT16_MAX) { r = INT16_MAX; sat = 1; }
+        else if (v < INT16_MIN) { r = INT16_MIN; sat = 1; }
+        else r = (int16_t)v;
+        if (out16) out16[i] = r;
+        if (y) y[i] = (float)r * inv;
+        if (sat && ovf) ovf[i / (size_t)V] = 1;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------- */
 /* a13: PS float combine, launch.py:42-52 (and launch_async.py:42-57):         */
 /*   local += (w * step) * sum([p_w - local for w])                            */

@@ -72,6 +72,9 @@ int orc_sum_reduce_i16_sat(const int16_t* const* bufs, int W, int16_t* out, size
 int orc_quantize_reduce_f32_i32(const float* const* bufs, int W, int32_t* out, size_t n, int k);
 int orc_quantize_reduce_f32_i16_sat(const float* const* bufs, int W, int16_t* out, size_t n,
                                     int k, int V, uint8_t* ovf);
+int orc_quantize_f32_i16_wire(const float* x, int32_t* wire, size_t n, int k);
+int orc_i16_wire_finish(const int32_t* wsum, size_t n, int k, int V, int16_t* out16, float* y,
+                        uint8_t* ovf);
 int orc_ps_combine_f32(const float* local, const float* const* paras, int W,
                        double weight_step, float* out, size_t n);
 int orc_ps_combine_ina_f32(const float* local, const float* const* paras, int W, int k,

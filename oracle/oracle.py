@@ -73,6 +73,8 @@ def lib():
             "orc_sum_reduce_i16_sat": [vp, i, vp, sz, i, vp],
             "orc_quantize_reduce_f32_i32": [vp, i, vp, sz, i],
             "orc_quantize_reduce_f32_i16_sat": [vp, i, vp, sz, i, i, vp],
+            "orc_quantize_f32_i16_wire": [vp, vp, sz, i],
+            "orc_i16_wire_finish": [vp, sz, i, i, vp, vp, vp],
             "orc_ps_combine_f32": [vp, vp, i, C.c_double, vp, sz],
             "orc_ps_combine_ina_f32": [vp, vp, i, i, C.c_double, vp, sz],
             "orc_pack_nga": [vp, sz, C.POINTER(NgaParams), vp, vp, sz],
@@ -176,6 +178,25 @@ def quantize_reduce_i16_sat(bufs, k: int, V: int):
     _chk(lib().orc_quantize_reduce_f32_i16_sat(_ptr_array(bufs), len(bufs), _p(out), n, k, V,
                                                _p(ovf)))
     return out, ovf
+
+
+# -- int16 wire under sharding (build-defined; include/ina.h) -----------
+def quantize_i16_wire(x: np.ndarray, k: int) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float32)
+    w = np.empty(x.shape, np.int32)
+    _chk(lib().orc_quantize_f32_i16_wire(_p(x), _p(w), x.size, k))
+    return w
+
+
+def i16_wire_finish(wsum: np.ndarray, k: int, V: int):
+    """summed wire -> (int16, fp32 dequantised, per-slot overflow flags)"""
+    wsum = np.ascontiguousarray(wsum, np.int32)
+    n = wsum.size
+    out16 = np.empty(n, np.int16)
+    y = np.empty(n, np.float32)
+    ovf = np.zeros((n + V - 1) // V, np.uint8)
+    _chk(lib().orc_i16_wire_finish(_p(wsum), n, k, V, _p(out16), _p(y), _p(ovf)))
+    return out16, y, ovf
 
 
 # -- a13 PS float combine ---------------------------------------------------------

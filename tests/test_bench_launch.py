@@ -1,0 +1,44 @@
+"""bench.py's multi-rank launcher on CPU: `bench.py --gpus N` with no launcher around it
+starts N ranks itself (torch.distributed.run on 127.0.0.1), every rank asserts the group
+size, and rank 0 prints one line with n_gpus == N.  --check-launch does no GPU work, so
+this runs here with gloo; the GPU rehearsal is tests/test_gpu_bench_contract.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import REPO
+
+
+def _bench(*args, env=None, timeout=240):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO,
+                          capture_output=True, text=True, timeout=timeout, env=e)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_bench_gpus_n_spawns_n_ranks(n):
+    r = _bench("--gpus", str(n), "--check-launch")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["rccl_world"] == n and d["ranks"] == list(range(n))
+    assert d["backend"] == ("gloo" if n > 1 else "none")
+
+
+def test_bench_refuses_a_group_of_the_wrong_size():
+    r = _bench("--gpus", "2", "--check-launch", env={"WORLD_SIZE": "1"})
+    assert r.returncode != 0
+    assert "--gpus 2 but the launcher started 1 ranks" in r.stderr
+
+
+def test_cgroup_quota_reader_is_safe():
+    sys.path.insert(0, REPO)
+    import bench
+    q = bench.cgroup_cpus()
+    assert q is None or q > 0

@@ -121,6 +121,8 @@ def _einval_cases():
         "ina_quantize_f32_i32": (None, None, 64, 16, None),
         "ina_quantize_f32_i16_sat": (None, None, 64, 8, 32, None, None),
         "ina_dequantize_i32_f32": (None, None, 64, 16, None),
+        "ina_quantize_f32_i16_wire": (None, None, 64, 11, None),
+        "ina_i16_wire_finish": (None, 64, 11, 256, None, None, None, None),
         "ina_dequantize_i16_f32": (None, None, 64, 16, None),
         "ina_sum_reduce_i32": (P([None, None]), 2, None, 64, None),
         "ina_sum_reduce_i16_sat": (P([None, None]), 2, None, 64, 32, None, None),

@@ -2,7 +2,9 @@
 ina_amd.dist over gloo with world_size 2 and 3 (127.0.0.1 rendezvous).  Inputs
 are quantised by the CPU oracle (test infrastructure) since the product's
 quantiser is device-only; the integer aggregate must be bit-identical to the
-oracle's W-way wrapping sum (the switch's Processor add)."""
+oracle's W-way wrapping sum (the switch's Processor add), and the int16 wire
+(q16 + saturated << 22, summed in int32, decoded once per shard) bit-identical
+to the single-bucket int16 saturating path with its per-slot overflow flags."""
 import os
 import socket
 
@@ -70,3 +72,79 @@ def test_shard_plan_alignment():
     rs = [p.range_of(r) for r in range(3)]
     assert rs[0][0] == 0 and rs[-1][1] == p.n and all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
     assert ShardPlan(0, 4).padded == 0
+
+
+def _worker_i16(rank, world, port, n, k, V, results):
+    import sys
+    for p in (REPO, PKG_ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import math
+    from ina_amd.dist import ShardPlan, all_gather_shards, reduce_scatter_sum
+    from oracle import oracle as orc
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = _i16_bucket(rank, n)
+        wire = orc.quantize_i16_wire(x, k)
+        plan = ShardPlan(n, world, align=1024 * V // math.gcd(1024, V))
+        wp = torch.zeros(plan.padded, dtype=torch.int32)
+        wp[:n] = torch.from_numpy(wire)
+        shard = reduce_scatter_sum(wp, plan)
+        o16, y, ovf = orc.i16_wire_finish(shard.numpy(), k, V)
+        full16 = all_gather_shards(torch.from_numpy(o16), plan)
+        fully = all_gather_shards(torch.from_numpy(y), plan)
+        fullf = all_gather_shards(torch.from_numpy(ovf), plan)
+        results[rank] = (full16[:n].numpy().copy(), fully[:n].numpy().copy(),
+                         fullf[: (n + V - 1) // V].numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+def _i16_bucket(rank, n):
+    """~N(0, 1) gradients with a few 100x outliers: at k=11 a single value saturates
+    past |x| = 16, and the sum of several ranks saturates more often."""
+    rng = np.random.default_rng(1000 + rank)
+    x = rng.standard_normal(n).astype(np.float32)
+    idx = rng.choice(n, max(1, n // 200), replace=False)
+    x[idx] *= 100
+    if n > 7:
+        x[7] = np.nan
+    return x
+
+
+@pytest.mark.parametrize("world,n,V", [(2, 100_003, 256), (3, 5000, 32), (2, 1, 256), (4, 9000, 100)])
+def test_sharded_i16_wire_gloo(world, n, V):
+    k = 11
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker_i16, args=(world, _free_port(), n, k, V, results), nprocs=world, join=True)
+    from oracle import oracle as orc
+    want16, want_ovf = orc.quantize_reduce_i16_sat([_i16_bucket(r, n) for r in range(world)], k, V)
+    assert 0 < want_ovf.sum() < want_ovf.size or n < 2 * V     # the flag path is exercised
+    for r in range(world):
+        o16, y, ovf = results[r]
+        assert np.array_equal(o16, want16)
+        assert np.array_equal(y, orc.dequantize_i16(want16, k))
+        assert np.array_equal(ovf, want_ovf)
+
+
+def test_i16_wire_oracle_identity():
+    """The wire decode equals the one-GPU int16 path for every rank count up to the
+    wire's limit (64): extremes of the 22-bit field included."""
+    from oracle import oracle as orc
+    rng = np.random.default_rng(5)
+    n, V, k = 4096, 256, 0
+    for world in (1, 2, 7, 64):
+        xs = [rng.integers(-40000, 40000, n).astype(np.float32) for _ in range(world)]
+        xs[0][:64] = 32767.0                       # all ranks at the top: 64 * 32767 < 2^21
+        for x in xs:
+            x[:64] = 32767.0
+            x[64:128] = -32768.0                   # and the bottom: 64 * -32768 = -2^21
+        s = np.zeros(n, np.int64)
+        for x in xs:
+            s += orc.quantize_i16_wire(x, k)
+        assert np.abs(s).max() < 2 ** 31
+        o16, y, ovf = orc.i16_wire_finish(s.astype(np.int32), k, V)
+        w16, wovf = orc.quantize_reduce_i16_sat(xs, k, V)
+        assert np.array_equal(o16, w16) and np.array_equal(ovf, wovf)

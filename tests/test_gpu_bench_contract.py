@@ -1,5 +1,9 @@
-"""bench.py's output contract (one JSON line with the driver's keys, roofline and
-cpu_baseline objects) on a short run; the bench runs as a child process."""
+"""bench.py's output contract (one JSON line with the driver's keys, roofline,
+cpu_baseline and sharded_c5 objects) on short runs; the bench runs as a child process.
+The two-rank rehearsal puts both ranks on the one GPU of the test box with a gloo group
+(bench.py --gpus 2 launching its own ranks, INA_BENCH_BACKEND=gloo): the launcher, the
+group-size assertion, the per-rank slot ranges and the config-5 path through
+ShardedAggregator at world size 2 -- the RCCL run itself needs the 8-GPU node."""
 import json
 import os
 import subprocess
@@ -10,38 +14,67 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.gpu
-def test_bench_json_line_contract():
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--cpu-sample", str(1 << 16)],
-                       cwd=REPO, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
+def _line(r):
+    assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def _run(*args, env=None, timeout=300):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO,
+                          capture_output=True, text=True, timeout=timeout, env=e)
+
+
+@pytest.mark.gpu
+def test_bench_json_line_contract():
+    d = _line(_run("--steps", "3", "--warmup", "1", "--cpu-sample", str(1 << 16),
+                   "--c5-values", str(1 << 22), "--c5-steps", "2"))
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline",
+                "rccl_world", "sharded_c5"):
         assert key in d, key
-    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["n_gpus"] == 1 and d["rccl_world"] == 1 and d["steps"] == 3 and d["warmup"] == 1
+    assert d["scaling"] == "weak"
     assert d["higher_is_better"] is True and d["value"] > 0 and d["parity_spot_check"] is True
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert rf["algorithmic_bytes_per_launch"] == 9 * 26_214_400 * 4
     cb = d["cpu_baseline"]
-    assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
-    assert cb["matches_gpu"] is True
+    assert cb["kind"] in ("port", "reference") and cb["value"] > 0
+    assert cb["affinity_cores"] == len(os.sched_getaffinity(0)) and 1 <= cb["cores"] <= cb["affinity_cores"]
+    assert cb["value"] == max(cb["value_by_threads"].values())
+    assert cb["matches_gpu"] is True and cb["value_1core"] > 0
     assert "workload" in d["config"]
+    c5 = d["sharded_c5"]
+    assert c5["parity_spot_check"] is True and c5["rccl_world"] == 1 and c5["values_per_rank"] == 1 << 22
 
 
 @pytest.mark.gpu
 def test_bench_sharded_mode_line():
-    """Config-5 mode on one GPU (the collectives are identities): a JSON line whose
-    aggregate passes its own parity spot check."""
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--mode", "sharded", "--steps", "2",
-                        "--warmup", "1", "--values", str(1 << 22)],
-                       cwd=REPO, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity_spot_check"] is True
-    assert d["config"]["values_per_worker"] == 1 << 22
+    """Config-5 mode on one GPU (the collectives are identities), both wires."""
+    for wire in ("i32", "i16"):
+        d = _line(_run("--mode", "sharded", "--c5-steps", "2", "--c5-values", str(1 << 22),
+                       "--wire", wire))
+        assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity_spot_check"] is True, wire
+        assert d["config"]["values_per_worker"] == 1 << 22
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal_on_one_gpu():
+    """bench.py --gpus 2 starts two ranks itself; both on cuda:0 with gloo."""
+    d = _line(_run("--gpus", "2", "--steps", "3", "--warmup", "1", "--values", str(1 << 22),
+                   "--c5-values", str(1 << 22), "--c5-steps", "2",
+                   env={"INA_BENCH_BACKEND": "gloo"}, timeout=400))
+    assert d["n_gpus"] == 2 and d["rccl_world"] == 2 and d["backend"] == "gloo"
+    assert d["parity_spot_check"] is True and "cpu_baseline" not in d
+    c5 = d["sharded_c5"]
+    assert c5["rccl_world"] == 2 and c5["parity_spot_check"] is True
+    assert c5["xgmi"]["rs_send_bytes_per_rank"] == c5["shard_values"] * 4
+    d = _line(_run("--gpus", "2", "--mode", "sharded", "--wire", "i16", "--c5-values", "1000003",
+                   "--c5-steps", "2", env={"INA_BENCH_BACKEND": "gloo"}, timeout=400))
+    assert d["n_gpus"] == 2 and d["parity_spot_check"] is True

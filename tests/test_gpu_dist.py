@@ -1,0 +1,141 @@
+"""Sharded aggregation (SURVEY.md 8e, config 5 layout A) at world size > 1 with the
+device kernels: two ranks launched by torch.distributed.run, both on cuda:0 with a gloo
+group (the collectives stage through host memory; one GPU cannot hold two RCCL ranks),
+quantise / wire decode / dequantise through libina.so.  Every rank's full aggregate is
+compared bit for bit with the oracle's single-bucket path over all ranks' buckets:
+  i32: dequantize_i32(quantize_reduce_i32)           (the switch's wrapping slot sum)
+  i16: dequantize_i16(quantize_reduce_i16_sat) + the per-slot overflow flags
+Plus config 5 at its full size on one rank (1 GiB bucket), checked on a strided sample."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests.conftest import REPO
+from tests._dist_gpu_rank import bucket
+
+RANK_SCRIPT = os.path.join(REPO, "tests", "_dist_gpu_rank.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(tmp_path, world, n, wire, k, V=256):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", RANK_SCRIPT,
+           "--size", str(n), "--wire", wire, "--k", str(k), "--V", str(V), "--out", str(tmp_path)]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return [dict(np.load(os.path.join(tmp_path, f"rank{i}.npz"))) for i in range(world)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n", [(2, 1_000_003), (3, 70_001), (2, 1)])
+def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n):
+    from oracle import oracle as orc
+    k = 20
+    res = _run_ranks(tmp_path, world, n, "i32", k)
+    want_int = orc.quantize_reduce_i32([bucket(r, n, "i32") for r in range(world)], k)
+    want = orc.dequantize_i32(want_int, k)
+    for r, d in enumerate(res):
+        assert int(d["world"][0]) == world
+        assert d["lib"][0].endswith("libina.so")
+        assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
+        lo, hi = d["range"]
+        assert np.array_equal(d["shard"], want_int[lo:hi])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,V", [(2, 1_000_003, 256), (3, 50_000, 32), (2, 300, 100)])
+def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V):
+    from oracle import oracle as orc
+    k = 11
+    res = _run_ranks(tmp_path, world, n, "i16", k, V)
+    want16, want_ovf = orc.quantize_reduce_i16_sat([bucket(r, n, "i16") for r in range(world)], k, V)
+    assert want_ovf.any() and not want_ovf.all()
+    want = orc.dequantize_i16(want16, k)
+    for r, d in enumerate(res):
+        assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
+        assert np.array_equal(d["ovf"], want_ovf), f"rank {r}"
+        lo, hi = d["range"]
+        assert np.array_equal(d["shard"], want16[lo:hi])
+
+
+@pytest.mark.gpu
+def test_c5_full_size_one_rank_strided_sample():
+    """Config 5's 1 GiB fp32 bucket (268,435,456 values) through ShardedAggregator on one
+    rank, both wires; every 4099th value plus the last 10,000 against the oracle."""
+    import torch
+    from ina_amd.dist import ShardedAggregator
+    from oracle import oracle as orc
+    n, dev = 268_435_456, torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000)
+    x = torch.randn(n, device=dev, generator=g) * 1e-2
+    idx = np.concatenate([np.arange(0, n, 4099), np.arange(n - 10_000, n)])
+    tidx = torch.from_numpy(idx).to(dev)
+    xs = x[tidx].cpu().numpy()
+    agg = ShardedAggregator(n, k=16, device=dev)
+    y = agg(x)
+    assert np.array_equal(y[tidx].cpu().numpy(), orc.dequantize_i32(orc.quantize_i32(xs, 16), 16))
+    del agg, y
+    agg = ShardedAggregator(n, k=20, device=dev, wire="i16", V=256)   # 1e-2 * 2^20 saturates often
+    y = agg(x)
+    w16, _ = orc.quantize_reduce_i16_sat([xs], 20, 1)
+    assert np.array_equal(y[tidx].cpu().numpy(), orc.dequantize_i16(w16, 20))
+    ovf = agg.overflow.cpu().numpy()
+    assert ovf.size == n // 256
+    slots = np.unique(idx // 256)
+    sat = np.zeros(n // 256, bool)
+    _, f1 = orc.quantize_reduce_i16_sat([xs], 20, 1)
+    np.logical_or.at(sat, idx // 256, f1.astype(bool))
+    # a sampled saturating value flags its slot; unsampled values may flag more
+    assert (ovf[slots][sat[slots]] == 1).all()
+    full_slot = x[: 256 * 64].cpu().numpy()                   # 64 whole slots exactly
+    _, f64 = orc.quantize_reduce_i16_sat([full_slot], 20, 256)
+    assert np.array_equal(ovf[:64], f64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 3, 4, 255, 1000, 65_536, 1_000_003])
+@pytest.mark.parametrize("V", [32, 256, 100, 512])
+def test_i16_wire_kernels_vs_oracle(n, V):
+    """ina_quantize_f32_i16_wire and ina_i16_wire_finish bit-exact against the oracle,
+    aligned (vector) and offset-by-one (scalar) buffers, summed over 3 ranks' wires."""
+    import torch
+    from ina_amd import ops
+    from oracle import oracle as orc
+    k, dev = 11, torch.device("cuda", 0)
+    xs = [bucket(r, n, "i16") for r in range(3)]
+    for off in (0, 1):
+        wires = []
+        for x in xs:
+            buf = torch.zeros(n + off, dtype=torch.float32, device=dev)
+            buf[off:] = torch.from_numpy(x).to(dev)
+            wbuf = torch.zeros(n + off, dtype=torch.int32, device=dev)
+            ops.quantize_i16_wire(buf[off:], k, out=wbuf[off:])
+            w = wbuf[off:].cpu().numpy()
+            assert np.array_equal(w, orc.quantize_i16_wire(x, k)), (off, n, V)
+            wires.append(w.astype(np.int64))
+        wsum = np.sum(wires, axis=0).astype(np.int32)
+        src = torch.zeros(n + off, dtype=torch.int32, device=dev)
+        src[off:] = torch.from_numpy(wsum).to(dev)
+        o16 = torch.empty(n + off, dtype=torch.int16, device=dev)
+        yv = torch.empty(n + off, dtype=torch.float32, device=dev)
+        g16, gy, govf = ops.i16_wire_finish(src[off:], k, V, out16=o16[off:], y=yv[off:])
+        w16, wy, wovf = orc.i16_wire_finish(wsum, k, V)
+        assert np.array_equal(g16.cpu().numpy(), w16), (off, n, V)
+        assert np.array_equal(gy.cpu().numpy().view(np.uint32), wy.view(np.uint32))
+        assert np.array_equal(govf.cpu().numpy(), wovf), (off, n, V)
+        r16, rovf = orc.quantize_reduce_i16_sat(xs, k, V)         # the one-GPU int16 path
+        assert np.array_equal(w16, r16) and np.array_equal(wovf, rovf)
+        # flags only (no value outputs) writes every slot flag too
+        ovf = torch.full(((n + V - 1) // V,), 7, dtype=torch.uint8, device=dev)
+        ops.i16_wire_finish(src[off:], k, V, overflow=ovf, want_out16=False, want_y=False)
+        assert np.array_equal(ovf.cpu().numpy(), wovf)
