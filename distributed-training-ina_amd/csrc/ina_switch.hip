@@ -743,10 +743,13 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                         }
                         have_reg = true;
                         act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
-                        const bool fused = kPs && act == INA_ACT_FWD_AGG;
-                        if (fused) {                         // launch.py:46-50 with the switch's sum
-                            const uint32_t ps_slot = frag_in - ps.seq0;
-                            if (ps_slot < ps.nslots) {
+                        // the PS consumes a completed packet of its bucket (ps_slot in range;
+                        // wave-uniform); one outside the bucket is forwarded like the two-call
+                        // path forwards it, whatever keep_fwd says
+                        const uint32_t ps_slot = frag_in - ps.seq0;
+                        const bool consumed = kPs && act == INA_ACT_FWD_AGG && ps_slot < ps.nslots;
+                        if (consumed) {                      // launch.py:46-50 with the switch's sum
+                            {
                                 const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)lane;
                                 if (vl && e0 + 4 <= ps.n) {
                                     const f32x4s l = *reinterpret_cast<const f32x4s*>(ps.local + e0);
@@ -770,7 +773,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                                 }
                             }
                         }
-                        if ((act != INA_ACT_DROP || st.write_dropped) && (!fused || ps.keep_fwd)) {
+                        if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
                             // out_value -> payload (processor.p4:22): chunk c from lane c-1
                             u32x4s p;
                             p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
@@ -1011,10 +1014,12 @@ int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t
     if (acks && (((uintptr_t)acks & 15u) || ack_stride % 16))
         return set_error(INA_EINVAL, "ack rows must be 16-byte aligned%s", "");
     if (!st || st->V <= 0) return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
-    // the PS step needs the layout ina_apply_completed_nga takes; refuse before the switch
-    // touches its state rather than after
-    if (st->V % 4 || st->V > 256 || stride % 16 || ((uintptr_t)pkts & 15u))
-        return set_error(INA_EINVAL, "process_apply needs V %% 4 == 0 <= 256 and 16-byte aligned rows%s", "");
+    // the PS step needs the layout ina_apply_completed_nga and the fused run kernel take
+    // (16-byte aligned rows and slot registers); refuse before the switch touches its state
+    // rather than after, so keep_forwarded always means what include/ina.h says
+    if (st->V % 4 || st->V > 256 || stride % 16 || ((uintptr_t)pkts & 15u) || ((uintptr_t)st->regs & 15u))
+        return set_error(INA_EINVAL,
+                         "process_apply needs V %% 4 == 0 <= 256 and 16-byte aligned rows and registers%s", "");
     const size_t nslots = (n + (size_t)st->V - 1) / (size_t)st->V;
     PsFuse ps{local, out, n, ldexpf(1.0f, -k), (float)weight_step, seq0,
               nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,

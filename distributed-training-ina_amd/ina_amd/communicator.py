@@ -16,15 +16,23 @@ data_size is the slice's byte count.
 
 Set `send_fd` to an open datagram socket to send there (ina_send_gradients_fd)
 instead of the raw IPPROTO_UDP socket send_gradients opens per call.
+
+The process fan-outs (multi_process_send, multi_process_send_futures_P) start their
+workers with the "spawn" method, never fork: send_gradients runs HIP (the packets are
+built on the GPU), and a child forked from a parent that has initialised HIP is not
+supported.  A `send_fd` travels to the spawned workers as a socket object (its
+descriptor is duplicated into the child by multiprocessing's resource sharer).
 """
 from __future__ import annotations
 
 import ctypes as C
+import multiprocessing
+import os
+import socket
 import threading
 import time
 from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
 from ctypes import POINTER, c_int, c_uint32
-from multiprocessing import Pool
 
 from . import _lib
 
@@ -81,13 +89,39 @@ def _report(process_num, data, start):
         process_num, end - start, data_size / max(end - start, 1e-12)))
 
 
+_SPAWN = multiprocessing.get_context("spawn")    # never fork a HIP-initialised parent
+
+
+def _child_send(sock, gradient, packet_num, dst_ip, worker_id, aggregator_index, tensor_index):
+    """Runs in a spawned worker: send on the parent's socket when it passed one."""
+    global send_fd
+    send_fd = sock.fileno() if sock is not None else None
+    try:
+        return c_send_wrapper(gradient, packet_num, dst_ip, worker_id, aggregator_index,
+                              tensor_index)
+    finally:
+        send_fd = None
+        if sock is not None:
+            sock.close()
+
+
+def _shared_socket():
+    """The caller's send_fd as a socket object a spawned worker can receive (a dup)."""
+    return socket.socket(fileno=os.dup(send_fd)) if send_fd is not None else None
+
+
 def multi_process_send(process_num, data):
     start = time.time()
-    with Pool(process_num) as pool:
-        rs = [pool.apply_async(c_send_wrapper, (s, n, ip2int(dst_ip_str), 0, 0, off))
-              for s, n, off in _slices(process_num, data)]
-        for r in rs:
-            r.get()
+    sock = _shared_socket()
+    try:
+        with _SPAWN.Pool(process_num) as pool:
+            rs = [pool.apply_async(_child_send, (sock, s, n, ip2int(dst_ip_str), 0, 0, off))
+                  for s, n, off in _slices(process_num, data)]
+            for r in rs:
+                r.get()
+    finally:
+        if sock is not None:
+            sock.close()
     _report(process_num, data, start)
 
 
@@ -103,11 +137,16 @@ def multi_thread_send_futures(process_num, data):
 
 def multi_process_send_futures_P(process_num, data):
     start = time.time()
-    with ProcessPoolExecutor() as ex:
-        fs = [ex.submit(c_send_wrapper, s, n, ip2int(dst_ip_str), 0, 0, off)
-              for s, n, off in _slices(process_num, data)]
-        for f in fs:
-            f.result()
+    sock = _shared_socket()
+    try:
+        with ProcessPoolExecutor(mp_context=_SPAWN) as ex:
+            fs = [ex.submit(_child_send, sock, s, n, ip2int(dst_ip_str), 0, 0, off)
+                  for s, n, off in _slices(process_num, data)]
+            for f in fs:
+                f.result()
+    finally:
+        if sock is not None:
+            sock.close()
     _report(process_num, data, start)
 
 

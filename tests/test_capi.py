@@ -198,3 +198,17 @@ def test_switch_scratch_bytes_monotonic():
             assert b >= prev, (slots, npk)
             assert b >= 16 * npk
             prev = b
+
+
+def test_process_apply_refuses_misaligned_registers():
+    """ina_switch_process_apply takes only layouts its fused kernel handles, so
+    keep_forwarded=0 always holds: misaligned slot registers are refused
+    before any device work (the pointers are never dereferenced)."""
+    from ina_amd import _lib
+    lib = _lib.load()
+    fake = 1 << 20                                   # aligned, never touched
+    st = _lib.SwitchState(64, 32, 1, 0, fake, fake, fake + 8)
+    rc = lib.ina_switch_process_apply(ctypes.byref(st), fake, 4, 144, fake, fake, 1, fake, 16, 0.5,
+                                      fake, 64, None, 144, 0, None)
+    assert rc == _lib.INA_EINVAL
+    assert b"registers" in lib.ina_last_error_string()

@@ -68,6 +68,29 @@ def test_communicator_thread_fanout_matches_reference_packets():
     assert sorted(got) == sorted(pkts)
 
 
+@pytest.mark.parametrize("fanout", ["multi_process_send", "multi_process_send_futures_P"])
+def test_communicator_process_fanout_after_gpu_use(fanout):
+    """The process fan-outs after the parent has initialised HIP (a device op first):
+    workers are spawned, not forked, and send on the parent's socket; the
+    packets equal the reference's captured bytes."""
+    from ina_amd import communicator as cm
+    from ina_amd import ops
+    ops.checksum(torch.arange(1024, dtype=torch.int32, device="cuda"))   # HIP is live here
+    torch.cuda.synchronize()
+    data, pkts = load_capture("c128_threads3_1000.bin")
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    b.settimeout(60)
+    try:
+        cm.send_fd = a.fileno()
+        getattr(cm, fanout)(3, data)
+        got = _drain(b, len(pkts))
+    finally:
+        cm.send_fd = None
+        a.close()
+        b.close()
+    assert sorted(got) == sorted(pkts)
+
+
 def _model_with(vec):
     class M(torch.nn.Module):
         def __init__(self):

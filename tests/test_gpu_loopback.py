@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 
 K = 16
 SIZES = {"small": (100, 1000), "big": (100, 6000)}   # big: 606,000 params -> 18,938 NGA-32 packets
+PARA_LEN = 25_557_032          # ResNet-50, communicator.py:11 (config 1's model size)
 
 
 def make_small():
@@ -28,6 +29,20 @@ def make_small():
 
 def make_big():
     return torch.nn.Linear(*SIZES["big"])
+
+
+class FlatResNet50(torch.nn.Module):
+    """Config 1 at its size: ResNet-50's 25,557,032 parameters as ONE flat Parameter --
+    aggregate() sees only parameters_to_vector (launch.py:42-52), so the layer layout
+    does not change the aggregation path."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(50)
+        self.flat = torch.nn.Parameter(torch.randn(PARA_LEN, generator=g) * 0.05)
+
+
+MAKERS = {"small": make_small, "big": make_big, "resnet50": FlatResNet50}
 
 
 def noise(idx, epoch, n):
@@ -47,7 +62,7 @@ def _worker(idx, W, port, path, size):
         if p not in sys.path:
             sys.path.insert(0, p)
     from ina_amd.loopback import worker_serve
-    worker_serve(idx, W, port, path, make_big if size == "big" else make_small, train_step)
+    worker_serve(idx, W, port, path, MAKERS[size], train_step)
 
 
 def _free_port():
@@ -56,14 +71,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("V,size", [(256, "small"), (32, "small"), (32, "big")])
-def test_loopback_two_workers_bit_exact(V, size):
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("V,size,epochs", [(256, "small", 3), (32, "small", 3), (32, "big", 3),
+                                           (256, "resnet50", 2), (32, "resnet50", 2)])
+def test_loopback_two_workers_bit_exact(V, size, epochs):
+    """resnet50: config 1 at its size -- 25,557,032 parameters, W = 2 -> 2 x 99,833
+    NGA-256 (or 2 x 798,657 NGA-32) packets per epoch through recvmmsg and the device
+    switch, every epoch bit-exact against the oracle."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from ina_amd.loopback import ps_serve
-    W, epochs = 2, 3
+    W = 2
     torch.manual_seed(0)
-    model = (make_big if size == "big" else make_small)().cuda()
+    model = MAKERS[size]().cuda()
     local0 = torch.nn.utils.parameters_to_vector(model.parameters()).detach().cpu().numpy()
     port = _free_port()
     seen = []
@@ -82,7 +102,7 @@ def test_loopback_two_workers_bit_exact(V, size):
         time.sleep(1.0)
         for p in procs:
             p.start()
-        th.join(timeout=240)
+        th.join(timeout=420 if size == "resnet50" else 240)
         for p in procs:
             p.join(timeout=60)
         assert not th.is_alive()

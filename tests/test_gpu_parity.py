@@ -717,6 +717,44 @@ def test_switch_process_apply_equals_two_steps(V, W, per, tail, keep):
     assert np.array_equal(c0, c1) and np.array_equal(f0, f1) and np.array_equal(r0, r1)
 
 
+@pytest.mark.parametrize("V,W,per", [(32, 4, 300), (256, 8, 70)])
+def test_process_apply_packets_outside_the_bucket_are_forwarded(V, W, per):
+    """keep_forwarded=False consumes only the completed packets the PS takes (frag_id -
+    seq0 inside the bucket); a completed packet outside it is forwarded with its slot sum
+    exactly as ina_switch_process forwards it (the fused kernel used to leave
+    such packets as they arrived)."""
+    o = ops()
+    n = V * per
+    stride = o.nga_stride(V)
+    g = np.random.default_rng(V + W)
+    q = [rand_i32(g, n, full=False) for _ in range(W)]
+    half = per // 2
+    seq_apply = 7 + half                    # packets 0..half-1 fall before the bucket
+    local = dev(np.random.default_rng(1).standard_normal(n).astype(np.float32))
+    res = {}
+    for fused in (False, True):
+        rows = torch.cat([o.pack_nga(dev(b), V, w + 1, W, 1, 7, num_slots=1 << 13) for w, b in enumerate(q)])
+        before = host(rows).copy()
+        sw = o.Switch(V, num_slots=1 << 13, switch_id=1, device=DEV)
+        out = torch.full_like(local, float("nan"))
+        if fused:
+            act, _ = sw.process_apply(rows, seq_apply, local, 16, 0.25, out=out, keep_forwarded=False)
+        else:
+            act = sw.process(rows)
+            o.apply_completed(rows, act, V, seq_apply, local, 16, 0.25, out=out)
+        res[fused] = (host(act), host(rows).copy(), host(out).view(np.uint32), before)
+    (a0, p0, u0, _), (a1, p1, u1, b1) = res[False], res[True]
+    assert np.array_equal(a0, a1) and np.array_equal(u0, u1)
+    done = np.nonzero(a1 == orc.ACT_FWD_AGG)[0]
+    assert done.size == per
+    frag = np.array([int.from_bytes(bytes(b1[p, 11:15]), "big") for p in done])
+    inside = frag - seq_apply >= 0
+    assert inside.sum() == per - half and (~inside).sum() == half
+    assert np.array_equal(p1[done[inside]], b1[done[inside]])     # consumed: as they arrived
+    assert np.array_equal(p1[done[~inside]], p0[done[~inside]])   # forwarded: slot sums
+    assert not np.array_equal(p0[done[~inside]], b1[done[~inside]])
+
+
 @pytest.mark.parametrize("V,W,per", [(32, 4, 3000), (256, 8, 700)])
 def test_steady_state_acks_ride_with_next_step(V, W, per):
     """Steady-state packet path: step t's PS acks sit in front of step t+1's worker packets
