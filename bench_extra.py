@@ -174,22 +174,28 @@ def run_extra(dev):
 
     # --- packet-stream switch: 8 workers x 100 MiB as NGA-256 packets ------------------------
     Ws = 8
-    stream = torch.cat([ops.pack_nga(b3[w], V, w + 1, Ws, 1, 1, num_slots=1 << 17) for w in range(Ws)])
+    packed = [ops.pack_nga(b3[w], V, w + 1, Ws, 1, 1, num_slots=1 << 17, desc=True) for w in range(Ws)]
+    stream = torch.cat([p for p, _ in packed])
+    desc_all = torch.cat([d for _, d in packed])      # the pack kernels' packet descriptors
+    del packed
     sw = ops.Switch(V, num_slots=1 << 17, switch_id=1, device=dev)
     acts = torch.empty(stream.shape[0], dtype=torch.uint8, device=dev)
 
     # replaying the same stream repeats the same work: every slot completes (count back to
     # 0) and keeps its frag id, so no state reset sits inside the timed region
-    def sw_round():
-        sw.process(stream, acts)
     # algorithmic bytes: every packet read once, the forwarded (completing) 1/Ws of them
     # written back, each touched slot's V registers, count and frag written once (a slot's
     # registers are read only when a packet adds to a stored value -- never here, every
     # slot starts with count_reg == 1), one action byte per packet
     npk_all = stream.shape[0]
-    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort)",
-                     _time(sw_round, reps=5, warm=1),
-                     stream.numel() + stream.numel() // Ws + npk * (V * 4 + 5) + npk_all))
+    sw_bytes = stream.numel() + stream.numel() // Ws + npk * (V * 4 + 5) + npk_all
+    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from descriptors)",
+                     _time(lambda: sw.process(stream, acts, desc=desc_all), reps=5, warm=1), sw_bytes,
+                     note="the pack kernels' 8-byte packet descriptors feed the slot sort "
+                          "(ina_switch_process_desc)"))
+    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from headers)",
+                     _time(lambda: sw.process(stream, acts), reps=5, warm=1), sw_bytes,
+                     note="ina_switch_process: the key pass reads each packet's header line"))
     # PS side, fused, on the switch's output: completed slots -> dequantise -> update + acks
     sw.process(stream, acts)
     local3 = rnd_f32(n3)
@@ -211,11 +217,13 @@ def run_extra(dev):
     ack_acts = torch.empty(npk, dtype=torch.uint8, device=dev)
     rows_w = stream.view(Ws, npk, stream.shape[1])
 
+    desc_w = desc_all.view(Ws, npk)
+
     def ina_step():
         for w in range(Ws):
             ops.quantize_pack_nga(xs[w], 16, V, w + 1, Ws, 1, 1, base=glob_p, num_slots=1 << 17,
-                                  out=rows_w[w])
-        sw.process(stream, acts)
+                                  out=rows_w[w], desc=desc_w[w])
+        sw.process(stream, acts, desc=desc_all)
         ops.apply_completed(stream, acts, V, 1, glob_p, 16, 1.0 / (Ws + 1), out=upd, acks=acks)
         sw.process(acks, ack_acts)
     t = _time(ina_step, reps=5, warm=1)
@@ -232,7 +240,7 @@ def run_extra(dev):
                      note="bytes = the sum of the four stages' algorithmic HBM bytes (so frac is the "
                           "path's roofline fraction); aggregated_GBps = worker fp32 bytes aggregated "
                           "per second through the packet path"))
-    del acks, ack_acts, rows_w, stream
+    del acks, ack_acts, rows_w, stream, desc_w, desc_all
 
     # steady state: the PS's acks for step t reach the switch in the same batch as the
     # workers' packets for step t+1, in front of them (the ack frees the slot before the
@@ -241,12 +249,15 @@ def run_extra(dev):
     ack_rows, rows_w2 = big[:npk], big[npk:].view(Ws, npk, row_b)
     acts2 = torch.empty((Ws + 1) * npk, dtype=torch.uint8, device=dev)
     sw2 = ops.Switch(V, num_slots=1 << 17, switch_id=1, device=dev)
+    desc_big = torch.empty((Ws + 1) * npk, dtype=torch.int64, device=dev)   # [acks | 8 workers]
+    desc_ack, desc_w2 = desc_big[:npk], desc_big[npk:].view(Ws, npk)
 
     def ina_step_steady():
         for w in range(Ws):
             ops.quantize_pack_nga(xs[w], 16, V, w + 1, Ws, 1, 1, base=glob_p, num_slots=1 << 17,
-                                  out=rows_w2[w])
-        sw2.process(big, acts2)
+                                  out=rows_w2[w], desc=desc_w2[w])
+        ops.nga_descriptors(ack_rows, out=desc_ack)          # the PS's ack rows
+        sw2.process(big, acts2, desc=desc_big)
         ops.apply_completed(big, acts2, V, 1, glob_p, 16, 1.0 / (Ws + 1), out=upd, acks=ack_rows)
     ina_step_steady()                      # first step: the ack rows are zero (another switch's)
     t = _time(ina_step_steady, reps=5, warm=1)
@@ -266,9 +277,10 @@ def run_extra(dev):
     def ina_step_fused():
         for w in range(Ws):
             ops.quantize_pack_nga(xs[w], 16, V, w + 1, Ws, 1, 1, base=glob_p, num_slots=1 << 17,
-                                  out=rows_w2[w])
+                                  out=rows_w2[w], desc=desc_w2[w])
+        ops.nga_descriptors(ack_rows, out=desc_ack)
         sw3.process_apply(big, 1, glob_p, 16, 1.0 / (Ws + 1), out=upd, acks=ack_rows,
-                          keep_forwarded=False, actions=acts2)
+                          keep_forwarded=False, actions=acts2, desc=desc_big)
     ina_step_fused()
     t = _time(ina_step_fused, reps=5, warm=1)
     ina_step_fused()
@@ -280,7 +292,7 @@ def run_extra(dev):
                      acks_and_slots_ok=ok,
                      note="ina_switch_process_apply(keep_forwarded=0): bytes = the steady-state row's "
                           "minus the PS's re-read of completed packets and their write-back"))
-    del xs, glob_p, upd, big, ack_rows, rows_w2, acts2, sw2, sw3
+    del xs, glob_p, upd, big, ack_rows, rows_w2, acts2, sw2, sw3, desc_big, desc_ack, desc_w2
 
     # small batches through the switch (P4 format: NGA-32, 16,384-slot pool): latency of
     # one ina_switch_process call, the stand-in's per-batch cost when packets arrive in

@@ -18,6 +18,8 @@ int set_h2d_streams(int v);   // ina_host.cpp
 int set_small_sort(int v);    // ina_switch.hip
 int set_switch_win(int v);    // ina_switch.hip
 int set_ack_fast(int v);      // ina_switch.hip
+int set_sort_mode(int v);     // ina_switch.hip
+int set_os_rounds(int v);     // ina_switch.hip
 
 }  // namespace ina
 

@@ -890,7 +890,8 @@ template <typename Src, int U>
 __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, NgaHdr h,
                                                           const uint8_t* __restrict__ ovf,
                                                           uint8_t* __restrict__ pkts, uint32_t C,
-                                                          uint32_t L, uint32_t nch) {
+                                                          uint32_t L, uint32_t nch,
+                                                          u32x2* __restrict__ desc) {
     const uint32_t gs = gridDim.x * kBlock;
     const int lane = threadIdx.x & 63;
     const uint32_t wave0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
@@ -939,6 +940,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, Nga
                 o.y = count | (flags << 8) | (bi << 16);
                 o.z = (bi >> 16) | (sw << 16) | (bf << 24);
                 o.w = (bf >> 8) | (nx & 0xFF000000u);        // value 0's top byte at byte 15
+                if (desc) desc[p] = u32x2{o.y, o.z};          // header bytes 4..11 (ina.h)
             } else if (c <= L) {
                 o.x = __builtin_amdgcn_perm(v[u].y, v[u].x, kSelWire);
                 o.y = __builtin_amdgcn_perm(v[u].z, v[u].y, kSelWire);
@@ -976,6 +978,26 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_bytes(Src src, size_t n,
             out = (uint8_t)(nga_val(src, n, p, V, (long)(q / 4)) >> (24 - 8 * (q % 4)));
         }
         pkts[g] = out;
+    }
+}
+
+// packet descriptors (include/ina.h): header bytes 4..11 of each packet, gathered; one
+// 8-byte result per lane, two dword loads when rows are 4-byte aligned
+__global__ __launch_bounds__(kBlock) void k_nga_desc(const uint8_t* __restrict__ pkts, size_t npk,
+                                                     size_t pstride, uint64_t* __restrict__ desc) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const bool al4 = (pstride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0;
+    for (size_t p = (size_t)blockIdx.x * kBlock + threadIdx.x; p < npk; p += gs) {
+        const uint8_t* pk = pkts + p * pstride;
+        uint64_t d;
+        if (al4) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(pk);
+            d = (uint64_t)w[1] | ((uint64_t)w[2] << 32);
+        } else {
+            d = 0;
+            for (int b = 0; b < 8; ++b) d |= (uint64_t)pk[4 + b] << (8 * b);
+        }
+        desc[p] = d;
     }
 }
 
@@ -1330,7 +1352,8 @@ static int fill_pack(PtrPack<T>& pk, const T* const* bufs, int W, bool& all_alig
 
 template <typename Src>
 static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina_nga_params_t* prm,
-                           const uint8_t* ovf, uint8_t* pkts, size_t pstride, hipStream_t s) {
+                           const uint8_t* ovf, uint8_t* pkts, size_t pstride, hipStream_t s,
+                           uint64_t* desc = nullptr) {
     if (!prm || prm->V <= 0 || prm->num_slots == 0)
         return set_error(INA_EINVAL, "bad nga params%s", "");
     const int V = prm->V;
@@ -1352,12 +1375,16 @@ static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina
             hp.seq0 = h.seq0 + (uint32_t)p0;
             hipLaunchKernelGGL((k_pack_nga_flat<Src, INA_PACK_U>), dim3(grid_for(np * C, INA_PACK_U, g_stream_blocks)),
                                dim3(kBlock), 0, s, src.shifted(v0), n - v0, hp, ovf ? ovf + p0 : nullptr,
-                               pkts + p0 * pstride, (uint32_t)C, (uint32_t)(V / 4), (uint32_t)(np * C));
+                               pkts + p0 * pstride, (uint32_t)C, (uint32_t)(V / 4), (uint32_t)(np * C),
+                               desc ? reinterpret_cast<u32x2*>(desc + p0) : nullptr);
         }
     } else {
         size_t nbytes = npk * pstride;
         hipLaunchKernelGGL(k_pack_nga_bytes<Src>, dim3(grid_for(nbytes, 1)), dim3(kBlock), 0, s, src, n,
                            h, ovf, pkts, pstride, nbytes);
+        if (desc)   // the generic layout gathers its descriptors from the written headers
+            hipLaunchKernelGGL(k_nga_desc, dim3(grid_for(npk, 1)), dim3(kBlock), 0, s, pkts, npk, pstride,
+                               desc);
     }
     return check_launch("pack_nga");
 }
@@ -1381,6 +1408,8 @@ int ina_set_tuning(int key, int value) {
         case 9: return set_small_sort(value);
         case 10: return set_switch_win(value);
         case 11: return set_ack_fast(value);
+        case 12: return set_sort_mode(value);
+        case 13: return set_os_rounds(value);
         default: return INA_EINVAL;
     }
 }
@@ -1588,20 +1617,44 @@ int ina_ps_combine_ina_f32(const float* local, const float* const* paras, int W,
     return check_launch("ps_combine_ina_f32");
 }
 
+int ina_pack_nga_desc(const int32_t* vals, size_t n, const ina_nga_params_t* prm, const uint8_t* ovf,
+                      uint8_t* pkts, size_t pstride, ina_nga_desc_t* desc, ina_stream_t stream) {
+    if (n && !vals) return set_error(INA_EINVAL, "null pointer%s", "");
+    if (desc && ((uintptr_t)desc & 7u)) return set_error(INA_EINVAL, "descriptors must be 8-byte aligned%s", "");
+    return pack_nga_launch(SrcI32{vals}, aligned16(vals), n, prm, ovf, pkts, pstride, hs(stream), desc);
+}
+
 int ina_pack_nga(const int32_t* vals, size_t n, const ina_nga_params_t* prm, const uint8_t* ovf,
                  uint8_t* pkts, size_t pstride, ina_stream_t stream) {
-    if (n && !vals) return set_error(INA_EINVAL, "null pointer%s", "");
-    return pack_nga_launch(SrcI32{vals}, aligned16(vals), n, prm, ovf, pkts, pstride, hs(stream));
+    return ina_pack_nga_desc(vals, n, prm, ovf, pkts, pstride, nullptr, stream);
+}
+
+int ina_quantize_pack_nga_desc(const float* x, const float* base, size_t n, int k,
+                               const ina_nga_params_t* prm, uint8_t* pkts, size_t pstride,
+                               ina_nga_desc_t* desc, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (n && !x) return set_error(INA_EINVAL, "null pointer%s", "");
+    if (desc && ((uintptr_t)desc & 7u)) return set_error(INA_EINVAL, "descriptors must be 8-byte aligned%s", "");
+    bool al = aligned16(x) && (!base || aligned16(base));
+    return pack_nga_launch(SrcQ32{x, base, ldexpf(1.0f, k)}, al, n, prm, nullptr, pkts, pstride,
+                           hs(stream), desc);
 }
 
 int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
                           const ina_nga_params_t* prm, uint8_t* pkts, size_t pstride,
                           ina_stream_t stream) {
-    if (int rc = check_k(k)) return rc;
-    if (n && !x) return set_error(INA_EINVAL, "null pointer%s", "");
-    bool al = aligned16(x) && (!base || aligned16(base));
-    return pack_nga_launch(SrcQ32{x, base, ldexpf(1.0f, k)}, al, n, prm, nullptr, pkts, pstride,
-                           hs(stream));
+    return ina_quantize_pack_nga_desc(x, base, n, k, prm, pkts, pstride, nullptr, stream);
+}
+
+int ina_nga_descriptors(const uint8_t* pkts, size_t npk, size_t pstride, ina_nga_desc_t* desc,
+                        ina_stream_t stream) {
+    if (pstride < (size_t)INA_NGA_HDR_BYTES) return set_error(INA_EINVAL, "stride < 15%s", "");
+    if (npk == 0) return INA_OK;
+    if (!pkts || !desc) return set_error(INA_EINVAL, "null pointer%s", "");
+    if ((uintptr_t)desc & 7u) return set_error(INA_EINVAL, "descriptors must be 8-byte aligned%s", "");
+    hipLaunchKernelGGL(k_nga_desc, dim3(grid_for(npk, 1)), dim3(kBlock), 0, hs(stream), pkts, npk, pstride,
+                       desc);
+    return check_launch("nga_descriptors");
 }
 
 int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,

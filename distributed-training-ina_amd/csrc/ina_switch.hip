@@ -112,12 +112,76 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
+// LDS digit count from every lane of a wave (call convergent; `valid` masks lanes out).
+// Neighbouring packets usually share their higher digits (a worker's consecutive slots),
+// and 64 same-address LDS atomics serialise, so a wave whose valid lanes all hold one
+// digit adds its popcount once.
+__device__ __forceinline__ void lds_count(uint32_t* h, uint32_t d, bool valid) {
+    const unsigned long long act = __ballot(valid);
+    if (!act) return;
+    const int first = __builtin_ctzll(act);
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, first);
+    const unsigned long long same = __ballot(valid && d == d0);
+    if (same == act) {
+        if ((int)(threadIdx.x & 63) == first) atomicAdd(&h[d0], (uint32_t)__builtin_popcountll(act));
+    } else if (valid) {
+        atomicAdd(&h[d], 1u);
+    }
+}
+
+// Stable scatter of one sort tile (both sort paths): on entry base[w][d] holds wave w's
+// count of digit d and gst[d] the tile's first output position for digit d; an item goes
+// to gst[d] + the counts of its digit in earlier waves and rounds + its rank among this
+// round's lanes with the same digit (ballots over the digit's bits).  Staging the tile in
+// LDS first, so each digit leaves as one contiguous run, measured no faster (pass 0
+// 15.1 -> 17.9 us, pass 1 17.9 -> 17.3 us at 819,200 packets: the passes are bound by
+// their dependent phases, not by the scattered stores; profiles/r02/lab/switch_sort_lab)
+template <int R>
+__device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const uint32_t (&v)[R],
+                                                size_t i0, size_t n, int shift, int bits,
+                                                uint32_t (*base)[kRsBins], const uint32_t* gst,
+                                                uint32_t* __restrict__ kout,
+                                                uint32_t* __restrict__ vout) {
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const uint32_t nb = 1u << bits;
+    constexpr int kDPT = kRsBins / kRsBlock;
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        if (d >= nb) continue;
+        uint32_t b = gst[d];
+#pragma unroll
+        for (int w = 0; w < kRsWaves; ++w) {
+            const uint32_t cw = base[w][d];
+            base[w][d] = b;
+            b += cw;
+        }
+    }
+    __syncthreads();
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (i0 - (size_t)lane + (size_t)r * 64 >= n) break;      // wave-uniform
+        const bool valid = i0 + (size_t)r * 64 < n;
+        const uint32_t d = (k[r] >> shift) & (nb - 1);
+        const unsigned long long pm = lanes_with_digit(d, bits, valid);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(pm & below);
+        const uint32_t b0 = base[wv][d];
+        if (valid) {
+            kout[b0 + rank] = k[r];
+            vout[b0 + rank] = v[r];
+            if (rank == 0) base[wv][d] = b0 + (uint32_t)__builtin_popcountll(pm);
+        }
+    }
+}
+
 // 1. keys: aggregator slot of each packet, or num_slots (sorts last) for packets that
 //    are not this switch's (switch_check miss, ngaa.p4:27-37,184-186); fused with the
 //    first digit pass's chunk histogram.
 constexpr uint32_t kAckBit = 0x80000000u;
-template <int R>
+template <int R, bool kDesc>
 __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restrict__ pkts,
+                                                          const uint2* __restrict__ desc,
                                                           size_t npk, size_t stride,
                                                           uint32_t num_slots, int switch_id,
                                                           uint32_t* __restrict__ keys,
@@ -132,7 +196,16 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
     __syncthreads();
     const size_t p0 = c * (kRsWaves * 64 * R) + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t idx[R], sid[R], ack[R];
-    if ((stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0) {   // header bytes 4..11
+    if (kDesc) {                                               // descriptors: header bytes 4..11
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t p = p0 + (size_t)r * 64;
+            const uint2 d = p < npk ? desc[p] : uint2{0u, 0u};
+            idx[r] = __builtin_bswap32((d.x >> 16) | (d.y << 16));
+            sid[r] = (d.y >> 16) & 0xFFu;
+            ack[r] = (d.x >> 14) & 1u;
+        }
+    } else if ((stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0) {   // header bytes 4..11
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const size_t p = p0 + (size_t)r * 64;
@@ -158,14 +231,14 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const size_t p = p0 + (size_t)r * 64;
+        const bool mine = switch_id >= 0 && sid[r] == (uint32_t)(uint8_t)switch_id;
+        const uint32_t key = mine ? idx[r] % num_slots : num_slots;
         if (p < npk) {
-            const bool mine = switch_id >= 0 && sid[r] == (uint32_t)(uint8_t)switch_id;
-            const uint32_t key = mine ? idx[r] % num_slots : num_slots;
             // bit 31 carries "PS ack" through the sort (the digit passes never read it)
             keys[p] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
             if (!mine) actions[p] = INA_ACT_FWD_OTHER;
-            atomicAdd(&h[key & (nb - 1)], 1u);
         }
+        lds_count(h, key & (nb - 1), p < npk);
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
@@ -185,6 +258,18 @@ constexpr int kSmallBlock = 1024;
 static std::atomic<int> g_small_sort{1};   // ina_set_tuning key 9 (0: always the radix path)
 static std::atomic<int> g_switch_win{0};   // ina_set_tuning key 10: run-kernel window (0: auto)
 static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack lane path (0: off)
+static std::atomic<int> g_sort_mode{0};    // ina_set_tuning key 12: 0 hist/colscan/scatter passes, 1 one-sweep
+static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: one-sweep tile rounds (0 auto, 4/8/16)
+int set_sort_mode(int v) {
+    if (v != 0 && v != 1) return INA_EINVAL;
+    g_sort_mode = v;
+    return INA_OK;
+}
+int set_os_rounds(int v) {
+    if (v != 0 && v != 4 && v != 8 && v != 16) return INA_EINVAL;
+    g_os_rounds = v;
+    return INA_OK;
+}
 int set_ack_fast(int v) {
     g_ack_fast = v ? 1 : 0;
     return INA_OK;
@@ -278,8 +363,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_hist(const uint32_t* __restrict
 #pragma unroll
     for (int r = 0; r < R; ++r) k[r] = i0 + (size_t)r * 64 < n ? keys[i0 + (size_t)r * 64] : 0u;
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (i0 + (size_t)r * 64 < n) atomicAdd(&h[(k[r] >> shift) & (nb - 1)], 1u);
+    for (int r = 0; r < R; ++r) lds_count(h, (k[r] >> shift) & (nb - 1), i0 + (size_t)r * 64 < n);
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
 }
@@ -329,7 +413,8 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
     const uint32_t nb = 1u << bits;
-    const size_t i0 = c * (kRsWaves * 64 * R) + (size_t)wv * (64 * R) + (size_t)lane;
+    const size_t tile0 = c * (kRsWaves * 64 * R);
+    const size_t i0 = tile0 + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t k[R], v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -352,10 +437,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
         const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
         if (d < nb) dbase[d] = tot[j];
     }
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r)              // this wave's digit counts
-        if (i0 + (size_t)r * 64 < n) atomicAdd(&base[wv][(k[r] >> shift) & (nb - 1)], 1u);
-    __syncthreads();
+        lds_count(base[wv], (k[r] >> shift) & (nb - 1), i0 + (size_t)r * 64 < n);
     if (wv == 0) {                                   // digit bases: exclusive scan of the totals
         uint32_t carry = 0;
         for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
@@ -368,33 +453,187 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kDPT; ++j) {
+    for (int j = 0; j < kDPT; ++j) {                 // the tile's first output position per digit
         const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
-        if (d >= nb) continue;
-        uint32_t b = dbase[d] + cpf[j];
-#pragma unroll
-        for (int w = 0; w < kRsWaves; ++w) {
-            const uint32_t cw = base[w][d];
-            base[w][d] = b;
-            b += cw;
-        }
+        if (d < nb) dbase[d] += cpf[j];
     }
     __syncthreads();
-    const unsigned long long below = (1ull << lane) - 1ull;
+    rs_tile_scatter<R>(k, v, i0, n, shift, bits, base, dbase, kout, vout);
+}
+
+// ---- one-sweep slot sort (ina_set_tuning key 12 = 1; measured slower, kept for the lab)
+// The same stable LSD digit passes, without the per-pass histogram and column-scan
+// launches: the key pass also counts every pass's digits (one global histogram per pass,
+// LDS counts then one atomic per nonzero bin and block), and each digit pass is ONE
+// kernel whose blocks take tiles in ticket order (an atomic counter, so every tile a block
+// waits for has already started) and find their tile's offset per digit by decoupled
+// look-back over the earlier tiles' published counts.  Status word per (tile, digit):
+// bits 31..30 = 1 aggregate of the tile alone, 2 inclusive prefix through the tile; bits
+// 29..0 the count.  A word is self-contained (one 4-byte store), so the hand-off needs no
+// ordering: agent-scope stores (write-through) and agent-scope relaxed loads polled by the
+// waiting lanes (MI355X_MICROARCH.md, inter-workgroup visibility).  Launches per batch:
+// memset + keys + one per digit pass (2 at <= 2^18 slots) -- 4 instead of 6.  Measured at
+// 819,200 NGA-256 packets (profiles/r02/lab): each pass 26.5-27.8 us at 4,096-item tiles
+// (44 us at 1,024) against 17-18 us per scatter + 5-6 us per histogram / column scan:
+// 512 digits per tile make every tile's look-back a chain of dependent agent-scope polls,
+// so the launches it saves cost more than they did.
+constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsCnt = (1u << 30) - 1u;
+constexpr int kOsMaxPasses = 4;
+
+__device__ __forceinline__ void os_publish(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t os_poll(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// keys (slot, foreign sentinel, PS-ack bit 31) + every pass's global digit histogram, from
+// the packet headers or from the batch's descriptors (header bytes 4..11, include/ina.h)
+template <bool kDesc>
+__global__ __launch_bounds__(kRsBlock) void k_switch_keys_os(const uint8_t* __restrict__ pkts,
+                                                             const uint2* __restrict__ desc,
+                                                             size_t npk, size_t stride,
+                                                             uint32_t num_slots, int switch_id,
+                                                             uint32_t* __restrict__ keys,
+                                                             uint8_t* __restrict__ actions,
+                                                             int passes, int bits,
+                                                             uint32_t* __restrict__ ghist,
+                                                             int ack_hint) {
+    __shared__ uint32_t h[kOsMaxPasses * kRsBins];
+    const uint32_t nb = 1u << bits;
+    for (uint32_t d = threadIdx.x; d < (uint32_t)passes * nb; d += kRsBlock) h[d] = 0;
+    __syncthreads();
+    const bool al4 = (stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0;
+    const size_t gs = (size_t)gridDim.x * kRsBlock;
+    const size_t tid = (size_t)blockIdx.x * kRsBlock + threadIdx.x;
+    for (size_t w0 = tid & ~(size_t)63; w0 < npk; w0 += gs) {       // wave-uniform trip count
+        const size_t p = w0 + (threadIdx.x & 63);
+        const bool valid = p < npk;
+        uint32_t idx = 0, sid = 0, ack = 0;
+        if (!valid) {
+        } else if (kDesc) {
+            const uint2 d = desc[p];
+            idx = __builtin_bswap32((d.x >> 16) | (d.y << 16));
+            sid = (d.y >> 16) & 0xFFu;
+            ack = (d.x >> 14) & 1u;                                  // flags byte 5, bit 6
+        } else if (al4) {
+            const uint32_t* pk = reinterpret_cast<const uint32_t*>(pkts + p * stride);
+            const uint32_t w1 = pk[1], w2 = pk[2];
+            idx = __builtin_bswap32((w1 >> 16) | (w2 << 16));
+            sid = (w2 >> 16) & 0xFFu;
+            ack = (w1 >> 14) & 1u;
+        } else {
+            idx = rd_be32(pkts + p * stride + 6);
+            sid = pkts[p * stride + 10];
+            ack = (pkts[p * stride + 5] >> 6) & 1u;
+        }
+        const bool mine = switch_id >= 0 && sid == (uint32_t)(uint8_t)switch_id;
+        const uint32_t key = mine ? idx % num_slots : num_slots;
+        if (valid) {
+            keys[p] = key | ((ack_hint && mine && ack) ? kAckBit : 0u);
+            if (!mine) actions[p] = INA_ACT_FWD_OTHER;               // ngaa.p4:184-186
+        }
+        for (int q = 0; q < passes; ++q) lds_count(h + q * nb, (key >> (q * bits)) & (nb - 1), valid);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < (uint32_t)passes * nb; d += kRsBlock)
+        if (h[d]) atomicAdd(&ghist[d], h[d]);
+}
+
+// one digit pass: tile = 4 waves x 64 x R items, wave w owns the tile's w-th quarter in
+// rounds of 64 (the layout and in-round ballot ranks of k_rs_scatter)
+template <bool kIds, int R>
+__global__ __launch_bounds__(kRsBlock) void k_rs_onesweep(const uint32_t* __restrict__ kin,
+                                                          const uint32_t* __restrict__ vin,
+                                                          uint32_t* __restrict__ kout,
+                                                          uint32_t* __restrict__ vout, size_t n,
+                                                          int shift, int bits,
+                                                          const uint32_t* __restrict__ ghist,
+                                                          uint32_t* __restrict__ ticket,
+                                                          uint32_t* __restrict__ status) {
+    __shared__ uint32_t base[kRsWaves][kRsBins];   // per-wave counts, then per-wave bases
+    __shared__ uint32_t dbase[kRsBins];            // global digit base (scan of ghist)
+    __shared__ uint32_t tile_s;
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const uint32_t nb = 1u << bits;
+    if (threadIdx.x == 0) tile_s = atomicAdd(ticket, 1u);
+    for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
+    __syncthreads();
+    const size_t c = __builtin_amdgcn_readfirstlane(tile_s);
+    const size_t tile0 = c * (kRsWaves * 64 * R);
+    const size_t i0 = tile0 + (size_t)wv * (64 * R) + (size_t)lane;
+    uint32_t k[R], v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (i0 - (size_t)lane + (size_t)r * 64 >= n) break;      // wave-uniform
-        const bool valid = i0 + (size_t)r * 64 < n;
-        const uint32_t d = (k[r] >> shift) & (nb - 1);
-        const unsigned long long pm = lanes_with_digit(d, bits, valid);
-        const uint32_t rank = (uint32_t)__builtin_popcountll(pm & below);
-        const uint32_t b0 = base[wv][d];
-        if (valid) {
-            kout[b0 + rank] = k[r];
-            vout[b0 + rank] = v[r];
-            if (rank == 0) base[wv][d] = b0 + (uint32_t)__builtin_popcountll(pm);
+        const size_t i = i0 + (size_t)r * 64;
+        k[r] = i < n ? kin[i] : 0u;
+        v[r] = kIds ? (i < n ? vin[i] : 0u) : (uint32_t)i;
+    }
+    constexpr int kDPT = kRsBins / kRsBlock;         // digits per thread
+    uint32_t gh[kDPT];
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        gh[j] = d < nb ? ghist[d] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)              // this wave's digit counts
+        lds_count(base[wv], (k[r] >> shift) & (nb - 1), i0 + (size_t)r * 64 < n);
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        if (d < nb) dbase[d] = gh[j];
+    }
+    __syncthreads();
+    // publish this tile's counts, then look back for its offsets (my digits)
+    uint32_t cnt[kDPT], excl[kDPT];
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        cnt[j] = 0;
+        if (d < nb) {
+#pragma unroll
+            for (int w = 0; w < kRsWaves; ++w) cnt[j] += base[w][d];
+            os_publish(status + c * nb + d, (c == 0 ? kOsInc : kOsAgg) | cnt[j]);
         }
     }
+    if (wv == 0) {                                   // digit bases: exclusive scan of ghist
+        uint32_t carry = 0;
+        for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
+            const uint32_t d = d0 + (uint32_t)lane;
+            const uint32_t t = d < nb ? dbase[d] : 0u;
+            const uint32_t inc = wave_incl_scan(t);
+            if (d < nb) dbase[d] = carry + inc - t;
+            carry += __builtin_amdgcn_readlane(inc, 63);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        excl[j] = 0;
+        if (d < nb && c > 0) {
+            size_t t = c - 1;
+            for (;;) {
+                const uint32_t sv = os_poll(status + t * nb + d);
+                if ((sv >> 30) == 0u) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl[j] += sv & kOsCnt;
+                if ((sv >> 30) == 2u || t == 0) break;
+                --t;
+            }
+            os_publish(status + c * nb + d, kOsInc | (excl[j] + cnt[j]));
+        }
+    }
+    __syncthreads();                                  // dbase scanned, base[][] counts final
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {                 // the tile's first output position per digit
+        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        if (d < nb) dbase[d] += excl[j];
+    }
+    __syncthreads();
+    rs_tile_scatter<R>(k, v, i0, n, shift, bits, base, dbase, kout, vout);
 }
 
 // 2. one wave per slot segment of the sorted stream
@@ -853,6 +1092,22 @@ static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
     return align_up(hist * 4, 256) + align_up((size_t)kRsBins * 4, 256);
 }
 
+// one-sweep sort's auxiliary words, zeroed by one memset per batch: global digit
+// histograms [kOsMaxPasses][512], tickets (one per pass), status [passes][tiles][2^bits]
+constexpr size_t kOsHistBytes = (size_t)kOsMaxPasses * kRsBins * 4;
+constexpr int kOsMinRounds = 4;
+static size_t os_tiles(size_t npk, int rounds) {
+    const size_t tile = (size_t)kRsWaves * 64 * (size_t)rounds;
+    return (npk + tile - 1) / tile;
+}
+static size_t os_aux_bytes(size_t npk, const SortPlan& p, int rounds) {
+    return kOsHistBytes + 256 + (size_t)p.passes * os_tiles(npk, rounds) * ((size_t)1 << p.bits) * 4;
+}
+static int os_rounds_for(size_t npk) {
+    if (const int r = g_os_rounds.load()) return r;
+    return npk <= (size_t)INA_RS_MID_ITEMS ? 4 : 8;
+}
+
 }  // namespace ina
 
 namespace ina {
@@ -897,12 +1152,14 @@ extern "C" {
 
 size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots) {
     if (npkts == 0 || npkts > 0x7FFFFFFFu || num_slots == 0) return 256;
-    return 4 * align_up(npkts * 4, 256) + align_up(sort_temp_bytes(npkts, num_slots), 256) + 256;
+    const size_t aux = std::max(sort_temp_bytes(npkts, num_slots),
+                                os_aux_bytes(npkts, sort_plan(npkts, num_slots), kOsMinRounds));
+    return 4 * align_up(npkts * 4, 256) + align_up(aux, 256) + 256;
 }
 
 static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                               uint8_t* actions, void* scratch, ina_stream_t stream, const PsFuse& ps,
-                               bool* fused_out) {
+                               const uint64_t* desc, uint8_t* actions, void* scratch,
+                               ina_stream_t stream, const PsFuse& ps, bool* fused_out) {
     *fused_out = false;
     if (!st || st->V <= 0 || st->V > kMaxV || st->num_slots == 0)
         return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
@@ -913,6 +1170,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     if (npk > 0x7FFFFFFFu) return set_error(INA_EINVAL, "too many packets%s", "");
     if (!pkts || !actions || !scratch || !st->count || !st->frag || !st->regs)
         return set_error(INA_EINVAL, "null pointer%s", "");
+    if (desc && ((uintptr_t)desc & 7u))
+        return set_error(INA_EINVAL, "descriptors must be 8-byte aligned%s", "");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     uint8_t* base = reinterpret_cast<uint8_t*>(align_up((uintptr_t)scratch, 256));
     size_t arr = align_up(npk * 4, 256);
@@ -924,7 +1183,10 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     // sort chunk geometry (sort_plan): one instantiation per rounds-per-wave choice
     constexpr int kR0 = INA_RS_ROUNDS_SMALL, kR1 = INA_RS_ROUNDS_MID, kR2 = kRsRounds;
     const int ri = sp.rounds == kR0 ? 0 : sp.rounds == kR1 ? 1 : 2;
-    auto* k_keys = ri == 0 ? &k_switch_keys<kR0> : ri == 1 ? &k_switch_keys<kR1> : &k_switch_keys<kR2>;
+    auto* k_keys = desc ? (ri == 0 ? &k_switch_keys<kR0, true> : ri == 1 ? &k_switch_keys<kR1, true>
+                                                                : &k_switch_keys<kR2, true>)
+                        : (ri == 0 ? &k_switch_keys<kR0, false> : ri == 1 ? &k_switch_keys<kR1, false>
+                                                                 : &k_switch_keys<kR2, false>);
     auto* k_hist = ri == 0 ? &k_rs_hist<kR0> : ri == 1 ? &k_rs_hist<kR1> : &k_rs_hist<kR2>;
     auto* k_sc0 = ri == 0 ? &k_rs_scatter<false, kR0>
                 : ri == 1 ? &k_rs_scatter<false, kR1> : &k_rs_scatter<false, kR2>;
@@ -939,10 +1201,47 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     uint32_t *kc = k_in, *vc = v_in, *kn = k_out, *vn = v_out;
     const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
                       st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
-    // keys carry the PS-ack bit for the run kernel when bit 31 is free of slot bits
-    const bool ack_hint = fast && end_bit_for(st->num_slots) <= 31 && g_ack_fast.load();
+    // keys carry the PS-ack bit for the run kernel when bit 31 is outside every digit pass
+    const bool ack_hint = fast && sp.passes * sp.bits <= 31 && g_ack_fast.load();
     const bool small = npk <= (size_t)INA_SWITCH_SMALL_MAX && g_small_sort.load();
-    if (small) {
+    const bool onesweep = !small && g_sort_mode.load() == 1 && npk < ((size_t)1 << 30);
+    if (onesweep) {
+        // memset(aux) + keys/histograms + one kernel per digit pass
+        const int R = os_rounds_for(npk);
+        const size_t ntiles = os_tiles(npk, R);
+        uint8_t* aux = base + 4 * arr;
+        uint32_t* ghist = reinterpret_cast<uint32_t*>(aux);
+        uint32_t* tickets = reinterpret_cast<uint32_t*>(aux + kOsHistBytes);
+        uint32_t* status = reinterpret_cast<uint32_t*>(aux + kOsHistBytes + 256);
+        if (hipMemsetAsync(aux, 0, os_aux_bytes(npk, sp, R), s) != hipSuccess)
+            return set_error(INA_EHIP, "switch sort memset%s", "");
+        const unsigned gk = (unsigned)std::min<size_t>((npk + kRsBlock * 8 - 1) / (kRsBlock * 8), 2048);
+        if (desc)
+            hipLaunchKernelGGL(k_switch_keys_os<true>, dim3(gk), dim3(kRsBlock), 0, s, pkts,
+                               reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
+                               st->switch_id, kc, actions, sp.passes, sp.bits, ghist, ack_hint ? 1 : 0);
+        else
+            hipLaunchKernelGGL(k_switch_keys_os<false>, dim3(gk), dim3(kRsBlock), 0, s, pkts,
+                               static_cast<const uint2*>(nullptr), npk, stride, st->num_slots,
+                               st->switch_id, kc, actions, sp.passes, sp.bits, ghist, ack_hint ? 1 : 0);
+        for (int pass = 0; pass < sp.passes; ++pass) {
+            const int shift = pass * sp.bits;
+            const uint32_t* gh = ghist + (size_t)pass * nb;
+            uint32_t* stp = status + (size_t)pass * ntiles * nb;
+#define INA_OS_LAUNCH(IDS, RR)                                                                        \
+            hipLaunchKernelGGL((k_rs_onesweep<IDS, RR>), dim3((unsigned)ntiles), dim3(kRsBlock), 0, s, \
+                               kc, vc, kn, vn, npk, shift, sp.bits, gh, tickets + pass, stp)
+            if (pass == 0) {
+                if (R == 4) INA_OS_LAUNCH(false, 4); else if (R == 8) INA_OS_LAUNCH(false, 8); else INA_OS_LAUNCH(false, 16);
+            } else {
+                if (R == 4) INA_OS_LAUNCH(true, 4); else if (R == 8) INA_OS_LAUNCH(true, 8); else INA_OS_LAUNCH(true, 16);
+            }
+#undef INA_OS_LAUNCH
+            if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
+            std::swap(kc, kn);
+            std::swap(vc, vn);
+        }
+    } else if (small) {
         if ((uint64_t)st->num_slots + 1 <= (1u << 20))
             hipLaunchKernelGGL((k_switch_sort_small<uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, pkts,
                                (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
@@ -951,12 +1250,13 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                s, pkts, (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
-        hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts, npk, stride, st->num_slots,
+        hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
+                           reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
                            st->switch_id, k_in, actions, sp.bits, hist, sp.nch, ack_hint ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
     }
-    // digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
-    for (int pass = 0; pass < (small ? 0 : sp.passes); ++pass) {
+    // r01 digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
+    for (int pass = 0; pass < (small || onesweep ? 0 : sp.passes); ++pass) {
         const int shift = pass * sp.bits;
         if (pass > 0)
             hipLaunchKernelGGL(k_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits, hist,
@@ -995,17 +1295,32 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     return INA_OK;
 }
 
-int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                       uint8_t* actions, void* scratch, ina_stream_t stream) {
+int ina_switch_process_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                            const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                            ina_stream_t stream) {
     PsFuse off{};
     bool fused = false;
-    return switch_process_impl(st, pkts, npk, stride, actions, scratch, stream, off, &fused);
+    return switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, off, &fused);
+}
+
+int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                       uint8_t* actions, void* scratch, ina_stream_t stream) {
+    return ina_switch_process_desc(st, pkts, npk, stride, nullptr, actions, scratch, stream);
 }
 
 int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
                              uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
                              double weight_step, float* out, size_t n, uint8_t* acks,
                              size_t ack_stride, int keep_forwarded, ina_stream_t stream) {
+    return ina_switch_process_apply_desc(st, pkts, npk, stride, nullptr, actions, scratch, seq0, local, k,
+                                         weight_step, out, n, acks, ack_stride, keep_forwarded, stream);
+}
+
+int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                                  const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                                  uint32_t seq0, const float* local, int k, double weight_step,
+                                  float* out, size_t n, uint8_t* acks, size_t ack_stride,
+                                  int keep_forwarded, ina_stream_t stream) {
     if (k < -126 || k > 127) return set_error(INA_EINVAL, "k out of range [-126,127]%s", "");
     if (npk == 0) return INA_OK;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
@@ -1025,7 +1340,7 @@ int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t
               nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,
               keep_forwarded ? 1 : 0};
     bool fused = false;
-    if (int rc = switch_process_impl(st, pkts, npk, stride, actions, scratch, stream, ps, &fused)) return rc;
+    if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused)) return rc;
     if (fused) return INA_OK;
     // layouts the register-resident run kernel does not take: the two steps one by one
     return ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,

@@ -69,6 +69,9 @@ SIGNATURES = {
     "ina_ps_combine_ina_f32": [_vp, _vp, _i, _i, _d, _vp, _sz, _vp],
     "ina_pack_nga": [_vp, _sz, C.POINTER(NgaParams), _vp, _vp, _sz, _vp],
     "ina_quantize_pack_nga": [_vp, _vp, _sz, _i, C.POINTER(NgaParams), _vp, _sz, _vp],
+    "ina_pack_nga_desc": [_vp, _sz, C.POINTER(NgaParams), _vp, _vp, _sz, _vp, _vp],
+    "ina_quantize_pack_nga_desc": [_vp, _vp, _sz, _i, C.POINTER(NgaParams), _vp, _sz, _vp, _vp],
+    "ina_nga_descriptors": [_vp, _sz, _sz, _vp, _vp],
     "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
     "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],
@@ -76,6 +79,9 @@ SIGNATURES = {
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
     "ina_switch_process_apply": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i, _d,
                                  _vp, _sz, _vp, _sz, _i, _vp],
+    "ina_switch_process_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _vp],
+    "ina_switch_process_apply_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _u32, _vp,
+                                      _i, _d, _vp, _sz, _vp, _sz, _i, _vp],
     "ina_route_ipv4": [_vp, _vp, _u32, _sz, _vp, _vp, _i, _vp, _vp],
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],
     "ina_absmax_f32": [_vp, _vp, _sz, _vp, _vp],

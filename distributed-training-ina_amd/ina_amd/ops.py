@@ -271,10 +271,26 @@ def ps_apply(local: torch.Tensor, sum_int: torch.Tensor, k: int, weight_step: fl
 
 
 # -- packets -----------------------------------------------------------------------------------
+def _desc_arg(desc, npk, dev):
+    """Descriptor output/input: True -> a new int64 [npk] tensor; a tensor -> checked."""
+    if desc is None or desc is False:
+        return None
+    if desc is True:
+        return torch.empty(npk, dtype=torch.int64, device=dev)
+    _req(desc, torch.int64, "desc")
+    _fits(desc, npk, "desc")
+    if desc.device != torch.device(dev):
+        raise ValueError("all tensors must be on the same device")
+    return desc
+
+
 def pack_nga(vals: torch.Tensor, V: int, bitmap: int, count: int, switch_id: int, seq0: int,
              flags: int = 0, num_slots: int = NUM_REGISTER, stride: int | None = None,
-             overflow: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Returns uint8 [npkts, stride] device packets (first 15 + 4V bytes of each row on the wire)."""
+             overflow: torch.Tensor | None = None, out: torch.Tensor | None = None,
+             desc=None):
+    """Returns uint8 [npkts, stride] device packets (first 15 + 4V bytes of each row on the
+    wire).  desc=True (or an int64 [npkts] tensor) also writes each packet's descriptor
+    (header bytes 4..11, include/ina.h) and returns (packets, descriptors)."""
     _req(vals, torch.int32, "vals")
     stride = stride or nga_stride(V)
     npk = (vals.numel() + V - 1) // V
@@ -287,17 +303,29 @@ def pack_nga(vals: torch.Tensor, V: int, bitmap: int, count: int, switch_id: int
         _req(overflow, torch.uint8, "overflow")
         _fits(overflow, npk, "overflow")
         ovp = overflow.data_ptr()
-    check(load().ina_pack_nga(vals.data_ptr(), vals.numel(), C.byref(prm), ovp, out.data_ptr(),
-                              stride, _stream(vals)), "pack_nga")
-    return out
+    d = _desc_arg(desc, npk, vals.device)
+    check(load().ina_pack_nga_desc(vals.data_ptr(), vals.numel(), C.byref(prm), ovp, out.data_ptr(),
+                                   stride, d.data_ptr() if d is not None else None, _stream(vals)),
+          "pack_nga")
+    return (out, d) if d is not None else out
+
+
+def nga_descriptors(pkts: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """int64 [npkts] descriptors (header bytes 4..11) gathered from uint8 [npkts, stride]."""
+    _req(pkts, torch.uint8, "pkts")
+    npk, stride = pkts.shape
+    d = _desc_arg(True if out is None else out, npk, pkts.device)
+    check(load().ina_nga_descriptors(pkts.data_ptr(), npk, stride, d.data_ptr(), _stream(pkts)),
+          "nga_descriptors")
+    return d
 
 
 def quantize_pack_nga(x: torch.Tensor, k: int, V: int, bitmap: int, count: int, switch_id: int,
                       seq0: int, base: torch.Tensor | None = None, flags: int = 0,
                       num_slots: int = NUM_REGISTER, stride: int | None = None,
-                      out: torch.Tensor | None = None) -> torch.Tensor:
+                      out: torch.Tensor | None = None, desc=None):
     """Fused worker side: NGA-V packets of quantize(x - base, k) in one pass (same bytes as
-    quantize() then pack_nga())."""
+    quantize() then pack_nga()); desc as in pack_nga."""
     _req(x, torch.float32, "x")
     if base is not None:
         _req(base, torch.float32, "base")
@@ -310,10 +338,12 @@ def quantize_pack_nga(x: torch.Tensor, k: int, V: int, bitmap: int, count: int, 
     _fits(out, npk * stride)
     prm = _lib.NgaParams(bitmap & 0xFFFFFFFF, count & 0xFF, flags & 0xFF, switch_id & 0xFF, 0,
                          seq0 & 0xFFFFFFFF, num_slots, V)
-    check(load().ina_quantize_pack_nga(x.data_ptr(), base.data_ptr() if base is not None else None,
-                                       x.numel(), k, C.byref(prm), out.data_ptr(), stride,
-                                       _stream(x)), "quantize_pack_nga")
-    return out
+    d = _desc_arg(desc, npk, x.device)
+    check(load().ina_quantize_pack_nga_desc(x.data_ptr(), base.data_ptr() if base is not None else None,
+                                            x.numel(), k, C.byref(prm), out.data_ptr(), stride,
+                                            d.data_ptr() if d is not None else None, _stream(x)),
+          "quantize_pack_nga")
+    return (out, d) if d is not None else out
 
 
 def unpack_nga(pkts: torch.Tensor, V: int, stride: int | None = None, with_values: bool = True):
@@ -458,11 +488,15 @@ class Switch:
                                        self.regs.data_ptr())
         self._scratch = None
 
-    def process(self, pkts: torch.Tensor, actions: torch.Tensor | None = None) -> torch.Tensor:
+    def process(self, pkts: torch.Tensor, actions: torch.Tensor | None = None,
+                desc: torch.Tensor | None = None) -> torch.Tensor:
         """Runs packets (uint8 [npkts, stride], arrival order) through the switch in place;
-        returns the uint8 action per packet (ACT_*)."""
+        returns the uint8 action per packet (ACT_*).  desc: the batch's descriptors
+        (int64 [npkts], pack_nga(desc=True) / nga_descriptors) -- the slot sort then reads
+        them instead of the packet headers; results identical."""
         _req(pkts, torch.uint8, "pkts")
         npk, stride = pkts.shape
+        d = _desc_arg(desc, npk, pkts.device)
         actions = torch.empty(npk, dtype=torch.uint8, device=pkts.device) if actions is None else actions
         _req(actions, torch.uint8, "actions")
         if actions.numel() < npk:
@@ -471,15 +505,16 @@ class Switch:
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
-        check(load().ina_switch_process(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                        actions.data_ptr(), self._scratch.data_ptr(),
-                                        _stream(pkts)), "switch_process")
+        check(load().ina_switch_process_desc(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                             d.data_ptr() if d is not None else None,
+                                             actions.data_ptr(), self._scratch.data_ptr(),
+                                             _stream(pkts)), "switch_process")
         return actions
 
     def process_apply(self, pkts: torch.Tensor, seq0: int, local: torch.Tensor, k: int,
                       weight_step: float, out: torch.Tensor | None = None,
                       acks: torch.Tensor | None = None, keep_forwarded: bool = True,
-                      actions: torch.Tensor | None = None):
+                      actions: torch.Tensor | None = None, desc: torch.Tensor | None = None):
         """process() + apply_completed() in one pass (the PS on the switch's GPU): completed
         slots update out = local + weight_step * sum * 2^-k and write their PS ack rows.
         keep_forwarded=False leaves completed packets as they arrived (consumed here).
@@ -492,13 +527,15 @@ class Switch:
         out = torch.empty_like(local) if out is None else out
         _fits(out, local.numel())
         _check_apply(pkts, actions, self.V, local, out, acks)
+        d = _desc_arg(desc, npk, pkts.device)
         ack_ptr, ack_stride = None, 0
         if acks is not None:
             ack_ptr, ack_stride = acks.data_ptr(), acks.shape[1]
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
-        check(load().ina_switch_process_apply(C.byref(self._state), pkts.data_ptr(), npk, stride,
+        check(load().ina_switch_process_apply_desc(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                              d.data_ptr() if d is not None else None,
                                               actions.data_ptr(), self._scratch.data_ptr(),
                                               seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
                                               out.data_ptr(), local.numel(), ack_ptr, ack_stride,
@@ -539,7 +576,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                stream_blocks: int | None = None, combine_blocks: int | None = None,
                combine_ina_blocks: int | None = None, h2d_streams: int | None = None,
                launch_chunks: int | None = None, switch_small_sort: bool | None = None,
-               switch_window: int | None = None, switch_ack_fast: bool | None = None):
+               switch_window: int | None = None, switch_ack_fast: bool | None = None,
+               switch_sort: int | None = None, switch_sort_rounds: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -549,7 +587,10 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     switch_small_sort the one-workgroup key+sort path for switch batches <= 4096 packets,
     switch_window the sorted positions one wave of the switch run kernel owns (0 = auto,
     1..64), switch_ack_fast the lane-parallel path for PS acks alone in their slot's
-    segment; unroll is the sum-reduce's 16-byte chunks per worker per thread."""
+    segment, switch_sort the slot sort (0 histogram / column-scan / scatter passes, 1
+    one-sweep passes with decoupled look-back), switch_sort_rounds the one-sweep tile
+    (64-item rounds per wave: 0 auto, 4, 8, 16); unroll is the sum-reduce's 16-byte chunks
+    per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")
@@ -569,6 +610,10 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(10, int(switch_window)), "set_tuning")
     if switch_ack_fast is not None:
         check(lib.ina_set_tuning(11, int(bool(switch_ack_fast))), "set_tuning")
+    if switch_sort is not None:
+        check(lib.ina_set_tuning(12, int(switch_sort)), "set_tuning")
+    if switch_sort_rounds is not None:
+        check(lib.ina_set_tuning(13, int(switch_sort_rounds)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

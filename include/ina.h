@@ -68,7 +68,9 @@ const char* ina_last_error_string(void);
  * 5 fp32 PS-combine grid, 6 INA PS-combine grid, 7 host-ingest H2D streams (1/2),
  * 8 16-byte chunks per flat packet-kernel launch, 9 switch one-workgroup small-batch
  * path (0/1), 10 switch run-kernel window in sorted positions (0 = auto, 1..64),
- * 11 switch lane-parallel path for PS acks alone in their slot's segment (0/1).
+ * 11 switch lane-parallel path for PS acks alone in their slot's segment (0/1), 12 switch
+ * slot sort (0 histogram / column-scan / scatter passes, 1 one-sweep passes with decoupled
+ * look-back), 13 one-sweep tile rounds (0 auto, 4, 8, 16).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 
@@ -180,6 +182,24 @@ int ina_pack_nga(const int32_t* vals, size_t n, const ina_nga_params_t* prm,
 int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
                           const ina_nga_params_t* prm, uint8_t* pkts, size_t stride,
                           ina_stream_t stream);
+/* Packet descriptors: desc[p] holds bytes 4..11 of packet p's NGA header (count, flags,
+ * index, switch_id and frag_id's first byte) in wire order, byte 4 lowest -- all the
+ * fields the switch reads to order a batch by slot (ngaa.p4:27-37 switch_check,
+ * headers.p4:27-38).  They play the part of a NIC's receive descriptors: the producer of
+ * the packets hands them over beside the payload, so the switch sorts a batch from 8 bytes
+ * per packet instead of fetching one 128-byte line of every packet's header
+ * (ina_switch_process_desc).  The pack entry points write them as they write each header
+ * (desc may be NULL); ina_nga_descriptors gathers them from packets that arrive without.
+ * desc: device memory, 8-byte aligned, npkts entries. */
+typedef uint64_t ina_nga_desc_t;
+int ina_pack_nga_desc(const int32_t* vals, size_t n, const ina_nga_params_t* prm,
+                      const uint8_t* overflow_per_slot, uint8_t* pkts, size_t stride,
+                      ina_nga_desc_t* desc, ina_stream_t stream);
+int ina_quantize_pack_nga_desc(const float* x, const float* base, size_t n, int k,
+                               const ina_nga_params_t* prm, uint8_t* pkts, size_t stride,
+                               ina_nga_desc_t* desc, ina_stream_t stream);
+int ina_nga_descriptors(const uint8_t* pkts, size_t npkts, size_t stride, ina_nga_desc_t* desc,
+                        ina_stream_t stream);
 /* PS-side parse (NGAPacket.py:62-143 / get_data_from_nic, utils.py:61-64), following
  * headers.p4: payload at byte 15, big-endian.  vals gets npkts*V int32 (may be NULL). */
 int ina_unpack_nga(const uint8_t* pkts, size_t npkts, int V, size_t stride,
@@ -233,6 +253,17 @@ int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t
                              const float* local, int k, double weight_step, float* out, size_t n,
                              uint8_t* acks, size_t ack_stride, int keep_forwarded,
                              ina_stream_t stream);
+/* The same two calls with the batch's packet descriptors (ina_pack_nga_desc /
+ * ina_nga_descriptors; desc[p] must equal bytes 4..11 of packet p): the slot sort reads
+ * the descriptors instead of the headers; results identical. */
+int ina_switch_process_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
+                            const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                            ina_stream_t stream);
+int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
+                                  size_t stride, const ina_nga_desc_t* desc, uint8_t* actions,
+                                  void* scratch, uint32_t seq0, const float* local, int k,
+                                  double weight_step, float* out, size_t n, uint8_t* acks,
+                                  size_t ack_stride, int keep_forwarded, ina_stream_t stream);
 
 /* ---- ipRoute (ngaa.p4:39-61, entries as bfrt/setup.py:85-95 installs them) -------
  * Every packet the ingress does not drop (actions FWD_AGG, FWD_COLLISION, FWD_ACK,

@@ -138,6 +138,12 @@ def _einval_cases():
         "ina_apply_completed_nga": (None, 2, 32, 144, None, 1, None, 16, 0.5, None, 64, None, 144,
                                     None),
         "ina_switch_process": (ctypes.byref(st), None, 2, 144, None, None, None),
+        "ina_switch_process_desc": (ctypes.byref(st), None, 2, 144, None, None, None, None),
+        "ina_switch_process_apply_desc": (ctypes.byref(st), None, 2, 144, None, None, None, 1, None, 16,
+                                          0.5, None, 64, None, 144, 1, None),
+        "ina_pack_nga_desc": (None, 64, ctypes.byref(prm), None, None, 144, None, None),
+        "ina_quantize_pack_nga_desc": (None, None, 64, 16, ctypes.byref(prm), None, 144, None, None),
+        "ina_nga_descriptors": (None, 2, 144, None, None),
         "ina_switch_process_apply": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
                                      None, 64, None, 144, 1, None),
         "ina_route_ipv4": (None, None, 0, 4, None, None, 1, None, None),
@@ -184,6 +190,9 @@ def test_set_tuning_rejects_unknown_keys_and_values():
     assert lib.ina_set_tuning(10, 65) == _lib.INA_EINVAL        # switch window <= 64
     assert lib.ina_set_tuning(10, 0) == _lib.INA_OK             # 0 = automatic
     assert lib.ina_set_tuning(11, 1) == _lib.INA_OK
+    assert lib.ina_set_tuning(12, 2) == _lib.INA_EINVAL        # sort: 0 histogram passes, 1 one-sweep
+    assert lib.ina_set_tuning(13, 5) == _lib.INA_EINVAL        # one-sweep rounds: 0, 4, 8, 16
+    assert lib.ina_set_tuning(12, 0) == _lib.INA_OK and lib.ina_set_tuning(13, 0) == _lib.INA_OK
 
 
 def test_switch_scratch_bytes_monotonic():

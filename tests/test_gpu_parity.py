@@ -556,6 +556,76 @@ def test_switch_fuzz_vs_oracle(seed):
     assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
 
 
+# slot sort variants: (sort 0 = histogram passes / 1 = one-sweep, descriptors, one-sweep rounds)
+SORT_VARIANTS = [(0, True, 0), (0, False, 0), (1, False, 4), (1, True, 16), (1, False, 8)]
+
+
+@pytest.mark.parametrize("variant", SORT_VARIANTS)
+@pytest.mark.parametrize("seed", range(8))
+def test_switch_sort_paths_vs_oracle(seed, variant):
+    """Batches above the one-workgroup size (> 2,048 packets) through each slot sort --
+    the one-sweep passes (decoupled look-back; tiles of 1,024 / 2,048 / 4,096 items; keys
+    from the packet headers or from the batch's descriptors) and the r01 histogram /
+    column-scan / scatter passes -- bit-exact against the P4 restatement, state carried
+    across batches, pools of 1 .. 2^18 slots (1-3 digit passes)."""
+    sort, use_desc, rounds = variant
+    rng = np.random.default_rng(40_000 + seed)
+    o = ops()
+    V = int(rng.choice([4, 32, 64, 256, 33]))
+    num_slots = int(rng.choice([1, 64, 1000, 16384, 1 << 17, (1 << 18) - 5]))
+    W = int(rng.integers(1, 17))
+    stride = o.nga_stride(V) if rng.random() < 0.7 else 15 + 4 * V
+    wd = bool(rng.integers(0, 2))
+    o.set_tuning(switch_sort=sort, switch_sort_rounds=rounds)
+    try:
+        sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=wd)
+        sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+        for rnd in range(3):
+            used = int(rng.integers(2100 // W + 1, 9000 // W + 2))
+            stream = make_stream(rng, V, used, W, num_slots, collide=float(rng.uniform(0, 0.2)),
+                                 ack=float(rng.uniform(0, 0.3)), other=float(rng.uniform(0, 0.1)),
+                                 stride=stride)
+            assert stream.shape[0] > 2048
+            want_pk, want_act = sw_orc.run(stream, stride=stride)
+            d = dev(stream)
+            desc = o.nga_descriptors(d) if use_desc else None
+            act = sw_dev.process(d, desc=desc)
+            assert np.array_equal(host(act), want_act), (seed, rnd)
+            got_pk = host(d)
+            if wd:
+                assert np.array_equal(got_pk, want_pk), (seed, rnd)
+            else:
+                fwd = want_act != orc.ACT_DROP
+                assert np.array_equal(got_pk[fwd], want_pk[fwd]), (seed, rnd)
+                assert np.array_equal(got_pk[~fwd], stream[~fwd]), (seed, rnd)
+        cnt, frag, regs = sw_orc.registers()
+        assert np.array_equal(host(sw_dev.count), cnt)
+        assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+        assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+    finally:
+        o.set_tuning(switch_sort=0, switch_sort_rounds=0)
+
+
+@pytest.mark.parametrize("V,stride_kind", [(32, "padded"), (256, "padded"), (33, "tight"),
+                                           (64, "tight"), (4, "padded")])
+def test_pack_descriptors_are_header_bytes(V, stride_kind):
+    """pack_nga / quantize_pack_nga desc output == ina_nga_descriptors == header bytes
+    4..11 of each packet (byte 4 lowest), flat and generic pack paths alike."""
+    o = ops()
+    rng = np.random.default_rng(V)
+    n = 97 * V + 3
+    stride = o.nga_stride(V) if stride_kind == "padded" else 15 + 4 * V
+    vals = dev(rand_i32(rng, n))
+    pk, d = o.pack_nga(vals, V, 5, 3, 2, 4_000_000_000, flags=0x40, num_slots=1000, stride=stride,
+                       desc=True)
+    hb = host(pk)[:, 4:12].copy().view(np.int64).reshape(-1)
+    assert np.array_equal(host(d), hb)
+    assert np.array_equal(host(o.nga_descriptors(pk)), hb)
+    x = dev(rng.standard_normal(n).astype(np.float32))
+    pk2, d2 = o.quantize_pack_nga(x, 16, V, 2, 3, 1, 9, stride=stride, desc=True)
+    assert np.array_equal(host(d2), host(pk2)[:, 4:12].copy().view(np.int64).reshape(-1))
+
+
 @pytest.mark.parametrize("write_dropped", [True, False])
 @pytest.mark.parametrize("ack_fast", [True, False])
 @pytest.mark.parametrize("W,ack", [(1, 0.5), (1, 1.0), (2, 0.4), (5, 0.3)])
@@ -656,10 +726,12 @@ def test_switch_config3_full_size_equals_bulk_reduce(V, n, pool):
     bufs = [torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
             for _ in range(W)]
     want = o.sum_reduce(bufs)
-    stream = torch.cat([o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=pool) for w, b in enumerate(bufs)])
-    del bufs
+    packed = [o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=pool, desc=True) for w, b in enumerate(bufs)]
+    stream = torch.cat([p for p, _ in packed])
+    desc = torch.cat([d for _, d in packed])
+    del bufs, packed
     sw = o.Switch(V, num_slots=pool, switch_id=1, device=DEV)
-    act = sw.process(stream)
+    act = sw.process(stream, desc=desc)
     npk = n // V
     done = torch.nonzero(act == orc.ACT_FWD_AGG).flatten()
     assert done.numel() == npk and bool((done >= (W - 1) * npk).all())

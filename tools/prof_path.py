@@ -21,13 +21,17 @@ stride = ops.nga_stride(V)
 batch = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=dev)
 acks, rows = batch[:npk], batch[npk:].view(W, npk, stride)
 acts = torch.empty((W + 1) * npk, dtype=torch.uint8, device=dev)
+desc = torch.empty((W + 1) * npk, dtype=torch.int64, device=dev)     # packet descriptors
+desc_ack, desc_w = desc[:npk], desc[npk:].view(W, npk)
 out = torch.empty_like(params)
 sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
 for step in range(int(os.environ.get("STEPS", 6))):
     for w in range(W):
-        ops.quantize_pack_nga(xs[w], 16, V, w + 1, W, 1, 1, base=params, num_slots=slots, out=rows[w])
+        ops.quantize_pack_nga(xs[w], 16, V, w + 1, W, 1, 1, base=params, num_slots=slots, out=rows[w],
+                              desc=desc_w[w])
+    ops.nga_descriptors(acks, out=desc_ack)
     sw.process_apply(batch, 1, params, 16, 1.0 / (W + 1), out=out, acks=acks, keep_forwarded=False,
-                     actions=acts)
+                     actions=acts, desc=desc)
 torch.cuda.synchronize()
 assert int((acts[npk:] == 1).sum()) == npk and bool((acts[:npk] == 3).all())
 print("done", batch.shape)

@@ -1,5 +1,6 @@
 """Profile target: the device packet-stream switch on 8 workers x NGA-256 packets of
-a config-3 bucket (run under rocprofv3 --kernel-trace --stats)."""
+a config-3 bucket (run under rocprofv3 --kernel-trace --stats); the slot sort reads the
+pack kernels' packet descriptors (DESC=0: the packet headers)."""
 import os
 import sys
 
@@ -15,13 +16,17 @@ g = torch.Generator(device=dev).manual_seed(1)
 bufs = [torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
         for _ in range(W)]
 slots = 1 << 17
-stream = torch.cat([ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots) for w, b in enumerate(bufs)])
+packed = [ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots, desc=True) for w, b in enumerate(bufs)]
+stream = torch.cat([p for p, _ in packed])
+desc = torch.cat([d for _, d in packed])     # the pack kernels' packet descriptors
+del packed
 sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
 acts = torch.empty(stream.shape[0], dtype=torch.uint8, device=dev)
+use_desc = os.environ.get("DESC", "1") == "1"
 for i in range(int(os.environ.get("REPS", 5))):
     sw.count.zero_()
     sw.frag.zero_()
-    sw.process(stream, acts)
+    sw.process(stream, acts, desc=desc if use_desc else None)
 torch.cuda.synchronize()
 ok = torch.equal(stream.view(W, -1, stream.shape[1])[-1, :, 15:15 + 4 * V].contiguous().view(-1).view(torch.uint8)[:8], stream[stream.shape[0] // W * (W - 1), 15:23])
 print("done", stream.shape, int((acts == 1).sum()))
