@@ -259,7 +259,7 @@ static std::atomic<int> g_small_sort{1};   // ina_set_tuning key 9 (0: always th
 static std::atomic<int> g_switch_win{0};   // ina_set_tuning key 10: run-kernel window (0: auto)
 static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack lane path (0: off)
 static std::atomic<int> g_sort_mode{0};    // ina_set_tuning key 12: 0 hist/colscan/scatter passes, 1 one-sweep
-static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: one-sweep tile rounds (0 auto, 4/8/16)
+static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: sort tile rounds (0 auto, 4/8/16)
 int set_sort_mode(int v) {
     if (v != 0 && v != 1) return INA_EINVAL;
     g_sort_mode = v;
@@ -1077,6 +1077,7 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     p.rounds = npk <= (size_t)INA_RS_SMALL_ITEMS ? INA_RS_ROUNDS_SMALL
              : npk <= (size_t)INA_RS_MID_ITEMS   ? INA_RS_ROUNDS_MID
                                                  : kRsRounds;
+    if (const int r = g_os_rounds.load()) p.rounds = r;   // ina_set_tuning key 13 (lab sweeps)
     const size_t chunk = (size_t)kRsWaves * 64 * (size_t)p.rounds;
     p.nch = (npk + chunk - 1) / chunk;
     p.hist_elems = ((size_t)1 << p.bits) * p.nch;

@@ -588,9 +588,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     switch_window the sorted positions one wave of the switch run kernel owns (0 = auto,
     1..64), switch_ack_fast the lane-parallel path for PS acks alone in their slot's
     segment, switch_sort the slot sort (0 histogram / column-scan / scatter passes, 1
-    one-sweep passes with decoupled look-back), switch_sort_rounds the one-sweep tile
-    (64-item rounds per wave: 0 auto, 4, 8, 16); unroll is the sum-reduce's 16-byte chunks
-    per worker per thread."""
+    one-sweep passes with decoupled look-back), switch_sort_rounds the sort tile of either
+    sort (64-item rounds per wave: 0 auto, 4, 8, 16); unroll is the sum-reduce's 16-byte
+    chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")

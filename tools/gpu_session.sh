@@ -3,9 +3,9 @@
 # Every GPU step has its own time limit; the script stops at the first crash,
 # abort or timeout (only an ordinary pytest failure, rc 1, lets it continue).
 # usage: tools/gpu_session.sh TAG [stages...]   stages: smoke test bench prof pmc extra swprof
-#        config1 rehearse sharded
+#        config1 rehearse sharded swlab
 set -u
-TAG=${1:-r01}; shift || true
+TAG=${1:-r02}; shift || true
 STAGES=${*:-"smoke test bench prof pmc extra"}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -46,12 +46,18 @@ for st in $STAGES; do
       timeout -k 10 600 python examples/config1_loopback.py --epochs 3 --local-steps 5 > "$OUT/config1.log" 2>&1
       rc=$?; tail -8 "$OUT/config1.log"; [ $rc -ne 0 ] && fatal config1 $rc ;;
     rehearse)
-      INA_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 > "$OUT/rehearse2.json" 2> "$OUT/rehearse2.err"
+      # bench.py starts its own two ranks (no launcher); both on the box's one GPU over gloo
+      INA_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
+        --c5-values 67108864 > "$OUT/rehearse2.json" 2> "$OUT/rehearse2.err"
       rc=$?; cat "$OUT/rehearse2.json"; tail -3 "$OUT/rehearse2.err"; [ $rc -ne 0 ] && fatal rehearse $rc ;;
     sharded)
-      timeout -k 10 400 python bench.py --mode sharded --steps 10 --warmup 3 > "$OUT/sharded1.json" 2> "$OUT/sharded1.err"
-      rc=$?; cat "$OUT/sharded1.json"; tail -3 "$OUT/sharded1.err"; [ $rc -ne 0 ] && fatal sharded $rc ;;
+      for wire in i32 i16; do
+        timeout -k 10 400 python bench.py --mode sharded --wire $wire > "$OUT/sharded1_$wire.json" 2> "$OUT/sharded1_$wire.err"
+        rc=$?; cat "$OUT/sharded1_$wire.json"; tail -3 "$OUT/sharded1_$wire.err"; [ $rc -ne 0 ] && fatal sharded $rc
+      done ;;
+    swlab)
+      timeout -k 10 400 python tools/lab/switch_sort_lab.py > "$OUT/switch_sort_lab.json" 2> "$OUT/switch_sort_lab.err"
+      rc=$?; cat "$OUT/switch_sort_lab.json"; [ $rc -ne 0 ] && fatal swlab $rc ;;
     extra)
       timeout -k 10 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --extra > "$OUT/extra_bench.json" 2> "$OUT/extra.err"
       rc=$?; tail -3 "$OUT/extra.err"; [ $rc -ne 0 ] && fatal extra $rc

@@ -21,6 +21,8 @@ from ina_amd import ops  # noqa: E402
 VARIANTS = {                      # name: (sort, rounds, use descriptors)
     "r01_hdr": (0, 0, False),
     "r01_desc": (0, 0, True),
+    "r01_desc_r4": (0, 4, True),
+    "r01_desc_r8": (0, 8, True),
     "os_hdr": (1, 0, False),
     "os_desc": (1, 0, True),
     "os_desc_r4": (1, 4, True),
