@@ -54,7 +54,7 @@ def _row(name, secs, nbytes, **kw):
 
 
 DEFAULTS = {"max_blocks": 16384, "reduce_blocks": 0, "stream_blocks": 8192, "combine_blocks": 256,
-            "combine_ina_blocks": 8192}
+            "combine_ina_blocks": 8192, "ew_blocks": 1 << 24}
 
 
 def _sweep(ops, rows, sweeps, name, knob, values, fn, nbytes):
@@ -107,11 +107,28 @@ def run_extra(dev):
     # --- quantise / dequantise ------------------------------------------------------------
     x = rnd_f32(n3)
     q = torch.empty(n3, dtype=torch.int32, device=dev)
-    _sweep(ops, rows, gsweep, "quantize_f32_i32", "stream_blocks", (512, 2048, 8192),
+    _sweep(ops, rows, gsweep, "quantize_f32_i32", "ew_blocks", (2048, 8192, 65536),
            lambda: ops.quantize(x, 16, out=q), 8 * n3)
     y = torch.empty(n3, dtype=torch.float32, device=dev)
-    _sweep(ops, rows, gsweep, "dequantize_i32_f32", "stream_blocks", (512, 2048, 8192),
+    _sweep(ops, rows, gsweep, "dequantize_i32_f32", "ew_blocks", (2048, 8192, 65536),
            lambda: ops.dequantize(q, 16, out=y), 8 * n3)
+    del x, q, y
+
+    # --- config 5, one rank: a 1 GiB fp32 bucket through both wires' device steps ----------
+    n5 = 268_435_456
+    x5 = rnd_f32(n5)
+    w5 = torch.empty(n5, dtype=torch.int32, device=dev)
+    y5 = torch.empty(n5, dtype=torch.float32, device=dev)
+    f5 = torch.empty(n5 // 256, dtype=torch.uint8, device=dev)
+    rows.append(_row("quantize_f32_i32 (C5 rank, 1 GiB)", _time(lambda: ops.quantize(x5, 16, out=w5)), 8 * n5))
+    rows.append(_row("dequantize_i32_f32 (C5 rank, 1 GiB)", _time(lambda: ops.dequantize(w5, 16, out=y5)),
+                     8 * n5))
+    rows.append(_row("quantize_i16_wire (C5 rank, 1 GiB, int16 wire)",
+                     _time(lambda: ops.quantize_i16_wire(x5, 20, out=w5)), 8 * n5))
+    rows.append(_row("i16_wire_finish (C5 rank, 1 GiB: saturate once, dequantise, slot flags)",
+                     _time(lambda: ops.i16_wire_finish(w5, 20, 256, y=y5, overflow=f5, want_out16=False)),
+                     8 * n5 + f5.numel()))
+    del x5, w5, y5, f5
 
     # --- config 2: fused quantise + reduce, 4 x ResNet-50 fp32 -----------------------------
     n2 = 25_557_032

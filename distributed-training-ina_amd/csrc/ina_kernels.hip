@@ -81,6 +81,13 @@ constexpr int kEwU = INA_EW_U;
 #endif
 // the other chunk_loop<4> streaming kernels
 static std::atomic<int> g_stream_blocks{8192};
+// the one-in one-out elementwise kernels (quantise, dequantise, PS apply, the int16 wire
+// kernels of ina_shard.hip): one 16-byte chunk per thread, the grid covering the whole
+// array -- no grid-stride loop.  At a 1 GiB bucket (config 5) that is 330-340 us (80 %)
+// against 416-425 us (64 %) with an 8192-workgroup grid striding; at config-2 size it is
+// within +-1 us of it (tools/lab/ew_grid_lab.py, profiles/r02/lab/ew_grid_lab.json)
+static std::atomic<int> g_ew_blocks{1 << 24};
+int ew_grid_cap() { return g_ew_blocks.load(); }
 // PS combine kernels (W+2 streams), measured per kernel (bench_extra grid sweeps and
 // ew_lab): the fp32 combine runs best at 256 workgroups (6.6-6.7 TB/s vs 6.0 at 512),
 // the INA combine (quantiser in the loop) with one chunk in flight at 8192
@@ -1401,6 +1408,7 @@ int ina_set_tuning(int key, int value) {
         case 2: g_nontemporal = value ? 1 : 0; return INA_OK;
         case 3: if (value < 0) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
         case 4: if (value < 1) return INA_EINVAL; g_stream_blocks = value; return INA_OK;
+        case 14: if (value < 1) return INA_EINVAL; g_ew_blocks = value; return INA_OK;
         case 5: if (value < 1) return INA_EINVAL; g_combine_blocks = value; return INA_OK;
         case 6: if (value < 1) return INA_EINVAL; g_combine_ina_blocks = value; return INA_OK;
         case 7: return set_h2d_streams(value);
@@ -1446,7 +1454,7 @@ int ina_quantize_f32_i32(const float* x, int32_t* q, size_t n, int k, ina_stream
     if (n == 0) return INA_OK;
     if (!x || !q) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(x) && aligned16(q);
-    hipLaunchKernelGGL(k_quantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_quantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_ew_blocks)), dim3(kBlock), 0,
                        hs(stream), x, q, n, ldexpf(1.0f, k), vec);
     return check_launch("quantize_i32");
 }
@@ -1477,7 +1485,7 @@ int ina_dequantize_i32_f32(const int32_t* sv, float* y, size_t n, int k, ina_str
     if (n == 0) return INA_OK;
     if (!sv || !y) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(sv) && aligned16(y);
-    hipLaunchKernelGGL(k_dequantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_dequantize_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_ew_blocks)), dim3(kBlock), 0,
                        hs(stream), sv, y, n, ldexpf(1.0f, -k), vec);
     return check_launch("dequantize_i32");
 }
@@ -1487,7 +1495,7 @@ int ina_dequantize_i16_f32(const int16_t* sv, float* y, size_t n, int k, ina_str
     if (n == 0) return INA_OK;
     if (!sv || !y) return set_error(INA_EINVAL, "null pointer%s", "");
     const int vec = ((uintptr_t)sv % 8 == 0) && aligned16(y);
-    hipLaunchKernelGGL(k_dequantize_i16, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)),
+    hipLaunchKernelGGL(k_dequantize_i16, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_ew_blocks)),
                        dim3(kBlock), 0, hs(stream), sv, y, n, ldexpf(1.0f, -k), vec);
     return check_launch("dequantize_i16");
 }
@@ -1591,7 +1599,7 @@ int ina_ps_apply_i32(const float* local, const int32_t* sum_int, int k, double w
     if (n == 0) return INA_OK;
     if (!local || !sum_int || !out) return set_error(INA_EINVAL, "null pointer%s", "");
     int vec = aligned16(local) && aligned16(sum_int) && aligned16(out);
-    hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_stream_blocks)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_ps_apply_i32, dim3(grid_for(vec ? n / 4 + 1 : n, kEwU, g_ew_blocks)), dim3(kBlock), 0,
                        hs(stream), local, sum_int, ldexpf(1.0f, -k), (float)weight_step, out, n, vec);
     return check_launch("ps_apply_i32");
 }

@@ -143,7 +143,8 @@ __global__ __launch_bounds__(kBlk) void k_i16_wire_finish_scalar(const int32_t* 
 
 inline unsigned grid_of(size_t items) {
     size_t g = (items + kBlk - 1) / kBlk;
-    if (g > 8192) g = 8192;        // 32 workgroups per CU, grid-stride beyond
+    const size_t cap = (size_t)ew_grid_cap();       // the elementwise kernels' cap (tuning key 14)
+    if (g > cap) g = cap;                           // grid-stride beyond
     return g ? (unsigned)g : 1u;
 }
 inline bool al(const void* p, unsigned a) { return ((uintptr_t)p % a) == 0; }

@@ -577,7 +577,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                combine_ina_blocks: int | None = None, h2d_streams: int | None = None,
                launch_chunks: int | None = None, switch_small_sort: bool | None = None,
                switch_window: int | None = None, switch_ack_fast: bool | None = None,
-               switch_sort: int | None = None, switch_sort_rounds: int | None = None):
+               switch_sort: int | None = None, switch_sort_rounds: int | None = None,
+               ew_blocks: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -589,8 +590,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     1..64), switch_ack_fast the lane-parallel path for PS acks alone in their slot's
     segment, switch_sort the slot sort (0 histogram / column-scan / scatter passes, 1
     one-sweep passes with decoupled look-back), switch_sort_rounds the sort tile of either
-    sort (64-item rounds per wave: 0 auto, 4, 8, 16); unroll is the sum-reduce's 16-byte
-    chunks per worker per thread."""
+    sort (64-item rounds per wave: 0 auto, 4, 8, 16), ew_blocks the grid cap of the one-in
+    one-out elementwise kernels (default 2^24: one 16-byte chunk per thread); unroll is the
+    sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")
@@ -614,6 +616,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(12, int(switch_sort)), "set_tuning")
     if switch_sort_rounds is not None:
         check(lib.ina_set_tuning(13, int(switch_sort_rounds)), "set_tuning")
+    if ew_blocks is not None:
+        check(lib.ina_set_tuning(14, int(ew_blocks)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:
