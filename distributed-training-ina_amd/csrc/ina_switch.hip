@@ -186,8 +186,8 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
                                                           uint32_t num_slots, int switch_id,
                                                           uint32_t* __restrict__ keys,
                                                           uint8_t* __restrict__ actions, int bits,
-                                                          uint32_t* __restrict__ hist, size_t nch,
-                                                          int ack_hint) {
+                                                          int shift, uint32_t* __restrict__ hist,
+                                                          size_t nch, int ack_hint) {
     __shared__ uint32_t h[kRsBins];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
             keys[p] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
             if (!mine) actions[p] = INA_ACT_FWD_OTHER;
         }
-        lds_count(h, key & (nb - 1), p < npk);
+        lds_count(h, (key >> shift) & (nb - 1), p < npk);
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
@@ -258,10 +258,14 @@ constexpr int kSmallBlock = 1024;
 static std::atomic<int> g_small_sort{1};   // ina_set_tuning key 9 (0: always the radix path)
 static std::atomic<int> g_switch_win{0};   // ina_set_tuning key 10: run-kernel window (0: auto)
 static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack lane path (0: off)
-static std::atomic<int> g_sort_mode{0};    // ina_set_tuning key 12: 0 hist/colscan/scatter passes, 1 one-sweep
+// ina_set_tuning key 12, the slot sort: 0 auto (bucket + local for two-digit keys, else the
+// digit passes), 1 one-sweep, 2 bucket + local where it applies, 3 hist/colscan/scatter
+// digit passes (r01).  Bucket + local measured 265.3 -> 251.0 us against the digit passes
+// at 819,200 NGA-256 packets with descriptors (profiles/r02/lab/switch_sort_lab_hyb.json)
+static std::atomic<int> g_sort_mode{0};
 static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: sort tile rounds (0 auto, 4/8/16)
 int set_sort_mode(int v) {
-    if (v != 0 && v != 1) return INA_EINVAL;
+    if (v < 0 || v > 3) return INA_EINVAL;
     g_sort_mode = v;
     return INA_OK;
 }
@@ -459,6 +463,114 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
     }
     __syncthreads();
     rs_tile_scatter<R>(k, v, i0, n, shift, bits, base, dbase, kout, vout);
+}
+
+// ---- bucket + local slot sort (ina_set_tuning key 12 = 2) -----------------------------
+// Two-digit keys sorted MSD-first: ONE global pass (keys + histogram, column scan, scatter)
+// on the high digit leaves every bucket of 2^lbits consecutive slots contiguous and in
+// arrival order; then one workgroup per bucket sorts it stably on the low digit, the
+// bucket's whole tile staying in registers and LDS.  The permutation equals the LSD
+// passes' (stable by (high, low) digit, arrival order inside a slot), so the run kernel
+// sees the same arrays; the second pass's histogram and column-scan launches and its
+// global rank bookkeeping are gone.  A bucket larger than one tile (skewed slot use) is
+// sorted tile by tile: a counting sweep over the bucket first, then the tiles in order.
+template <int R>
+__global__ __launch_bounds__(kRsBlock) void k_rs_local(const uint32_t* __restrict__ kin,
+                                                       const uint32_t* __restrict__ vin,
+                                                       uint32_t* __restrict__ kout,
+                                                       uint32_t* __restrict__ vout, int lbits,
+                                                       const uint32_t* __restrict__ totals) {
+    __shared__ uint32_t base[kRsWaves][kRsBins];
+    __shared__ uint32_t gst[kRsBins];               // bucket digit counts, then output positions
+    __shared__ uint32_t red[kRsWaves];
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const uint32_t b = blockIdx.x;
+    // bucket start = sum of the earlier buckets' totals (high-digit pass)
+    uint32_t part = 0;
+    for (uint32_t d = threadIdx.x; d < b; d += kRsBlock) part += totals[d];
+    part = __builtin_amdgcn_readlane(wave_incl_scan(part), 63);
+    if (lane == 0) red[wv] = part;
+    const uint32_t cnt = totals[b];
+    const uint32_t nb = 1u << lbits;
+    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) gst[d] = 0;
+    __syncthreads();
+    if (cnt == 0) return;                           // block-uniform
+    uint32_t s0 = 0;
+#pragma unroll
+    for (int w = 0; w < kRsWaves; ++w) s0 += red[w];
+    constexpr uint32_t kTile = (uint32_t)kRsWaves * 64u * (uint32_t)R;
+    const uint32_t ntile = (cnt + kTile - 1) / kTile;
+    const size_t n_end = (size_t)s0 + cnt;
+    constexpr int kDPT = kRsBins / kRsBlock;
+    if (ntile > 1) {                                // bucket digit totals -> output positions
+        for (uint32_t t = 0; t < ntile; ++t) {
+            const size_t i0 = (size_t)s0 + (size_t)t * kTile + (size_t)wv * (64 * R) + (size_t)lane;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const size_t i = i0 + (size_t)r * 64;
+                lds_count(gst, (i < n_end ? kin[i] : 0u) & (nb - 1), i < n_end);
+            }
+        }
+        __syncthreads();
+        if (wv == 0) {
+            uint32_t carry = s0;
+            for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
+                const uint32_t d = d0 + (uint32_t)lane;
+                const uint32_t t = d < nb ? gst[d] : 0u;
+                const uint32_t inc = wave_incl_scan(t);
+                if (d < nb) gst[d] = carry + inc - t;
+                carry += __builtin_amdgcn_readlane(inc, 63);
+            }
+        }
+    }
+    for (uint32_t t = 0; t < ntile; ++t) {
+        const size_t i0 = (size_t)s0 + (size_t)t * kTile + (size_t)wv * (64 * R) + (size_t)lane;
+        uint32_t k[R], v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = i0 + (size_t)r * 64;
+            k[r] = i < n_end ? kin[i] : 0u;
+            v[r] = i < n_end ? vin[i] : 0u;
+        }
+        for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            lds_count(base[wv], k[r] & (nb - 1), i0 + (size_t)r * 64 < n_end);
+        __syncthreads();
+        uint32_t tc[kDPT];                          // this tile's count per digit
+#pragma unroll
+        for (int j = 0; j < kDPT; ++j) {
+            const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+            tc[j] = 0;
+            if (d < nb) {
+#pragma unroll
+                for (int w = 0; w < kRsWaves; ++w) tc[j] += base[w][d];
+                if (ntile == 1) gst[d] = tc[j];
+            }
+        }
+        if (ntile == 1) {                           // one tile: positions from its own counts
+            __syncthreads();
+            if (wv == 0) {
+                uint32_t carry = s0;
+                for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
+                    const uint32_t d = d0 + (uint32_t)lane;
+                    const uint32_t x = d < nb ? gst[d] : 0u;
+                    const uint32_t inc = wave_incl_scan(x);
+                    if (d < nb) gst[d] = carry + inc - x;
+                    carry += __builtin_amdgcn_readlane(inc, 63);
+                }
+            }
+        }
+        __syncthreads();
+        rs_tile_scatter<R>(k, v, i0, n_end, 0, lbits, base, gst, kout, vout);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kDPT; ++j) {
+            const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+            if (d < nb) gst[d] += tc[j];
+        }
+    }
 }
 
 // ---- one-sweep slot sort (ina_set_tuning key 12 = 1; measured slower, kept for the lab)
@@ -1206,6 +1318,9 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     const bool ack_hint = fast && sp.passes * sp.bits <= 31 && g_ack_fast.load();
     const bool small = npk <= (size_t)INA_SWITCH_SMALL_MAX && g_small_sort.load();
     const bool onesweep = !small && g_sort_mode.load() == 1 && npk < ((size_t)1 << 30);
+    // bucket + local sort: two-digit keys only (the low digit is one workgroup's LDS bins)
+    const int mode = g_sort_mode.load();
+    const bool hybrid = !small && (mode == 0 || mode == 2) && sp.passes == 2;
     if (onesweep) {
         // memset(aux) + keys/histograms + one kernel per digit pass
         const int R = os_rounds_for(npk);
@@ -1250,14 +1365,25 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             hipLaunchKernelGGL((k_switch_sort_small<unsigned long long, 32>), dim3(1), dim3(kSmallBlock), 0,
                                s, pkts, (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
+    } else if (hybrid) {
+        // high digit (bits lb..eb-1) over the whole batch, then each bucket on its low digit
+        const int lb = end_bit_for(st->num_slots) - sp.bits;
+        hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
+                           reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
+                           st->switch_id, kc, actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
+        hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, hist, sp.nch, nb, totals);
+        hipLaunchKernelGGL(k_sc0, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn, vn, npk, lb, sp.bits,
+                           hist, totals, sp.nch);
+        hipLaunchKernelGGL(k_rs_local<kRsRounds>, dim3(nb), dim3(kRsBlock), 0, s, kn, vn, kc, vc, lb, totals);
+        if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
         hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
                            reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
-                           st->switch_id, k_in, actions, sp.bits, hist, sp.nch, ack_hint ? 1 : 0);
+                           st->switch_id, k_in, actions, sp.bits, 0, hist, sp.nch, ack_hint ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
     }
     // r01 digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
-    for (int pass = 0; pass < (small || onesweep ? 0 : sp.passes); ++pass) {
+    for (int pass = 0; pass < (small || onesweep || hybrid ? 0 : sp.passes); ++pass) {
         const int shift = pass * sp.bits;
         if (pass > 0)
             hipLaunchKernelGGL(k_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits, hist,

@@ -588,8 +588,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     switch_small_sort the one-workgroup key+sort path for switch batches <= 4096 packets,
     switch_window the sorted positions one wave of the switch run kernel owns (0 = auto,
     1..64), switch_ack_fast the lane-parallel path for PS acks alone in their slot's
-    segment, switch_sort the slot sort (0 histogram / column-scan / scatter passes, 1
-    one-sweep passes with decoupled look-back), switch_sort_rounds the sort tile of either
+    segment, switch_sort the slot sort (0 auto = bucket + local where the keys have two
+    digits, 1 one-sweep passes with decoupled look-back, 2 bucket + local, 3 histogram /
+    column-scan / scatter digit passes), switch_sort_rounds the sort tile of either
     sort (64-item rounds per wave: 0 auto, 4, 8, 16), ew_blocks the grid cap of the one-in
     one-out elementwise kernels (default 2^24: one 16-byte chunk per thread); unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""

@@ -462,12 +462,13 @@ def test_send_gradients_fd_over_socketpair():
 # --------------------------------------------------------------------------------------
 # device packet-stream switch vs the oracle's P4 restatement
 # --------------------------------------------------------------------------------------
-def make_stream(rng, V, nslots_used, W, num_slots, collide=0.05, ack=0.1, other=0.05, stride=None):
+def make_stream(rng, V, nslots_used, W, num_slots, collide=0.05, ack=0.1, other=0.05, stride=None,
+                idx_hi=None):
     pk = []
     for s in range(nslots_used):
         frag = int(rng.integers(0, 4)) if rng.random() < 0.1 else 1000 + s
         deg = int(rng.choice([W, W, W, 1, 0, 2]))
-        idx = int(rng.integers(0, num_slots * 2))
+        idx = int(rng.integers(0, idx_hi or num_slots * 2))
         for w in range(W):
             vals = rand_i32(rng, V)
             f = frag if rng.random() > collide else frag + 1
@@ -556,15 +557,17 @@ def test_switch_fuzz_vs_oracle(seed):
     assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
 
 
-# slot sort variants: (sort 0 = histogram passes / 1 = one-sweep, descriptors, one-sweep rounds)
-SORT_VARIANTS = [(0, True, 0), (0, False, 0), (1, False, 4), (1, True, 16), (1, False, 8)]
+# slot sort variants: (sort 0 = auto / 1 = one-sweep / 2 = bucket + local / 3 = r01
+# histogram passes, descriptors, tile rounds)
+SORT_VARIANTS = [(3, True, 0), (3, False, 0), (1, False, 4), (1, True, 16), (1, False, 8),
+                 (2, True, 0), (2, False, 0), (0, True, 0)]
 
 
 @pytest.mark.parametrize("variant", SORT_VARIANTS)
 @pytest.mark.parametrize("seed", range(8))
 def test_switch_sort_paths_vs_oracle(seed, variant):
     """Batches above the one-workgroup size (> 2,048 packets) through each slot sort --
-    the one-sweep passes (decoupled look-back; tiles of 1,024 / 2,048 / 4,096 items; keys
+    bucket + local (the default for 2^10..2^18-slot pools), the one-sweep passes (decoupled look-back; tiles of 1,024 / 2,048 / 4,096 items; keys
     from the packet headers or from the batch's descriptors) and the r01 histogram /
     column-scan / scatter passes -- bit-exact against the P4 restatement, state carried
     across batches, pools of 1 .. 2^18 slots (1-3 digit passes)."""
@@ -604,6 +607,39 @@ def test_switch_sort_paths_vs_oracle(seed, variant):
         assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
     finally:
         o.set_tuning(switch_sort=0, switch_sort_rounds=0)
+
+
+@pytest.mark.parametrize("sort", [3, 2])
+@pytest.mark.parametrize("case", ["one_bucket", "one_slot", "two_buckets"])
+def test_switch_skewed_buckets_vs_oracle(sort, case):
+    """Slot use concentrated in one or two sort buckets (2^8 consecutive slots of a 2^17
+    pool), so a bucket holds more than one 4,096-item tile and the bucket + local sort takes
+    its multi-tile path (a counting sweep, then the tiles in order); one case puts every
+    packet in ONE slot (a segment of > 4,096 packets).  Bit-exact against the P4
+    restatement with state carried across batches, for the bucket sort and the r01 passes."""
+    rng = np.random.default_rng({"one_bucket": 1, "one_slot": 2, "two_buckets": 3}[case])
+    o = ops()
+    V, num_slots, W = 32, 1 << 17, 16
+    idx_hi = {"one_bucket": 256, "one_slot": 1, "two_buckets": 512}[case]
+    o.set_tuning(switch_sort=sort)
+    try:
+        sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
+        sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+        for rnd in range(2):
+            stream = make_stream(rng, V, 700, W, num_slots, collide=0.05, ack=0.05, other=0.05,
+                                 idx_hi=idx_hi)
+            assert stream.shape[0] > 2 * 4096
+            want_pk, want_act = sw_orc.run(stream, stride=o.nga_stride(V))
+            d = dev(stream)
+            act = sw_dev.process(d)
+            assert np.array_equal(host(act), want_act), rnd
+            assert np.array_equal(host(d), want_pk), rnd
+        cnt, frag, regs = sw_orc.registers()
+        assert np.array_equal(host(sw_dev.count), cnt)
+        assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+        assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+    finally:
+        o.set_tuning(switch_sort=0)
 
 
 @pytest.mark.parametrize("V,stride_kind", [(32, "padded"), (256, "padded"), (33, "tight"),

@@ -1,5 +1,5 @@
 """Lab: ina_switch_process on config 3's packet stream (8 workers x 102,400 NGA-256
-packets, 2^17-slot pool) per slot-sort variant -- the r01 passes vs the one-sweep sort,
+packets, 2^17-slot pool) per slot-sort variant -- the r01 passes vs the one-sweep sort vs bucket + local,
 keys from the packet headers vs from the pack kernel's descriptors, one-sweep tile sizes.
 Interleaved rounds, HIP events around each process() call, median per variant; every
 variant's actions are checked against the first one's.
@@ -19,15 +19,17 @@ sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
 from ina_amd import ops  # noqa: E402
 
 VARIANTS = {                      # name: (sort, rounds, use descriptors)
-    "r01_hdr": (0, 0, False),
-    "r01_desc": (0, 0, True),
-    "r01_desc_r4": (0, 4, True),
-    "r01_desc_r8": (0, 8, True),
+    "r01_hdr": (3, 0, False),
+    "r01_desc": (3, 0, True),
+    "r01_desc_r4": (3, 4, True),
+    "r01_desc_r8": (3, 8, True),
     "os_hdr": (1, 0, False),
     "os_desc": (1, 0, True),
     "os_desc_r4": (1, 4, True),
     "os_desc_r8": (1, 8, True),
     "os_desc_r16": (1, 16, True),
+    "hyb_hdr": (2, 0, False),
+    "hyb_desc": (2, 0, True),
 }
 
 
