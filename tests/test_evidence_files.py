@@ -8,10 +8,11 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = os.path.join(REPO, "profiles")
+RD = os.environ.get("INA_EVIDENCE_ROUND", "r02")
 
 
 def test_bench_line_and_traffic_agree():
-    b = json.load(open(os.path.join(P, "r01", "bench.json")))
+    b = json.load(open(os.path.join(P, RD, "bench.json")))
     t = json.load(open(os.path.join(P, "traffic_sum_reduce_c3.json")))
     rf = b["roofline"]
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Regenerate the "Measured (MI355X)" column of DESIGN.md's kernel table (§4) from the
-committed evidence: profiles/r01/bench.json, bench_extra.json, kernel_stats_bench.csv,
-profiles/traffic_switch.json and traffic_sum_reduce_c3.json.  Static notes (what a row's
+committed evidence of one round (INA_EVIDENCE_ROUND, default r02): profiles/<round>/bench.json,
+bench_extra.json, kernel_stats_bench.csv, traffic_switch.json, profiles/traffic_sum_reduce_c3.json,
+and the driver's own bench line of the previous round (BENCH_r*.json at the repo root).  Static notes (what a row's
 history was, lab references) are kept verbatim after the numbers.
 
 usage: design_table.py SESSION_TAG [--check]
@@ -9,19 +10,33 @@ usage: design_table.py SESSION_TAG [--check]
 import csv
 import json
 import os
+import re
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = os.path.join(REPO, "profiles")
+RD = os.environ.get("INA_EVIDENCE_ROUND", "r02")
+
+
+def driver_bench():
+    """(file, avg_launch_us, frac) of the newest driver BENCH_rNN.json, or None."""
+    fs = sorted(f for f in os.listdir(REPO) if re.fullmatch(r"BENCH_r\d+\.json", f))
+    for f in reversed(fs):
+        try:
+            rf = json.load(open(os.path.join(REPO, f)))["parsed"]["roofline"]
+            return f, rf["avg_launch_us"], rf["frac"]
+        except Exception:
+            continue
+    return None
 
 
 def load():
-    bench = json.load(open(os.path.join(P, "r01", "bench.json")))
-    extra = {r["kernel"]: r for r in json.load(open(os.path.join(P, "r01", "bench_extra.json")))["rows"]}
-    sw = json.load(open(os.path.join(P, "traffic_switch.json")))["kernels"]
+    bench = json.load(open(os.path.join(P, RD, "bench.json")))
+    extra = {r["kernel"]: r for r in json.load(open(os.path.join(P, RD, "bench_extra.json")))["rows"]}
+    sw = json.load(open(os.path.join(P, RD, "traffic_switch.json")))["kernels"]
     tr = json.load(open(os.path.join(P, "traffic_sum_reduce_c3.json")))
     prof_us = None
-    for r in csv.DictReader(open(os.path.join(P, "r01", "kernel_stats_bench.csv"))):
+    for r in csv.DictReader(open(os.path.join(P, RD, "kernel_stats_bench.csv"))):
         if "k_sum_reduce_i32_vec<8, 4, true>" in r["Name"]:
             prof_us = float(r["AverageNs"]) / 1e3
     return bench, extra, sw, tr, prof_us
@@ -35,6 +50,8 @@ def row_cells(tag):
     bench, ex, sw, tr, prof_us = load()
     e = lambda k: ex[k]                                              # noqa: E731
     rf = bench["roofline"]
+    d = driver_bench()
+    drv = (f"the driver's {d[0]}: {d[1]:.2f} µs = {100 * d[2]:.1f} %" if d else "no driver bench yet")
     keys = sorted(sw, key=lambda k: -sw[k]["avg_us"])
     run2 = next(k for k in keys if "k_switch_run2" in k)
     kk = next(k for k in keys if "k_switch_keys" in k)
@@ -44,8 +61,8 @@ def row_cells(tag):
     return {
         "`k_sum_reduce_i32_vec<W=8,U=4>`":
             f"**{rf['avg_launch_us']:.1f} µs, {rf['achieved'] / 1e3:.2f} TB/s = {100 * rf['frac']:.1f} %** "
-            f"on the {tag} box (bench.py events; rocprof {prof_us:.1f} µs; 143.4–150.7 µs = 78–82 % "
-            f"across boxes this round; {e('sum_reduce_i32 W=8')['us']:.1f} µs with the cold flush of this "
+            f"on the {tag} box (bench.py events; rocprof {prof_us:.1f} µs; {drv}; "
+            f"{e('sum_reduce_i32 W=8')['us']:.1f} µs with the cold flush of this "
             f"table); PMC traffic {tr['hbm_bytes_per_launch']:,} B = {tr['traffic_over_algorithmic']:.5f}× "
             f"algorithmic",
         "same, W = 2 / 4 / 16":
@@ -66,12 +83,15 @@ def row_cells(tag):
         "`k_absmax_f32`": fmt(e("absmax_f32 ResNet-50 delta (dynamic scale)")),
         "`k_pack_c128`": fmt(e("pack_c128 ResNet-50")),
         "`ina_switch_process` (819,200":
-            fmt(e("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort)"))
-            + f" event-timed; under rocprof ({tag}, `profiles/traffic_switch.json`) `k_switch_run2` "
+            fmt(e("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from descriptors)"))
+            + " with keys from the pack kernels' descriptors ("
+            + fmt(e("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from headers)"))
+            + " from the headers)"
+            + f" event-timed; under rocprof ({tag}, `profiles/{RD}/traffic_switch.json`) `k_switch_run2` "
               f"{sw[run2]['avg_us']:.1f} µs moving "
               f"{(sw[run2]['hbm_read_bytes'] + sw[run2]['hbm_write_bytes']) / 1e9:.2f} GB at "
-              f"{sw[run2]['TB_per_s']:.1f} TB/s, keys {sw[kk]['avg_us']:.1f} µs (one 128-byte line per "
-              f"packet, {sw[kk]['hbm_read_bytes'] / 1e6:.0f} MB), sort passes {sort_us:.1f} µs",
+              f"{sw[run2]['TB_per_s']:.1f} TB/s, keys {sw[kk]['avg_us']:.1f} µs "
+              f"({sw[kk]['hbm_read_bytes'] / 1e6:.1f} MB read), sort passes {sort_us:.1f} µs",
         "`ina_switch_process`, small batches":
             ", ".join(f"{k.split(': ')[1].split(' NGA')[0]} packets {r['us']:.1f} µs"
                       for k, r in ((r['kernel'], r) for r in small))
@@ -126,8 +146,8 @@ def main():
         c[3] = cells[key] + NOTES.get(key, "")
         out.append("| " + " | ".join(c) + " |")
     s2 = s[:i] + "\n".join(out) + s[j:]
-    s2 = s2.replace("`profiles/r01/bench_extra.json` (session ", "`profiles/r01/bench_extra.json` (session ", 1)
-    k = s2.index("`profiles/r01/bench_extra.json` (session ") + len("`profiles/r01/bench_extra.json` (session ")
+    s2 = re.sub(r"`profiles/r\d+/bench_extra\.json` \(session ", f"`profiles/{RD}/bench_extra.json` (session ", s2, 1)
+    k = s2.index(f"`profiles/{RD}/bench_extra.json` (session ") + len(f"`profiles/{RD}/bench_extra.json` (session ")
     s2 = s2[:k] + tag + s2[s2.index(",", k):]
     if "--check" in sys.argv:
         print("\n".join(out))

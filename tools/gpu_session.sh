@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; the script stops at the first crash,
 # abort or timeout (only an ordinary pytest failure, rc 1, lets it continue).
 # usage: tools/gpu_session.sh TAG [stages...]   stages: smoke test bench prof pmc extra swprof
-#        config1 rehearse sharded swlab
+#        config1 rehearse sharded swlab pathprof
 set -u
 TAG=${1:-r02}; shift || true
 STAGES=${*:-"smoke test bench prof pmc extra"}
@@ -42,6 +42,10 @@ for st in $STAGES; do
           python3 tools/prof_switch.py > "$OUT/swpmc_$c.log" 2>&1
         rc=$?; tail -2 "$OUT/swpmc_$c.log"; [ $rc -ne 0 ] && fatal "swpmc $c" $rc
       done ;;
+    pathprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pathprof" -o run -- \
+        python3 tools/prof_path.py > "$OUT/pathprof.log" 2>&1
+      rc=$?; tail -2 "$OUT/pathprof.log"; [ $rc -ne 0 ] && fatal pathprof $rc ;;
     config1)
       timeout -k 10 600 python examples/config1_loopback.py --epochs 3 --local-steps 5 > "$OUT/config1.log" 2>&1
       rc=$?; tail -8 "$OUT/config1.log"; [ $rc -ne 0 ] && fatal config1 $rc ;;

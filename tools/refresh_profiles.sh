@@ -1,10 +1,12 @@
 #!/bin/bash
-# Copy one gpu_session.sh run (stages bench prof pmc extra swprof) into profiles/r01 and
-# regenerate the traffic summaries.  usage: tools/refresh_profiles.sh TAG
+# Copy one gpu_session.sh run (stages test bench prof pmc extra swprof [rehearse sharded
+# config1 pathprof]) into profiles/<round> and regenerate the traffic summaries, DESIGN.md's
+# kernel table and profiles/README.md.  usage: tools/refresh_profiles.sh TAG
 set -eu
 TAG=$1
 S=gpurun_out/$TAG
-D=profiles/r01
+D=profiles/${INA_EVIDENCE_ROUND:-r02}
+mkdir -p "$D"
 cp "$S/bench.json" "$D/bench.json"
 cp "$S/prof/run_kernel_stats.csv" "$D/kernel_stats_bench.csv"
 cp "$S/pmc_FETCH_SIZE/run_counter_collection.csv" "$D/pmc_FETCH_SIZE.csv"
@@ -13,7 +15,14 @@ python tools/pmc_traffic.py "$S" "k_sum_reduce_i32_vec<8, 4, true>" profiles/tra
 cp "$S/swprof/run_kernel_stats.csv" "$D/kernel_stats_switch.csv"
 cp "$S/swpmc_FETCH_SIZE/run_counter_collection.csv" "$D/switch_pmc_FETCH_SIZE.csv"
 cp "$S/swpmc_WRITE_SIZE/run_counter_collection.csv" "$D/switch_pmc_WRITE_SIZE.csv"
-python tools/switch_traffic.py "$S" profiles/traffic_switch.json "$TAG" > /dev/null
+python tools/switch_traffic.py "$S" "$D/traffic_switch.json" "$TAG" > /dev/null
 cp "$S/bench_extra.json" "$D/bench_extra.json"
-echo "profiles refreshed from $TAG"
+# optional stages
+[ -f "$S/pytest_gpu.log" ] && cp "$S/pytest_gpu.log" "$D/pytest_gpu.log"
+[ -f "$S/rehearse2.json" ] && cp "$S/rehearse2.json" "$D/rehearse_2ranks_gloo.json"
+[ -f "$S/sharded1_i32.json" ] && cp "$S/sharded1_i32.json" "$D/sharded_c5_1gpu_i32.json"
+[ -f "$S/sharded1_i16.json" ] && cp "$S/sharded1_i16.json" "$D/sharded_c5_1gpu_i16.json"
+[ -f "$S/config1.log" ] && cp "$S/config1.log" "$D/config1_loopback.log"
+[ -f "$S/pathprof/run_kernel_stats.csv" ] && cp "$S/pathprof/run_kernel_stats.csv" "$D/kernel_stats_packet_path.csv"
+echo "profiles refreshed from $TAG into $D"
 python tools/design_table.py "$TAG" && python tools/profiles_readme.py "$TAG"
