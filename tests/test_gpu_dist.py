@@ -139,3 +139,17 @@ def test_i16_wire_kernels_vs_oracle(n, V):
         ovf = torch.full(((n + V - 1) // V,), 7, dtype=torch.uint8, device=dev)
         ops.i16_wire_finish(src[off:], k, V, overflow=ovf, want_out16=False, want_y=False)
         assert np.array_equal(ovf.cpu().numpy(), wovf)
+
+
+@pytest.mark.gpu
+def test_rccl_world1_collectives_on_this_image():
+    """The config-5 collectives through RCCL itself (backend nccl, one rank: one GPU
+    cannot host two RCCL ranks), so the N > 1 bench's calls -- process group with
+    device_id, reduce_scatter_tensor(int32, SUM), all_gather_into_tensor (fp32, uint8),
+    all_reduce(float64, MAX/MIN) -- are known to run on this ROCm/RCCL image."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "tests", "_rccl_world1.py")]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "rccl world-1 collectives ok" in r.stdout
