@@ -136,22 +136,23 @@ __device__ __forceinline__ void lds_count(uint32_t* h, uint32_t d, bool valid) {
 // LDS first, so each digit leaves as one contiguous run, measured no faster (pass 0
 // 15.1 -> 17.9 us, pass 1 17.9 -> 17.3 us at 819,200 packets: the passes are bound by
 // their dependent phases, not by the scattered stores; profiles/r02/lab/switch_sort_lab)
-template <int R>
+template <int R, int NW = kRsWaves>
 __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const uint32_t (&v)[R],
                                                 size_t i0, size_t n, int shift, int bits,
                                                 uint32_t (*base)[kRsBins], const uint32_t* gst,
                                                 uint32_t* __restrict__ kout,
-                                                uint32_t* __restrict__ vout) {
+                                                uint32_t* __restrict__ vout, int rw = R) {
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const uint32_t nb = 1u << bits;
-    constexpr int kDPT = kRsBins / kRsBlock;
+    constexpr int kThr = NW * 64;
+    constexpr int kDPT = (kRsBins + kThr - 1) / kThr;
 #pragma unroll
     for (int j = 0; j < kDPT; ++j) {
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        const uint32_t d = threadIdx.x + (uint32_t)j * kThr;
         if (d >= nb) continue;
         uint32_t b = gst[d];
 #pragma unroll
-        for (int w = 0; w < kRsWaves; ++w) {
+        for (int w = 0; w < NW; ++w) {
             const uint32_t cw = base[w][d];
             base[w][d] = b;
             b += cw;
@@ -161,7 +162,7 @@ __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const ui
     const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (i0 - (size_t)lane + (size_t)r * 64 >= n) break;      // wave-uniform
+        if (r >= rw || i0 - (size_t)lane + (size_t)r * 64 >= n) break;   // wave-uniform
         const bool valid = i0 + (size_t)r * 64 < n;
         const uint32_t d = (k[r] >> shift) & (nb - 1);
         const unsigned long long pm = lanes_with_digit(d, bits, valid);
@@ -474,43 +475,43 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
 // sees the same arrays; the second pass's histogram and column-scan launches and its
 // global rank bookkeeping are gone.  A bucket larger than one tile (skewed slot use) is
 // sorted tile by tile: a counting sweep over the bucket first, then the tiles in order.
-template <int R>
-__global__ __launch_bounds__(kRsBlock) void k_rs_local(const uint32_t* __restrict__ kin,
-                                                       const uint32_t* __restrict__ vin,
-                                                       uint32_t* __restrict__ kout,
-                                                       uint32_t* __restrict__ vout, int lbits,
-                                                       const uint32_t* __restrict__ totals) {
-    __shared__ uint32_t base[kRsWaves][kRsBins];
+#ifndef INA_LOCAL_WAVES
+#define INA_LOCAL_WAVES 16
+#endif
+constexpr int kLcWaves = INA_LOCAL_WAVES;           // waves per bucket workgroup
+constexpr int kLcRounds = 64 / kLcWaves > 4 ? 64 / kLcWaves : 4;   // tile = max(4096, 256 x waves) items
+template <int NW, int R>
+__global__ __launch_bounds__(NW * 64) void k_rs_local(const uint32_t* __restrict__ kin,
+                                                      const uint32_t* __restrict__ vin,
+                                                      uint32_t* __restrict__ kout,
+                                                      uint32_t* __restrict__ vout, int lbits,
+                                                      const uint32_t* __restrict__ totals) {
+    constexpr int kThr = NW * 64;
+    constexpr int kDPT = (kRsBins + kThr - 1) / kThr;
+    __shared__ uint32_t base[NW][kRsBins];
     __shared__ uint32_t gst[kRsBins];               // bucket digit counts, then output positions
-    __shared__ uint32_t red[kRsWaves];
+    __shared__ uint32_t red[NW];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const uint32_t b = blockIdx.x;
     // bucket start = sum of the earlier buckets' totals (high-digit pass)
     uint32_t part = 0;
-    for (uint32_t d = threadIdx.x; d < b; d += kRsBlock) part += totals[d];
+    for (uint32_t d = threadIdx.x; d < b; d += kThr) part += totals[d];
     part = __builtin_amdgcn_readlane(wave_incl_scan(part), 63);
     if (lane == 0) red[wv] = part;
     const uint32_t cnt = totals[b];
     const uint32_t nb = 1u << lbits;
-    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) gst[d] = 0;
+    for (uint32_t d = threadIdx.x; d < nb; d += kThr) gst[d] = 0;
     __syncthreads();
     if (cnt == 0) return;                           // block-uniform
     uint32_t s0 = 0;
 #pragma unroll
-    for (int w = 0; w < kRsWaves; ++w) s0 += red[w];
-    constexpr uint32_t kTile = (uint32_t)kRsWaves * 64u * (uint32_t)R;
+    for (int w = 0; w < NW; ++w) s0 += red[w];
+    constexpr uint32_t kTile = (uint32_t)kThr * (uint32_t)R;
     const uint32_t ntile = (cnt + kTile - 1) / kTile;
     const size_t n_end = (size_t)s0 + cnt;
-    constexpr int kDPT = kRsBins / kRsBlock;
     if (ntile > 1) {                                // bucket digit totals -> output positions
-        for (uint32_t t = 0; t < ntile; ++t) {
-            const size_t i0 = (size_t)s0 + (size_t)t * kTile + (size_t)wv * (64 * R) + (size_t)lane;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const size_t i = i0 + (size_t)r * 64;
-                lds_count(gst, (i < n_end ? kin[i] : 0u) & (nb - 1), i < n_end);
-            }
-        }
+        for (size_t i = (size_t)s0 + (size_t)wv * 64 + (size_t)lane; i - (size_t)lane < n_end; i += kThr)
+            lds_count(gst, (i < n_end ? kin[i] : 0u) & (nb - 1), i < n_end);
         __syncthreads();
         if (wv == 0) {
             uint32_t carry = s0;
@@ -524,28 +525,34 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_local(const uint32_t* __restric
         }
     }
     for (uint32_t t = 0; t < ntile; ++t) {
-        const size_t i0 = (size_t)s0 + (size_t)t * kTile + (size_t)wv * (64 * R) + (size_t)lane;
+        // the tile's items split evenly over the waves in order (wave w: rw rounds of 64
+        // consecutive items), so a 2,048-item bucket is 2 rounds per wave, not 8 of 4 waves
+        const uint32_t tn = min(kTile, cnt - t * kTile);
+        const int rw = (int)((tn + (uint32_t)kThr - 1) / (uint32_t)kThr);
+        const size_t i0 = (size_t)s0 + (size_t)t * kTile + (size_t)wv * 64 * (size_t)rw + (size_t)lane;
+        const size_t t_end = (size_t)s0 + (size_t)t * kTile + tn;
         uint32_t k[R], v[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const size_t i = i0 + (size_t)r * 64;
-            k[r] = i < n_end ? kin[i] : 0u;
-            v[r] = i < n_end ? vin[i] : 0u;
+            const bool ok = r < rw && i < t_end;
+            k[r] = ok ? kin[i] : 0u;
+            v[r] = ok ? vin[i] : 0u;
         }
         for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            lds_count(base[wv], k[r] & (nb - 1), i0 + (size_t)r * 64 < n_end);
+            if (r < rw) lds_count(base[wv], k[r] & (nb - 1), i0 + (size_t)r * 64 < t_end);
         __syncthreads();
         uint32_t tc[kDPT];                          // this tile's count per digit
 #pragma unroll
         for (int j = 0; j < kDPT; ++j) {
-            const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+            const uint32_t d = threadIdx.x + (uint32_t)j * kThr;
             tc[j] = 0;
             if (d < nb) {
 #pragma unroll
-                for (int w = 0; w < kRsWaves; ++w) tc[j] += base[w][d];
+                for (int w = 0; w < NW; ++w) tc[j] += base[w][d];
                 if (ntile == 1) gst[d] = tc[j];
             }
         }
@@ -563,11 +570,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_local(const uint32_t* __restric
             }
         }
         __syncthreads();
-        rs_tile_scatter<R>(k, v, i0, n_end, 0, lbits, base, gst, kout, vout);
+        rs_tile_scatter<R, NW>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kDPT; ++j) {
-            const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+            const uint32_t d = threadIdx.x + (uint32_t)j * kThr;
             if (d < nb) gst[d] += tc[j];
         }
     }
@@ -1374,7 +1381,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, hist, sp.nch, nb, totals);
         hipLaunchKernelGGL(k_sc0, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn, vn, npk, lb, sp.bits,
                            hist, totals, sp.nch);
-        hipLaunchKernelGGL(k_rs_local<kRsRounds>, dim3(nb), dim3(kRsBlock), 0, s, kn, vn, kc, vc, lb, totals);
+        hipLaunchKernelGGL((k_rs_local<kLcWaves, kLcRounds>), dim3(nb), dim3(kLcWaves * 64), 0, s, kn, vn, kc, vc, lb,
+                           totals);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
         hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
