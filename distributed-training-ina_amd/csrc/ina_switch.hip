@@ -180,8 +180,8 @@ __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const ui
 //    are not this switch's (switch_check miss, ngaa.p4:27-37,184-186); fused with the
 //    first digit pass's chunk histogram.
 constexpr uint32_t kAckBit = 0x80000000u;
-template <int R, bool kDesc>
-__global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restrict__ pkts,
+template <int R, bool kDesc, int NW = kRsWaves>
+__global__ __launch_bounds__(NW * 64) void k_switch_keys(const uint8_t* __restrict__ pkts,
                                                           const uint2* __restrict__ desc,
                                                           size_t npk, size_t stride,
                                                           uint32_t num_slots, int switch_id,
@@ -193,9 +193,9 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
     const uint32_t nb = 1u << bits;
-    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) h[d] = 0;
+    for (uint32_t d = threadIdx.x; d < nb; d += NW * 64) h[d] = 0;
     __syncthreads();
-    const size_t p0 = c * (kRsWaves * 64 * R) + (size_t)wv * (64 * R) + (size_t)lane;
+    const size_t p0 = c * (NW * 64 * R) + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t idx[R], sid[R], ack[R];
     if (kDesc) {                                               // descriptors: header bytes 4..11
 #pragma unroll
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(kRsBlock) void k_switch_keys(const uint8_t* __restr
         lds_count(h, (key >> shift) & (nb - 1), p < npk);
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < nb; d += kRsBlock) hist[d * nch + c] = h[d];
+    for (uint32_t d = threadIdx.x; d < nb; d += NW * 64) hist[d * nch + c] = h[d];
 }
 
 // 1b. batches of at most kSmallBatch packets (recvmmsg-sized, where launch latency and not
@@ -404,8 +404,8 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_colscan(uint32_t* __restrict__ 
 
 // scatter: out position = base(digit, chunk, wave) + items of that digit the wave already
 // placed + rank among this round's lanes with the same digit
-template <bool kIds, int R>
-__global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restrict__ kin,
+template <bool kIds, int R, int NW = kRsWaves>
+__global__ __launch_bounds__(NW * 64) void k_rs_scatter(const uint32_t* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin,
                                                          uint32_t* __restrict__ kout,
                                                          uint32_t* __restrict__ vout, size_t n,
@@ -413,12 +413,12 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
                                                          const uint32_t* __restrict__ colpref,
                                                          const uint32_t* __restrict__ totals,
                                                          size_t nch) {
-    __shared__ uint32_t base[kRsWaves][kRsBins];   // per-wave counts, then per-wave bases
+    __shared__ uint32_t base[NW][kRsBins];   // per-wave counts, then per-wave bases
     __shared__ uint32_t dbase[kRsBins];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
     const uint32_t nb = 1u << bits;
-    const size_t tile0 = c * (kRsWaves * 64 * R);
+    const size_t tile0 = c * (NW * 64 * R);
     const size_t i0 = tile0 + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t k[R], v[R];
 #pragma unroll
@@ -428,18 +428,18 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
         v[r] = kIds ? (i < n ? vin[i] : 0u) : (uint32_t)i;
     }
     // digit totals and this chunk's column prefixes: loaded with the keys, one round trip
-    constexpr int kDPT = kRsBins / kRsBlock;         // digits per thread
+    constexpr int kDPT = (kRsBins + NW * 64 - 1) / (NW * 64);   // digits per thread
     uint32_t tot[kDPT], cpf[kDPT];
 #pragma unroll
     for (int j = 0; j < kDPT; ++j) {
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        const uint32_t d = threadIdx.x + (uint32_t)j * (NW * 64);
         tot[j] = d < nb ? totals[d] : 0u;
         cpf[j] = d < nb ? colpref[d * nch + c] : 0u;
     }
     for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
 #pragma unroll
     for (int j = 0; j < kDPT; ++j) {
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        const uint32_t d = threadIdx.x + (uint32_t)j * (NW * 64);
         if (d < nb) dbase[d] = tot[j];
     }
     __syncthreads();
@@ -459,11 +459,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rs_scatter(const uint32_t* __restr
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kDPT; ++j) {                 // the tile's first output position per digit
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
+        const uint32_t d = threadIdx.x + (uint32_t)j * (NW * 64);
         if (d < nb) dbase[d] += cpf[j];
     }
     __syncthreads();
-    rs_tile_scatter<R>(k, v, i0, n, shift, bits, base, dbase, kout, vout);
+    rs_tile_scatter<R, NW>(k, v, i0, n, shift, bits, base, dbase, kout, vout);
 }
 
 // ---- bucket + local slot sort (ina_set_tuning key 12 = 2) -----------------------------
@@ -1373,14 +1373,30 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                s, pkts, (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else if (hybrid) {
-        // high digit (bits lb..eb-1) over the whole batch, then each bucket on its low digit
+        // high digit (bits lb..eb-1) over the whole batch, then each bucket on its low digit.
+        // The high pass's chunks (4 waves x 64 x rounds items) run as 16 waves x rounds/4,
+        // so each wave's dependent LDS-count / rank rounds are 4x fewer
         const int lb = end_bit_for(st->num_slots) - sp.bits;
-        hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
-                           reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
-                           st->switch_id, kc, actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
+        constexpr int kHw = 16;
+        const dim3 hb(kHw * 64);
+        const uint2* dsc = reinterpret_cast<const uint2*>(desc);
+        if (sp.rounds == kR2) {
+            hipLaunchKernelGGL((desc ? &k_switch_keys<kR2 / 4, true, kHw> : &k_switch_keys<kR2 / 4, false, kHw>),
+                               dim3(gc), hb, 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id, kc,
+                               actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
+        } else if (sp.rounds == kR1) {
+            hipLaunchKernelGGL((desc ? &k_switch_keys<kR1 / 4, true, kHw> : &k_switch_keys<kR1 / 4, false, kHw>),
+                               dim3(gc), hb, 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id, kc,
+                               actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
+        } else {
+            hipLaunchKernelGGL((desc ? &k_switch_keys<kR0 / 4, true, kHw> : &k_switch_keys<kR0 / 4, false, kHw>),
+                               dim3(gc), hb, 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id, kc,
+                               actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
+        }
         hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, hist, sp.nch, nb, totals);
-        hipLaunchKernelGGL(k_sc0, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn, vn, npk, lb, sp.bits,
-                           hist, totals, sp.nch);
+        auto* k_hs = sp.rounds == kR2 ? &k_rs_scatter<false, kR2 / 4, kHw>
+                   : sp.rounds == kR1 ? &k_rs_scatter<false, kR1 / 4, kHw> : &k_rs_scatter<false, kR0 / 4, kHw>;
+        hipLaunchKernelGGL(k_hs, dim3(gc), hb, 0, s, kc, nullptr, kn, vn, npk, lb, sp.bits, hist, totals, sp.nch);
         hipLaunchKernelGGL((k_rs_local<kLcWaves, kLcRounds>), dim3(nb), dim3(kLcWaves * 64), 0, s, kn, vn, kc, vc, lb,
                            totals);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
