@@ -485,8 +485,12 @@ __global__ __launch_bounds__(NW * 64) void k_rs_local(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ vin,
                                                       uint32_t* __restrict__ kout,
                                                       uint32_t* __restrict__ vout, int lbits,
-                                                      const uint32_t* __restrict__ totals) {
+                                                      const uint32_t* __restrict__ totals,
+                                                      uint32_t skip) {
     constexpr int kThr = NW * 64;
+    // the bucket holding nothing but foreign packets (sentinel key num_slots) is not sorted:
+    // they sort after every slot anyway and the run kernel skips them (nforeign)
+    if (blockIdx.x == skip) return;
     constexpr int kDPT = (kRsBins + kThr - 1) / kThr;
     __shared__ uint32_t base[NW][kRsBins];
     __shared__ uint32_t gst[kRsBins];               // bucket digit counts, then output positions
@@ -945,7 +949,11 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                                                           const uint32_t* __restrict__ keys,
                                                           const uint32_t* __restrict__ ids,
                                                           uint8_t* __restrict__ actions,
-                                                          uint32_t win, uint32_t kmask, PsFuse ps) {
+                                                          uint32_t win, uint32_t kmask, PsFuse ps,
+                                                          const uint32_t* __restrict__ nforeign) {
+    // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
+    // the run kernel never processes foreign packets, so it stops before them
+    if (nforeign) npk -= *nforeign;
     const int lane = threadIdx.x & 63;
     const int V = st.V;
     const int L = V >> 2;                       // lanes holding values
@@ -1328,6 +1336,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     // bucket + local sort: two-digit keys only (the low digit is one workgroup's LDS bins)
     const int mode = g_sort_mode.load();
     const bool hybrid = !small && (mode == 0 || mode == 2) && sp.passes == 2;
+    uint32_t skip_bucket = 0xFFFFFFFFu;
+    const uint32_t* nforeign = nullptr;
     if (onesweep) {
         // memset(aux) + keys/histograms + one kernel per digit pass
         const int R = os_rounds_for(npk);
@@ -1397,8 +1407,15 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         auto* k_hs = sp.rounds == kR2 ? &k_rs_scatter<false, kR2 / 4, kHw>
                    : sp.rounds == kR1 ? &k_rs_scatter<false, kR1 / 4, kHw> : &k_rs_scatter<false, kR0 / 4, kHw>;
         hipLaunchKernelGGL(k_hs, dim3(gc), hb, 0, s, kc, nullptr, kn, vn, npk, lb, sp.bits, hist, totals, sp.nch);
+        // a bucket of foreign packets only (a pool of a multiple of 2^lb slots): left where the
+        // high pass put them when the register-resident run kernel takes the batch (it stops
+        // before them); the generic run kernel reads every position, so then it is sorted
+        if (fast && (st->num_slots & ((1u << lb) - 1u)) == 0u) {
+            skip_bucket = st->num_slots >> lb;
+            nforeign = totals + skip_bucket;
+        }
         hipLaunchKernelGGL((k_rs_local<kLcWaves, kLcRounds>), dim3(nb), dim3(kLcWaves * 64), 0, s, kn, vn, kc, vc, lb,
-                           totals);
+                           totals, skip_bucket);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
         hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
@@ -1435,7 +1452,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         auto* run = ps.on ? &k_switch_run2<true> : &k_switch_run2<false>;
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc, vc, actions,
-                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps);
+                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign);
         *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));

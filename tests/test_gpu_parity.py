@@ -610,23 +610,25 @@ def test_switch_sort_paths_vs_oracle(seed, variant):
 
 
 @pytest.mark.parametrize("sort", [3, 2])
-@pytest.mark.parametrize("case", ["one_bucket", "one_slot", "two_buckets"])
+@pytest.mark.parametrize("case", ["one_bucket", "one_slot", "two_buckets", "foreign_heavy"])
 def test_switch_skewed_buckets_vs_oracle(sort, case):
     """Slot use concentrated in one or two sort buckets (2^8 consecutive slots of a 2^17
     pool), so a bucket holds more than one 4,096-item tile and the bucket + local sort takes
     its multi-tile path (a counting sweep, then the tiles in order); one case puts every
-    packet in ONE slot (a segment of > 4,096 packets).  Bit-exact against the P4
+    packet in ONE slot (a segment of > 4,096 packets), one is 70 % foreign packets (their
+    bucket is left unsorted at the end and the run kernel stops before it).  Bit-exact against the P4
     restatement with state carried across batches, for the bucket sort and the r01 passes."""
-    rng = np.random.default_rng({"one_bucket": 1, "one_slot": 2, "two_buckets": 3}[case])
+    rng = np.random.default_rng({"one_bucket": 1, "one_slot": 2, "two_buckets": 3, "foreign_heavy": 4}[case])
     o = ops()
     V, num_slots, W = 32, 1 << 17, 16
-    idx_hi = {"one_bucket": 256, "one_slot": 1, "two_buckets": 512}[case]
+    idx_hi = {"one_bucket": 256, "one_slot": 1, "two_buckets": 512, "foreign_heavy": None}[case]
+    other = 0.7 if case == "foreign_heavy" else 0.05      # packets for another switch
     o.set_tuning(switch_sort=sort)
     try:
         sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
         sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
         for rnd in range(2):
-            stream = make_stream(rng, V, 700, W, num_slots, collide=0.05, ack=0.05, other=0.05,
+            stream = make_stream(rng, V, 700, W, num_slots, collide=0.05, ack=0.05, other=other,
                                  idx_hi=idx_hi)
             assert stream.shape[0] > 2 * 4096
             want_pk, want_act = sw_orc.run(stream, stride=o.nga_stride(V))
