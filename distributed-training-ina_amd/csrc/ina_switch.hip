@@ -3,12 +3,16 @@
 // and the V Processor registers (processor.p4:14-24), restated on the device.
 //
 // A batch of NGA-V packets in arrival order is grouped by aggregator slot with a
-// stable radix sort (slot, arrival) -- slots are independent in the P4 program, so
-// per-slot arrival order is all that matters -- and each slot's packets are run
-// through the register state machine by ONE wave: the slot's V registers stay in
-// VGPRs for the whole segment, each packet is staged through LDS (16-byte loads of
-// the padded packet, byte-offset payload words at 15 + 4j extracted with
-// v_alignbyte), rewritten there (running sum, collision bit) and stored back.
+// stable sort (slot, arrival) -- slots are independent in the P4 program, so per-slot
+// arrival order is all that matters: by default one global pass on the key's high digit
+// and one workgroup per bucket of slots on the low digit (k_rs_local), else LSD digit
+// passes or a one-workgroup bitonic sort for small batches.  Each slot's packets are
+// then run through the register state machine by ONE wave (k_switch_run2): the slot's V
+// registers stay in VGPRs for the whole segment, lane l holds 16-byte chunk l of up to 8
+// packets at once, payload words at byte 15 + 4j are decoded with v_alignbyte from the
+// neighbouring lane's chunk (DPP), and a forwarded packet is re-encoded from the
+// registers.  Layouts that kernel does not take (V % 4 != 0, unaligned rows) run
+// k_switch_run, which stages each packet through LDS.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

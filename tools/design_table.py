@@ -122,7 +122,7 @@ NOTES = {
     "`k_dequantize_i16`": ": 4 values per lane (8-byte load, 16-byte store); was one 2-byte value per thread",
     "`k_pack_nga_flat<SrcQ32>`": "; was 80.9 µs (48 %) as a thread-per-chunk kernel that re-read and re-quantised a 5th value per chunk",
     "`k_apply_completed_nga`": "; was 98.6 µs (40 %) as one lane group per packet over every packet",
-    "`k_absmax_f32`": " at 256 workgroups; 86 µs at 8192 (one atomicMax per workgroup on one word serialises)",
+    "`k_absmax_f32`": " at 256 workgroups; 86 µs at 8192 (one atomicMax per workgroup on one word); a read-before-atomic skip changed nothing at 256 and larger grids stay slower with it (`profiles/r02/lab/absmax_skip_lab.log`)",
     "`k_unpack_nga_flat`": "; a thread-per-output-chunk variant (unbroken store stream, header chunks skipped by the loads) was 3 % faster without the header fields and 4 % slower with them (`profiles/r01/lab/unpack_out_lab.log`)",
     "`k_pack_c128`": ": thread per wire word (4-byte loads and stores, contiguous per instruction); a thread-per-16-byte-chunk variant that loads the aligned 8-word gradient window and selects per word was slower, 41.6 µs (`profiles/r01/lab/c128_lab.log`, `tools/lab/c128_lab.py`)",
 }
