@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Lab: the switch run kernel's gather without its state machine (tools/lab/gather_lab.hip)
+against ina_switch_process itself, on config 3's packet stream (8 workers x 102,400
+NGA-256 packets, 2^17-slot pool, keys from descriptors).  The sorted (slot, packet id)
+arrays are a stable torch sort of the packets' slots -- the order the switch's own sort
+produces.  Interleaved rounds, HIP events, median.
+
+  hipcc --offload-arch=gfx950 -O3 -shared -fPIC -o tools/lab/gather_lab.so tools/lab/gather_lab.hip
+  python tools/lab/gather_lab.py
+"""
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "distributed-training-ina_amd"))
+from ina_amd import ops  # noqa: E402
+
+lab = C.CDLL(os.path.join(HERE, "gather_lab.so"))
+lab.lab_gather.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_int,
+                           C.c_int, C.c_void_p]
+dev = torch.device("cuda")
+n, W, V, slots = 26_214_400, 8, 256, 1 << 17
+g = torch.Generator(device=dev).manual_seed(1)
+packed = []
+for w in range(W):
+    b = torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
+    packed.append(ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots, desc=True))
+    del b
+clean = torch.cat([p for p, _ in packed])
+desc = torch.cat([d for _, d in packed])
+del packed
+npk, stride = clean.shape
+slot_of = (torch.arange(n // V, device=dev, dtype=torch.int64) + 1) % slots     # seq0 = 1
+keys_all = slot_of.repeat(W)
+keys_sorted, order = torch.sort(keys_all, stable=True)
+keys32 = keys_sorted.to(torch.int32)
+ids32 = order.to(torch.int32)
+regs = torch.zeros(slots * V, dtype=torch.int32, device=dev)
+work = torch.empty_like(clean)
+sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
+acts = torch.empty(npk, dtype=torch.uint8, device=dev)
+st = torch.cuda.current_stream().cuda_stream
+algo = npk * stride + (n // V) * (stride + 4 * V + 5) + npk
+
+
+def gather(mode):
+    return lambda: lab.lab_gather(keys32.data_ptr(), ids32.data_ptr(), work.data_ptr(), npk, stride,
+                                  regs.data_ptr(), 16, mode, st)
+
+
+def switch():
+    sw.count.zero_()
+    sw.frag.zero_()
+    sw.process(work, acts, desc=desc)
+    return 0
+
+
+cases = {"gather reads only": gather(0), "gather + register rows": gather(1),
+         "gather + registers + forwarded packets": gather(2), "ina_switch_process (incl. sort)": switch}
+times = {k: [] for k in cases}
+for _ in range(int(os.environ.get("ROUNDS", 6))):
+    for k, fn in cases.items():
+        for _ in range(3):
+            work.copy_(clean)
+            if k.startswith("ina_"):
+                sw.count.zero_()
+                sw.frag.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            if k.startswith("ina_"):
+                sw.process(work, acts, desc=desc)
+            else:
+                assert fn() == 0
+            e1.record()
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1) * 1e3)
+print(json.dumps({k: {"median_us": round(statistics.median(v), 1),
+                      "frac_of_switch_algorithmic": round(algo / (statistics.median(v) * 1e-6) / 8e12, 4)}
+                  for k, v in times.items()}, indent=1))
