@@ -206,11 +206,11 @@ def run_extra(dev):
     # slot starts with count_reg == 1), one action byte per packet
     npk_all = stream.shape[0]
     sw_bytes = stream.numel() + stream.numel() // Ws + npk * (V * 4 + 5) + npk_all
-    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from descriptors)",
+    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; keys from descriptors)",
                      _time(lambda: sw.process(stream, acts, desc=desc_all), reps=5, warm=1), sw_bytes,
                      note="the pack kernels' 8-byte packet descriptors feed the slot sort "
                           "(ina_switch_process_desc)"))
-    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from headers)",
+    rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; keys from headers)",
                      _time(lambda: sw.process(stream, acts), reps=5, warm=1), sw_bytes,
                      note="ina_switch_process: the key pass reads each packet's header line"))
     # PS side, fused, on the switch's output: completed slots -> dequantise -> update + acks

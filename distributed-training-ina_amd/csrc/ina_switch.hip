@@ -919,6 +919,13 @@ static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWI
 #ifndef INA_SWITCH_TAIL_NT
 #define INA_SWITCH_TAIL_NT 0
 #endif
+// the batch's action bytes leave in one store (lane b: packet b) instead of one per packet:
+// 241.7 -> 234.9 us for the switch alone, but with the PS step fused the extra registers
+// cost an occupancy step (72 -> 78 VGPRs: 264.6 -> 289.1 us), so only without it
+// (profiles/r02/lab/switch_lab_actbatch.log)
+#ifndef INA_SWITCH_ACT_BATCH
+#define INA_SWITCH_ACT_BATCH 1
+#endif
 __device__ __forceinline__ u32x4s sw_ld(const u32x4s* p) {
 #if INA_SWITCH_NT
     return __builtin_nontemporal_load(p);
@@ -958,6 +965,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
+    constexpr bool kActBatch = INA_SWITCH_ACT_BATCH && !kPs;
     const int lane = threadIdx.x & 63;
     const int V = st.V;
     const int L = V >> 2;                       // lanes holding values
@@ -1044,10 +1052,11 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
 #pragma unroll
             for (int b = 1; b < kB; ++b) pid[b] = b < nb ? pid[b] : pid[0];
             u32x4s tl = {0u, 0u, 0u, 0u};
-            if (wide) {
-                uint32_t mypid = pid[0];
+            uint32_t mypid = pid[0];                 // lane b: packet b's id
 #pragma unroll
-                for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
+            for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
+            uint32_t act_v = 0;                      // lane b: packet b's action (kActBatch)
+            if (wide) {
 #if INA_SWITCH_TAIL_NT
                 tl = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
 #else
@@ -1171,8 +1180,11 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                         }
                     }
                 }
-                if (lane == 0) actions[pid[b]] = act;
+                if constexpr (kActBatch) act_v = lane == b ? (uint32_t)act : act_v;
+                else if (lane == 0) actions[pid[b]] = act;
             }
+            if constexpr (kActBatch)
+                if (lane < nb) actions[mypid] = (uint8_t)act_v;   // one store for the batch
         }
         if (lane == 0) {
             st.count[slot] = (uint8_t)cnt;

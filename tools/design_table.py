@@ -48,7 +48,7 @@ def fmt(r):
 
 def row_cells(tag):
     bench, ex, sw, tr, prof_us = load()
-    e = lambda k: ex[k]                                              # noqa: E731
+    e = lambda k: ex[k] if k in ex else ex[k.replace("slot sort", "radix sort")]   # noqa: E731 (r01 names)
     rf = bench["roofline"]
     d = driver_bench()
     drv = (f"the driver's {d[0]}: {d[1]:.2f} µs = {100 * d[2]:.1f} %" if d else "no driver bench yet")
@@ -83,9 +83,9 @@ def row_cells(tag):
         "`k_absmax_f32`": fmt(e("absmax_f32 ResNet-50 delta (dynamic scale)")),
         "`k_pack_c128`": fmt(e("pack_c128 ResNet-50")),
         "`ina_switch_process` (819,200":
-            fmt(e("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from descriptors)"))
+            fmt(e("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; keys from descriptors)"))
             + " with keys from the pack kernels' descriptors ("
-            + fmt(e("switch_process 8x NGA-256 (819,200 pkts, incl. radix sort; keys from headers)"))
+            + fmt(e("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; keys from headers)"))
             + " from the headers)"
             + f" event-timed; under rocprof ({tag}, `profiles/{RD}/traffic_switch.json`) `k_switch_run2` "
               f"{sw[run2]['avg_us']:.1f} µs moving "

@@ -53,15 +53,8 @@ def gather(mode):
                                   regs.data_ptr(), 16, mode, st)
 
 
-def switch():
-    sw.count.zero_()
-    sw.frag.zero_()
-    sw.process(work, acts, desc=desc)
-    return 0
-
-
 cases = {"gather reads only": gather(0), "gather + register rows": gather(1),
-         "gather + registers + forwarded packets": gather(2), "ina_switch_process (incl. sort)": switch}
+         "gather + registers + forwarded packets": gather(2), "ina_switch_process (incl. sort)": None}
 times = {k: [] for k in cases}
 for _ in range(int(os.environ.get("ROUNDS", 6))):
     for k, fn in cases.items():

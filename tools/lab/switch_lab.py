@@ -26,6 +26,12 @@ del bufs
 npk, stride = src.shape
 
 
+SHARED = dict(count=torch.zeros(slots, dtype=torch.uint8, device=dev),
+              frag=torch.zeros(slots, dtype=torch.int32, device=dev),
+              regs=torch.zeros((slots, V), dtype=torch.int32, device=dev),
+              acts=torch.empty(npk, dtype=torch.uint8, device=dev))
+
+
 class Variant:
     def __init__(self, path):
         self.name = os.path.basename(path)
@@ -36,14 +42,12 @@ class Variant:
         m = re.search(r"_w(\d+)\.so$", path)       # libina_w<N>.so: run-kernel window N (key 10)
         if m:
             assert self.lib.ina_set_tuning(10, int(m.group(1))) == 0
-        self.count = torch.zeros(slots, dtype=torch.uint8, device=dev)
-        self.frag = torch.zeros(slots, dtype=torch.int32, device=dev)
-        self.regs = torch.zeros((slots, V), dtype=torch.int32, device=dev)
+        # every variant runs on the SAME state, scratch and action buffers (only the library
+        # differs): buffer placement alone moved a variant by several % (fuse_lab_position.log)
+        self.count, self.frag, self.regs, self.acts = SHARED["count"], SHARED["frag"], SHARED["regs"], SHARED["acts"]
         self.st = _lib.SwitchState(slots, V, 1, 0, self.count.data_ptr(), self.frag.data_ptr(),
                                    self.regs.data_ptr())
-        self.scratch = torch.empty(self.lib.ina_switch_scratch_bytes(npk, slots), dtype=torch.uint8,
-                                   device=dev)
-        self.acts = torch.empty(npk, dtype=torch.uint8, device=dev)
+        self.scratch_bytes = self.lib.ina_switch_scratch_bytes(npk, slots)
         self.times = []
 
     def run(self, pk):
@@ -60,6 +64,9 @@ class Variant:
 
 
 vs = [Variant(p) for p in sys.argv[1:]]
+scratch = torch.empty(max(v.scratch_bytes for v in vs), dtype=torch.uint8, device=dev)
+for v in vs:
+    v.scratch = scratch
 work = src.clone()
 ref = None
 for v in vs:                                   # correctness: identical outputs
