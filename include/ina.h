@@ -69,8 +69,9 @@ const char* ina_last_error_string(void);
  * 8 16-byte chunks per flat packet-kernel launch, 9 switch one-workgroup small-batch
  * path (0/1), 10 switch run-kernel window in sorted positions (0 = auto, 1..64),
  * 11 switch lane-parallel path for PS acks alone in their slot's segment (0/1), 12 switch
- * slot sort (0 histogram / column-scan / scatter passes, 1 one-sweep passes with decoupled
- * look-back), 13 slot-sort tile rounds per wave, both sorts (0 auto, 4, 8, 16), 14 grid cap
+ * slot sort (0 auto = bucket + local for two-digit keys, 1 one-sweep passes with decoupled
+ * look-back, 2 bucket + local, 3 histogram / column-scan / scatter digit passes),
+ * 13 slot-sort tile rounds per wave (0 auto, 4, 8, 16), 14 grid cap
  * of the one-in one-out elementwise kernels (quantise, dequantise, PS apply, int16 wire).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
