@@ -1326,6 +1326,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     const SortPlan sp = sort_plan(npk, st->num_slots);
     // sort chunk geometry (sort_plan): one instantiation per rounds-per-wave choice
     constexpr int kR0 = INA_RS_ROUNDS_SMALL, kR1 = INA_RS_ROUNDS_MID, kR2 = kRsRounds;
+    static_assert(kR0 % 4 == 0 && kR1 % 4 == 0 && kR2 % 4 == 0, "bucket pass: 16 waves x rounds/4");
     const int ri = sp.rounds == kR0 ? 0 : sp.rounds == kR1 ? 1 : 2;
     auto* k_keys = desc ? (ri == 0 ? &k_switch_keys<kR0, true> : ri == 1 ? &k_switch_keys<kR1, true>
                                                                 : &k_switch_keys<kR2, true>)
