@@ -778,6 +778,37 @@ def test_switch_config3_full_size_equals_bulk_reduce(V, n, pool):
     assert torch.equal(vals.view(npk, V)[order].reshape(-1), want)
 
 
+def test_switch_config3_full_size_shuffled_arrival():
+    """Config 3 at full size in a random arrival order (as a NIC interleaves W workers):
+    every slot completes, the completed sums equal the bulk W-way reduce bit for bit, and
+    the packet that completes each slot is that slot's LAST arrival -- the slot sort
+    (bucket + local) kept arrival order inside every slot across 819,200 packets."""
+    o = ops()
+    W, V, n, pool = 8, 256, 26_214_400, 1 << 17
+    g = torch.Generator(device=DEV).manual_seed(37)
+    bufs = [torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
+            for _ in range(W)]
+    want = o.sum_reduce(bufs)
+    packed = [o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=pool, desc=True) for w, b in enumerate(bufs)]
+    del bufs
+    npk = n // V
+    perm = torch.randperm(W * npk, device=DEV, generator=g)
+    stream = torch.cat([p for p, _ in packed])[perm]
+    desc = torch.cat([d for _, d in packed])[perm]
+    del packed
+    sw = o.Switch(V, num_slots=pool, switch_id=1, device=DEV)
+    act = sw.process(stream, desc=desc)
+    done = torch.nonzero(act == orc.ACT_FWD_AGG).flatten()
+    assert done.numel() == npk
+    slot_of = perm % npk                                  # original packet i: slot i mod npk
+    last = torch.full((npk,), -1, dtype=torch.int64, device=DEV)
+    last.scatter_reduce_(0, slot_of, torch.arange(W * npk, device=DEV), reduce="amax")
+    assert torch.equal(torch.sort(done).values, torch.sort(last).values)
+    f, vals = o.unpack_nga(stream[done], V)
+    order = torch.argsort(f["frag_id"].to(torch.int64))
+    assert torch.equal(vals.view(npk, V)[order].reshape(-1), want)
+
+
 @pytest.mark.parametrize("keep", [True, False])
 @pytest.mark.parametrize("V,W,per,tail", [(32, 4, 60, 11), (256, 8, 700, 0), (32, 3, 3000, 5),
                                           (64, 16, 200, 37)])
