@@ -213,6 +213,18 @@ def run_extra(dev):
     rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; keys from headers)",
                      _time(lambda: sw.process(stream, acts), reps=5, warm=1), sw_bytes,
                      note="ina_switch_process: the key pass reads each packet's header line"))
+    # the same packets in other arrival orders (the sort is order-independent; the run
+    # kernel's gather follows the packets' places in the batch): round-robin over the
+    # workers as a NIC interleaves them (a slot's W packets adjacent), and a random order
+    for name, perm in (("round-robin over workers",
+                        torch.arange(npk_all, device=dev).view(Ws, npk).t().reshape(-1)),
+                       ("random", torch.randperm(npk_all, device=dev,
+                                                 generator=torch.Generator(device=dev).manual_seed(9)))):
+        st_p, ds_p = stream[perm], desc_all[perm]
+        rows.append(_row(f"switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; {name} arrival)",
+                         _time(lambda: sw.process(st_p, acts, desc=ds_p), reps=5, warm=1), sw_bytes,
+                         note="keys from descriptors; same packets, arrival order permuted"))
+        del st_p, ds_p
     # PS side, fused, on the switch's output: completed slots -> dequantise -> update + acks
     sw.process(stream, acts)
     local3 = rnd_f32(n3)

@@ -92,6 +92,13 @@ def row_cells(tag):
               f"{(sw[run2]['hbm_read_bytes'] + sw[run2]['hbm_write_bytes']) / 1e9:.2f} GB at "
               f"{sw[run2]['TB_per_s']:.1f} TB/s, keys {sw[kk]['avg_us']:.1f} µs "
               f"({sw[kk]['hbm_read_bytes'] / 1e6:.1f} MB read), sort passes {sort_us:.1f} µs",
+        "`ina_switch_process`, other arrival orders":
+            (lambda a, b: f"round-robin over the workers (a NIC's interleave: a slot's packets adjacent) "
+                          f"{fmt(a)}; random {fmt(b)}")(
+                e("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; round-robin over workers arrival)"),
+                e("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; random arrival)"))
+            if "switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; random arrival)" in ex
+            else "(not in this session's bench_extra)",
         "`ina_switch_process`, small batches":
             ", ".join(f"{k.split(': ')[1].split(' NGA')[0]} packets {r['us']:.1f} µs"
                       for k, r in ((r['kernel'], r) for r in small))
