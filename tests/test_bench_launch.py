@@ -20,7 +20,7 @@ def _bench(*args, env=None, timeout=240):
                           capture_output=True, text=True, timeout=timeout, env=e)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])         # 8: the driver's largest scaling run
 def test_bench_gpus_n_spawns_n_ranks(n):
     r = _bench("--gpus", str(n), "--check-launch")
     assert r.returncode == 0, r.stderr[-2000:]
