@@ -39,6 +39,8 @@ for f in sorted(f for f in os.listdir(REPO) if re.fullmatch(r"BENCH_r\d+\.json",
         pass
 opt = [(n, w) for n, w in (
     ("rehearse_2ranks_gloo.json", "bench.py --gpus 2 with no launcher: it starts two ranks itself (torch.distributed.run), both on the box's one GPU over gloo -- the multi-rank timing, max-over-ranks and the config-5 sharded path with device quantise/decode (collectives staged through host memory)"),
+    ("rehearse_8ranks_gloo.json", "bench.py --gpus 8 starting its own 8 ranks, all on the box's one GPU over gloo: the N = 8 flow end to end (group-size assert, max-over-ranks timing, the 8-way config-5 shard plan, parity spot checks); throughput numbers are meaningless with 8 ranks on one GPU"),
+    ("bench_boxes.json", "the headline line on every box of this round's evidence sessions, next to the driver's round-1 line"),
     ("sharded_c5_1gpu_i32.json", "bench.py --mode sharded --wire i32: config 5 (1 GiB fp32 per rank) as the headline on one GPU; the collectives are identities at N = 1"),
     ("sharded_c5_1gpu_i16.json", "the same on the int16 saturating wire (q16 + saturation count in one int32 SUM, saturate once)"),
     ("config1_loopback.log", "examples/config1_loopback.py: config 1 (ResNet-50 parameter count, 2 workers, loopback sockets, device switch stand-in)"),
@@ -63,7 +65,7 @@ of the headline bench on fresh boxes: {"; ".join(drivers) if drivers else "none 
 | `{RD}/kernel_stats_switch.csv` | rocprofv3 stats of `tools/prof_switch.py` (device switch on 819,200 NGA-256 packets, keys from the pack kernels' descriptors): `k_switch_run2` {sw[run2]['avg_us']} us, keys {sw[keys]['avg_us']} us, sort {sort_us:.1f} us |
 | `{RD}/switch_pmc_FETCH_SIZE.csv`, `{RD}/switch_pmc_WRITE_SIZE.csv`, `{RD}/traffic_switch.json` | PMC passes over the same program; per-kernel HBM bytes and rates computed by `tools/switch_traffic.py` (run kernel {(sw[run2]['hbm_read_bytes'] + sw[run2]['hbm_write_bytes']) / 1e9:.2f} GB at {sw[run2]['TB_per_s']} TB/s) |
 {rows}
-| `{RD}/lab/*` | interleaved A/B labs of this round (`tools/lab/`): slot sort variants (r01 passes, one-sweep, bucket + local), run-kernel window/batch, elementwise and packet-kernel grid caps, absmax |
+| `{RD}/lab/*` | interleaved A/B labs of this round (`tools/lab/`): slot sort variants (r01 passes, one-sweep, bucket + local), bucket workgroup waves, foreign-bucket skip, batched action stores, run-kernel window/batch/occupancy/prefetch/register-store policy, the run kernel's gather floor (`gather_lab.json`), switch arrival orders, elementwise and packet-kernel grid caps, absmax, lab buffer-placement check |
 | `r01/` | round 1: the same files for round 1's code, its labs (`r01/lab/`), the per-box bench spread (`r01/bench_boxes.json`) |
 """
 open(os.path.join(P, "README.md"), "w").write(txt)
