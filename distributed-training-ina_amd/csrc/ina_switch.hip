@@ -900,6 +900,10 @@ constexpr int kB = INA_SWITCH_BATCH;         // packets of a segment loaded at o
 #endif
 static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWITCH_WIN_LARGE >= 1 &&
               INA_SWITCH_WIN_LARGE <= 64, "a window is at most one wave of keys");
+// occupancy target of k_switch_run2 without the PS step (72 VGPRs -> 7 waves per SIMD)
+#ifndef INA_SWITCH_WAVES_RUN
+#define INA_SWITCH_WAVES_RUN 7
+#endif
 // occupancy target of k_switch_run2 (waves per SIMD); 4 fits its registers, 5 spills 4
 #ifndef INA_SWITCH_WAVES
 #define INA_SWITCH_WAVES 4
@@ -934,9 +938,26 @@ __device__ __forceinline__ u32x4s sw_ld(const u32x4s* p) {
 #endif
 }
 
+// byte shuffles of the NGA payload (values at byte 15 + 4j, big-endian) as one v_perm_b32
+// each (selector byte k: 0-3 = second operand's bytes, 4-7 = first operand's):
+//   dec_be(hi, lo) = the BE word at bytes {lo.b3, hi.b0, hi.b1, hi.b2}
+//   enc_lo(prev, v) = LE dword of BE bytes 1..3 of prev followed by BE byte 0 of v
+#ifndef INA_SWITCH_PERM
+#define INA_SWITCH_PERM 1
+#endif
+__device__ __forceinline__ uint32_t dec_be(uint32_t hi, uint32_t lo) {
+#if INA_SWITCH_PERM
+    return __builtin_amdgcn_perm(hi, lo, 0x03040506u);
+#else
+    return __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, 3));
+#endif
+}
 __device__ __forceinline__ uint32_t enc_lo(uint32_t prev, uint32_t v) {
-    // LE dword: BE bytes 1..3 of prev followed by BE byte 0 of v
+#if INA_SWITCH_PERM
+    return __builtin_amdgcn_perm(v, prev, 0x07000102u);
+#else
     return (__builtin_bswap32(prev) >> 8) | (v & 0xFF000000u);
+#endif
 }
 
 // PS co-located with the switch (ina_switch_process_apply): a completed slot's sum goes
@@ -954,7 +975,7 @@ struct PsFuse {
 };
 
 template <bool kPs>   // kPs: PS update fused (ina_switch_process_apply); false costs nothing
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SWITCH_WAVES, 8))) void k_switch_run2(ina_switch_state_t st,
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? INA_SWITCH_WAVES : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts, size_t npk,
                                                           size_t stride,
                                                           const uint32_t* __restrict__ keys,
@@ -1106,10 +1127,10 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                             if (lane == 63) c = u32x4s{tx, ty, tz, tw};
                         }
                         u32x4s v;                            // values 4l..4l+3
-                        v.x = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.x, a[b].w, 3));
-                        v.y = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.y, c.x, 3));
-                        v.z = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.z, c.y, 3));
-                        v.w = __builtin_bswap32(__builtin_amdgcn_alignbyte(c.w, c.z, 3));
+                        v.x = dec_be(c.x, a[b].w);
+                        v.y = dec_be(c.y, c.x);
+                        v.z = dec_be(c.z, c.y);
+                        v.w = dec_be(c.w, c.z);
                         if (first) {                         // processor.p4:16-21
                             reg = v;
                         } else if (have_reg) {
@@ -1164,8 +1185,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                                 e.x = enc_lo(p.x, p.y);
                                 e.y = enc_lo(p.y, p.z);
                                 e.z = enc_lo(p.z, p.w);
-                                e.w = lane < L ? enc_lo(p.w, reg.x)
-                                               : ((__builtin_bswap32(p.w) >> 8) | (e.w & 0xFF000000u));
+                                e.w = enc_lo(p.w, lane < L ? reg.x : e.w);
                             }
                             if (lane <= L)
                                 reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride)[lane] = e;
@@ -1174,7 +1194,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(INA_SW
                                 o.x = enc_lo(reg.x, reg.y);
                                 o.y = enc_lo(reg.y, reg.z);
                                 o.z = enc_lo(reg.z, reg.w);
-                                o.w = (__builtin_bswap32(reg.w) >> 8) | (tw & 0xFF000000u);
+                                o.w = enc_lo(reg.w, tw);
                                 reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride)[64] = o;
                             }
                         }
