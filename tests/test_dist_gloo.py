@@ -46,7 +46,7 @@ def _worker(rank, world, port, n, k, results):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 100_003), (3, 5000), (2, 1)])
+@pytest.mark.parametrize("world,n", [(2, 100_003), (3, 5000), (2, 1), (8, 50_001)])
 def test_sharded_integer_aggregate_gloo(world, n):
     k = 20
     mgr = mp.Manager()
@@ -113,7 +113,7 @@ def _i16_bucket(rank, n):
     return x
 
 
-@pytest.mark.parametrize("world,n,V", [(2, 100_003, 256), (3, 5000, 32), (2, 1, 256), (4, 9000, 100)])
+@pytest.mark.parametrize("world,n,V", [(2, 100_003, 256), (3, 5000, 32), (2, 1, 256), (4, 9000, 100), (8, 60_000, 32)])
 def test_sharded_i16_wire_gloo(world, n, V):
     k = 11
     mgr = mp.Manager()
