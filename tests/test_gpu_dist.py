@@ -1,5 +1,5 @@
 """Sharded aggregation (SURVEY.md 8e, config 5 layout A) at world size > 1 with the
-device kernels: two ranks launched by torch.distributed.run, both on cuda:0 with a gloo
+device kernels: 2, 3 and 8 ranks launched by torch.distributed.run, all on cuda:0 with a gloo
 group (the collectives stage through host memory; one GPU cannot hold two RCCL ranks),
 quantise / wire decode / dequantise through libina.so.  Every rank's full aggregate is
 compared bit for bit with the oracle's single-bucket path over all ranks' buckets:
@@ -36,7 +36,7 @@ def _run_ranks(tmp_path, world, n, wire, k, V=256):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n", [(2, 1_000_003), (3, 70_001), (2, 1)])
+@pytest.mark.parametrize("world,n", [(2, 1_000_003), (3, 70_001), (2, 1), (8, 400_001)])
 def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n):
     from oracle import oracle as orc
     k = 20
@@ -52,7 +52,7 @@ def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n,V", [(2, 1_000_003, 256), (3, 50_000, 32), (2, 300, 100)])
+@pytest.mark.parametrize("world,n,V", [(2, 1_000_003, 256), (3, 50_000, 32), (2, 300, 100), (8, 200_000, 32)])
 def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V):
     from oracle import oracle as orc
     k = 11
