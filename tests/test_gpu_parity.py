@@ -644,6 +644,38 @@ def test_switch_skewed_buckets_vs_oracle(sort, case):
         o.set_tuning(switch_sort=0)
 
 
+@pytest.mark.parametrize("num_slots", [513, 1023, 1024, 4097, 65536, (1 << 18) - 1])
+def test_switch_bucket_sort_pool_edges(num_slots):
+    """Pool sizes at the bucket sort's digit-split edges (2^9+1 .. 2^18-1 slots: high / low
+    digits of 5..9 bits, pools that are and are not a multiple of the bucket width, i.e.
+    with and without the unsorted foreign-only bucket), 30 % foreign packets and PS acks:
+    bucket + local and the r01 digit passes both bit-exact against the P4 restatement."""
+    o = ops()
+    V, W = 32, 8
+    res = {}
+    for sort in (2, 3):
+        rng = np.random.default_rng(num_slots)
+        o.set_tuning(switch_sort=sort)
+        try:
+            sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV)
+            sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+            for rnd in range(2):
+                stream = make_stream(rng, V, 600, W, num_slots, collide=0.05, ack=0.1, other=0.3)
+                assert stream.shape[0] > 2048
+                want_pk, want_act = sw_orc.run(stream, stride=o.nga_stride(V))
+                d = dev(stream)
+                act = sw_dev.process(d, desc=o.nga_descriptors(d))
+                assert np.array_equal(host(act), want_act), (sort, rnd)
+                fwd = want_act != orc.ACT_DROP
+                assert np.array_equal(host(d)[fwd], want_pk[fwd]), (sort, rnd)
+            cnt, frag, regs = sw_orc.registers()
+            assert np.array_equal(host(sw_dev.count), cnt)
+            assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+            assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+        finally:
+            o.set_tuning(switch_sort=0)
+
+
 @pytest.mark.parametrize("V,stride_kind", [(32, "padded"), (256, "padded"), (33, "tight"),
                                            (64, "tight"), (4, "padded")])
 def test_pack_descriptors_are_header_bytes(V, stride_kind):
