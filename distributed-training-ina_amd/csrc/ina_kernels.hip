@@ -1418,6 +1418,7 @@ int ina_set_tuning(int key, int value) {
         case 11: return set_ack_fast(value);
         case 12: return set_sort_mode(value);
         case 13: return set_os_rounds(value);
+        case 15: return set_tiny_max(value);
         default: return INA_EINVAL;
     }
 }

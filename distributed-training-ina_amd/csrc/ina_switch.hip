@@ -261,6 +261,9 @@ constexpr int kSmallBatch = 4096;                 // LDS capacity of the one-wor
 static_assert(INA_SWITCH_SMALL_MAX <= kSmallBatch, "small path limited by its LDS");
 constexpr int kSmallBlock = 1024;
 static std::atomic<int> g_small_sort{1};   // ina_set_tuning key 9 (0: always the radix path)
+#ifndef INA_SWITCH_TINY_MAX
+#define INA_SWITCH_TINY_MAX 128                // one-launch path (k_switch_tiny) up to this many packets (tiny_lab: break-even ~150)
+#endif
 static std::atomic<int> g_switch_win{0};   // ina_set_tuning key 10: run-kernel window (0: auto)
 static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack lane path (0: off)
 // ina_set_tuning key 12, the slot sort: 0 auto (bucket + local for two-digit keys, else the
@@ -288,6 +291,12 @@ int set_switch_win(int v) {
     g_switch_win = v;
     return INA_OK;
 }
+static std::atomic<int> g_tiny_max{INA_SWITCH_TINY_MAX};   // ina_set_tuning key 15 (0: off)
+int set_tiny_max(int v) {
+    if (v < 0 || v > INA_SWITCH_SMALL_MAX) return INA_EINVAL;
+    g_tiny_max = v;
+    return INA_OK;
+}
 int set_small_sort(int v) {
     g_small_sort = v ? 1 : 0;
     return INA_OK;
@@ -298,7 +307,7 @@ int set_small_sort(int v) {
 // groups, so they need only a wave barrier; the 21 stages with j >= 64 (M = 4096) need
 // the workgroup's.
 template <typename T, int kIdBits>
-__global__ __launch_bounds__(kSmallBlock) void k_switch_sort_small(
+__device__ __forceinline__ void switch_sort_small_body(
         const uint8_t* __restrict__ pkts, uint32_t npk, size_t stride, uint32_t num_slots,
         int switch_id, uint8_t* __restrict__ actions, uint32_t* __restrict__ keys,
         uint32_t* __restrict__ ids) {
@@ -354,6 +363,14 @@ __global__ __launch_bounds__(kSmallBlock) void k_switch_sort_small(
         keys[p] = (uint32_t)(v[p] >> kIdBits);
         ids[p] = (uint32_t)(v[p] & (((T)1 << kIdBits) - 1));
     }
+}
+
+template <typename T, int kIdBits>
+__global__ __launch_bounds__(kSmallBlock) void k_switch_sort_small(
+        const uint8_t* __restrict__ pkts, uint32_t npk, size_t stride, uint32_t num_slots,
+        int switch_id, uint8_t* __restrict__ actions, uint32_t* __restrict__ keys,
+        uint32_t* __restrict__ ids) {
+    switch_sort_small_body<T, kIdBits>(pkts, npk, stride, num_slots, switch_id, actions, keys, ids);
 }
 
 // later passes: chunk histogram of digit (key >> shift)
@@ -974,26 +991,27 @@ struct PsFuse {
     int on, keep_fwd;   // keep_fwd = 0: completed packets are consumed, not written back
 };
 
-template <bool kPs>   // kPs: PS update fused (ina_switch_process_apply); false costs nothing
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? INA_SWITCH_WAVES : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
-                                                          uint8_t* __restrict__ pkts, size_t npk,
-                                                          size_t stride,
-                                                          const uint32_t* __restrict__ keys,
-                                                          const uint32_t* __restrict__ ids,
-                                                          uint8_t* __restrict__ actions,
-                                                          uint32_t win, uint32_t kmask, PsFuse ps,
-                                                          const uint32_t* __restrict__ nforeign) {
-    // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
-    // the run kernel never processes foreign packets, so it stops before them
-    if (nforeign) npk -= *nforeign;
+// the run kernel's work for waves wave, wave + nwaves, ... (k_switch_run2: every wave of
+// the grid; k_switch_tiny: the 16 waves of its one workgroup)
+// kPs: PS update fused (ina_switch_process_apply); false costs nothing.  kLat (the
+// one-launch tiny path, latency-bound): the slot's count and frag are read into SGPRs
+// only after the first batch's packet loads are issued, so a segment waits for one memory
+// round trip instead of three (no gain where the kernel is bandwidth-bound, and it costs
+// registers there: profiles/r02/lab/switch_lab_state_late.log)
+template <bool kPs, bool kLat = false>
+__device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                                 size_t npk, size_t stride,
+                                                 const uint32_t* __restrict__ keys,
+                                                 const uint32_t* __restrict__ ids,
+                                                 uint8_t* __restrict__ actions, uint32_t win,
+                                                 uint32_t kmask, const PsFuse& ps, size_t wave,
+                                                 size_t nwaves) {
     constexpr bool kActBatch = INA_SWITCH_ACT_BATCH && !kPs;
     const int lane = threadIdx.x & 63;
     const int V = st.V;
     const int L = V >> 2;                       // lanes holding values
     const bool vl = lane < L;
     const bool wide = L == 64;                  // tail chunk lives in lane 63's t[]
-    const size_t wave = (size_t)blockIdx.x * (kSwBlock / 64) + wave_in_block();
-    const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
     const uint32_t NS = st.num_slots;
     // each wave takes windows of 64 sorted positions and processes the segments that
     // START in its window (a segment may run past the window's end)
@@ -1043,8 +1061,15 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
         // registers are loaded only if a packet adds to them before any overwrite
         // (count_reg == 1 overwrites, processor.p4:16-21), i.e. rarely
         const bool ack_led = (am >> hl) & 1ull;
-        uint32_t cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
-        uint32_t frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
+        uint32_t cnt = 0, frag = 0, cnt_ld = 0, frag_ld = 0;
+        bool st_ready = false;
+        if constexpr (kLat) {
+            cnt_ld = st.count[slot];
+            frag_ld = st.frag[slot];
+        } else {
+            cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
+            frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
+        }
         u32x4s reg = {0u, 0u, 0u, 0u};
         bool have_reg = false;
         for (size_t q0 = pos + (ack_led ? 1 : 0); q0 < end; q0 += kB) {
@@ -1088,6 +1113,13 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
             for (int b = 0; b < kB; ++b) {
                 const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[b] * stride);
                 a[b] = sw_ld(pk + (lane <= L ? lane : 0));
+            }
+            if constexpr (kLat) {
+                if (!st_ready) {
+                    cnt = __builtin_amdgcn_readfirstlane(cnt_ld);
+                    frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(frag_ld);
+                    st_ready = true;
+                }
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
@@ -1213,6 +1245,40 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
         if (have_reg && vl) *reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane) = reg;
         }
     }
+}
+
+template <bool kPs>
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? INA_SWITCH_WAVES : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
+                                                          uint8_t* __restrict__ pkts, size_t npk,
+                                                          size_t stride,
+                                                          const uint32_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ ids,
+                                                          uint8_t* __restrict__ actions,
+                                                          uint32_t win, uint32_t kmask, PsFuse ps,
+                                                          const uint32_t* __restrict__ nforeign) {
+    // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
+    // the run kernel never processes foreign packets, so it stops before them
+    if (nforeign) npk -= *nforeign;
+    switch_run2_body<kPs>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps,
+                          (size_t)blockIdx.x * (kSwBlock / 64) + wave_in_block(),
+                          ((size_t)gridDim.x * kSwBlock) >> 6);
+}
+
+// batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
+// one 16-wave workgroup -- the bitonic (slot, packet id) sort in LDS, then the run
+// kernel's work on the same 16 waves with the sorted arrays read from LDS.
+template <bool kPs, typename T, int kIdBits>
+__global__ __launch_bounds__(kSmallBlock) void k_switch_tiny(ina_switch_state_t st, uint8_t* __restrict__ pkts,
+                                                             uint32_t npk, size_t stride,
+                                                             uint8_t* __restrict__ actions, uint32_t win,
+                                                             PsFuse ps) {
+    // the sorted (slot, packet id) arrays stay in LDS: the run loop's window loads are LDS
+    // reads, not a memory round trip
+    __shared__ uint32_t keys_s[INA_SWITCH_SMALL_MAX], ids_s[INA_SWITCH_SMALL_MAX];
+    switch_sort_small_body<T, kIdBits>(pkts, npk, stride, st.num_slots, st.switch_id, actions, keys_s, ids_s);
+    __syncthreads();
+    switch_run2_body<kPs, true>(st, pkts, npk, stride, keys_s, ids_s, actions, win, 0xFFFFFFFFu, ps,
+                                wave_in_block(), kSmallBlock / 64);
 }
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -1411,6 +1477,21 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             std::swap(kc, kn);
             std::swap(vc, vn);
         }
+    } else if (small && fast && npk <= (size_t)g_tiny_max.load()) {
+        // sort and run in ONE launch of one workgroup (k_switch_tiny)
+        uint32_t win = (uint32_t)INA_SWITCH_WIN_SMALL;
+        if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
+        const bool narrow = (uint64_t)st->num_slots + 1 <= (1u << 20);
+        if (ps.on) {
+            if (narrow) hipLaunchKernelGGL((k_switch_tiny<true, uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
+            else hipLaunchKernelGGL((k_switch_tiny<true, unsigned long long, 32>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
+        } else {
+            if (narrow) hipLaunchKernelGGL((k_switch_tiny<false, uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
+            else hipLaunchKernelGGL((k_switch_tiny<false, unsigned long long, 32>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
+        }
+        if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch tiny launch%s", "");
+        *fused_out = ps.on != 0;
+        return INA_OK;
     } else if (small) {
         if ((uint64_t)st->num_slots + 1 <= (1u << 20))
             hipLaunchKernelGGL((k_switch_sort_small<uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, pkts,

@@ -578,7 +578,7 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                launch_chunks: int | None = None, switch_small_sort: bool | None = None,
                switch_window: int | None = None, switch_ack_fast: bool | None = None,
                switch_sort: int | None = None, switch_sort_rounds: int | None = None,
-               ew_blocks: int | None = None):
+               ew_blocks: int | None = None, switch_tiny_max: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -592,7 +592,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     digits, 1 one-sweep passes with decoupled look-back, 2 bucket + local, 3 histogram /
     column-scan / scatter digit passes), switch_sort_rounds the sort tile of either
     sort (64-item rounds per wave: 0 auto, 4, 8, 16), ew_blocks the grid cap of the one-in
-    one-out elementwise kernels (default 2^24: one 16-byte chunk per thread); unroll is the
+    one-out elementwise kernels (default 2^24: one 16-byte chunk per thread),
+    switch_tiny_max the largest batch the switch sorts and runs in ONE launch of one
+    workgroup (0 = off, at most 2048); unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
@@ -619,6 +621,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(13, int(switch_sort_rounds)), "set_tuning")
     if ew_blocks is not None:
         check(lib.ina_set_tuning(14, int(ew_blocks)), "set_tuning")
+    if switch_tiny_max is not None:
+        check(lib.ina_set_tuning(15, int(switch_tiny_max)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

@@ -72,7 +72,8 @@ const char* ina_last_error_string(void);
  * slot sort (0 auto = bucket + local for two-digit keys, 1 one-sweep passes with decoupled
  * look-back, 2 bucket + local, 3 histogram / column-scan / scatter digit passes),
  * 13 slot-sort tile rounds per wave (0 auto, 4, 8, 16), 14 grid cap
- * of the one-in one-out elementwise kernels (quantise, dequantise, PS apply, int16 wire).
+ * of the one-in one-out elementwise kernels (quantise, dequantise, PS apply, int16 wire),
+ * 15 largest switch batch sorted and run in ONE launch of one workgroup (0 = off, <= 2048).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 

@@ -192,6 +192,8 @@ def test_set_tuning_rejects_unknown_keys_and_values():
     assert lib.ina_set_tuning(11, 1) == _lib.INA_OK
     assert lib.ina_set_tuning(12, 4) == _lib.INA_EINVAL        # sort: 0 auto, 1 one-sweep, 2 bucket, 3 passes
     assert lib.ina_set_tuning(12, 3) == _lib.INA_OK
+    assert lib.ina_set_tuning(15, 4096) == _lib.INA_EINVAL      # tiny path: 0..2048 packets
+    assert lib.ina_set_tuning(15, 512) == _lib.INA_OK
     assert lib.ina_set_tuning(13, 5) == _lib.INA_EINVAL        # one-sweep rounds: 0, 4, 8, 16
     assert lib.ina_set_tuning(12, 0) == _lib.INA_OK and lib.ina_set_tuning(13, 0) == _lib.INA_OK
 

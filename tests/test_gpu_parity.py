@@ -737,9 +737,10 @@ def test_switch_lone_acks_vs_oracle(W, ack, ack_fast, write_dropped):
 
 @pytest.mark.parametrize("seed", range(6))
 def test_switch_small_batch_paths_agree(seed):
-    """Batches of <= 4096 packets take the one-workgroup key+bitonic-sort path; the same
-    batches through the chunked radix path give identical actions, packets and registers
-    (and both equal the P4 restatement)."""
+    """Batches of <= 4096 packets through the three paths -- ONE launch of one workgroup
+    (k_switch_tiny: LDS sort then the run kernel's work), the one-workgroup sort + run
+    kernel (two launches), and the multi-launch slot sort -- give identical actions,
+    packets and registers, all equal to the P4 restatement."""
     rng = np.random.default_rng(70_000 + seed)
     o = ops()
     V = int(rng.choice([32, 256, 33]))
@@ -750,18 +751,18 @@ def test_switch_small_batch_paths_agree(seed):
     assert stream.shape[0] <= 4096
     want_pk, want_act = orc.Switch(V, num_slots=num_slots, switch_id=1).run(stream, stride=o.nga_stride(V))
     outs = []
-    for small in (True, False):
+    for small, tiny in ((True, 2048), (True, 0), (False, 0)):
         sw = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
         d = dev(stream)
         try:
-            o.set_tuning(switch_small_sort=small)
+            o.set_tuning(switch_small_sort=small, switch_tiny_max=tiny)
             act = sw.process(d)
         finally:
-            o.set_tuning(switch_small_sort=True)
+            o.set_tuning(switch_small_sort=True, switch_tiny_max=128)
         outs.append((host(act), host(d), host(sw.regs)))
     for act, pk, regs in outs:
         assert np.array_equal(act, want_act) and np.array_equal(pk, want_pk)
-    assert np.array_equal(outs[0][2], outs[1][2])
+    assert np.array_equal(outs[0][2], outs[1][2]) and np.array_equal(outs[0][2], outs[2][2])
 
 
 def test_switch_collision_free_equals_bulk_reduce():
