@@ -102,7 +102,8 @@ def row_cells(tag):
         "`ina_switch_process`, small batches":
             ", ".join(f"{k.split(': ')[1].split(' NGA')[0]} packets {r['us']:.1f} µs"
                       for k, r in ((r['kernel'], r) for r in small))
-            + " (one-workgroup sort below 2,049 packets: 2 launches; radix path above)",
+            + " (up to 128 packets ONE launch -- sort and run in one workgroup, `tools/lab/tiny_lab.py`; up to "
+              "2,048 the one-workgroup sort + run kernel: 2 launches; the bucket sort above)",
         "INA packet path step, steady state, PS fused":
             (lambda r: f"{r['us']:.0f} µs per step = {r['aggregated_GBps']:,.0f} GB/s of worker gradients; "
                        f"{r['GB/s'] / 1e3:.1f} TB/s = {100 * r['frac']:.0f} % of peak for the path's bytes")(
