@@ -260,7 +260,14 @@ constexpr int kSmallBatch = 4096;                 // LDS capacity of the one-wor
 #endif
 static_assert(INA_SWITCH_SMALL_MAX <= kSmallBatch, "small path limited by its LDS");
 constexpr int kSmallBlock = 1024;
-static std::atomic<int> g_small_sort{1};   // ina_set_tuning key 9 (0: always the radix path)
+// ina_set_tuning key 9: the largest batch the one-workgroup sort takes (0: never; 1: the
+// default, INA_SWITCH_SMALL_DEFAULT; 2..INA_SWITCH_SMALL_MAX: that many packets).  Above
+// ~700 packets the bucket sort is faster (tiny_lab: 1,024 packets 26.6 vs 25.2 us, 2,048
+// 37.5 vs 25.3; 512: 23.1 vs 24.0 -- profiles/r02/lab/tiny_lab.log)
+#ifndef INA_SWITCH_SMALL_DEFAULT
+#define INA_SWITCH_SMALL_DEFAULT 768
+#endif
+static std::atomic<int> g_small_sort{INA_SWITCH_SMALL_DEFAULT};
 #ifndef INA_SWITCH_TINY_MAX
 #define INA_SWITCH_TINY_MAX 128                // one-launch path (k_switch_tiny) up to this many packets (tiny_lab: break-even ~150)
 #endif
@@ -298,7 +305,8 @@ int set_tiny_max(int v) {
     return INA_OK;
 }
 int set_small_sort(int v) {
-    g_small_sort = v ? 1 : 0;
+    if (v < 0 || v > INA_SWITCH_SMALL_MAX) return INA_EINVAL;
+    g_small_sort = v == 1 ? INA_SWITCH_SMALL_DEFAULT : v;
     return INA_OK;
 }
 
@@ -1434,7 +1442,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                       st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
     // keys carry the PS-ack bit for the run kernel when bit 31 is outside every digit pass
     const bool ack_hint = fast && sp.passes * sp.bits <= 31 && g_ack_fast.load();
-    const bool small = npk <= (size_t)INA_SWITCH_SMALL_MAX && g_small_sort.load();
+    const bool small = npk <= (size_t)g_small_sort.load();
     const bool onesweep = !small && g_sort_mode.load() == 1 && npk < ((size_t)1 << 30);
     // bucket + local sort: two-digit keys only (the low digit is one workgroup's LDS bins)
     const int mode = g_sort_mode.load();

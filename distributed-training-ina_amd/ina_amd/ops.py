@@ -575,7 +575,7 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                nontemporal: bool | None = None, reduce_blocks: int | None = None,
                stream_blocks: int | None = None, combine_blocks: int | None = None,
                combine_ina_blocks: int | None = None, h2d_streams: int | None = None,
-               launch_chunks: int | None = None, switch_small_sort: bool | None = None,
+               launch_chunks: int | None = None, switch_small_sort: bool | int | None = None,
                switch_window: int | None = None, switch_ack_fast: bool | None = None,
                switch_sort: int | None = None, switch_sort_rounds: int | None = None,
                ew_blocks: int | None = None, switch_tiny_max: int | None = None):
@@ -585,7 +585,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     PS combine, combine_ina_blocks the INA-semantics combine, h2d_streams the host-ingest
     pipeline's H2D copy streams (1 or 2), launch_chunks the 16-byte chunks one flat packet
     kernel launch covers (default 2^31 - 1; smaller values only split launches),
-    switch_small_sort the one-workgroup key+sort path for switch batches <= 4096 packets,
+    switch_small_sort the one-workgroup key+sort path for small switch batches (False: off,
+    True: up to the default 768 packets, an int: up to that many, at most 2048),
     switch_window the sorted positions one wave of the switch run kernel owns (0 = auto,
     1..64), switch_ack_fast the lane-parallel path for PS acks alone in their slot's
     segment, switch_sort the slot sort (0 auto = bucket + local where the keys have two
@@ -610,7 +611,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     if launch_chunks is not None:
         check(lib.ina_set_tuning(8, int(launch_chunks)), "set_tuning")
     if switch_small_sort is not None:
-        check(lib.ina_set_tuning(9, int(bool(switch_small_sort))), "set_tuning")
+        v = int(switch_small_sort) if not isinstance(switch_small_sort, bool) else int(switch_small_sort)
+        check(lib.ina_set_tuning(9, v), "set_tuning")
     if switch_window is not None:
         check(lib.ina_set_tuning(10, int(switch_window)), "set_tuning")
     if switch_ack_fast is not None:

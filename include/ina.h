@@ -66,8 +66,8 @@ const char* ina_last_error_string(void);
  * 0 elementwise grid cap, 1 reduce chunks per worker per thread (0 = per-W auto, 1/2/4), 2 reduce
  * non-temporal loads/stores (0/1), 3 reduce grid (0 = 64*W rule), 4 chunk-loop grid,
  * 5 fp32 PS-combine grid, 6 INA PS-combine grid, 7 host-ingest H2D streams (1/2),
- * 8 16-byte chunks per flat packet-kernel launch, 9 switch one-workgroup small-batch
- * path (0/1), 10 switch run-kernel window in sorted positions (0 = auto, 1..64),
+ * 8 16-byte chunks per flat packet-kernel launch, 9 largest switch batch for the
+ * one-workgroup sort (0 never, 1 default 768, 2..2048), 10 switch run-kernel window in sorted positions (0 = auto, 1..64),
  * 11 switch lane-parallel path for PS acks alone in their slot's segment (0/1), 12 switch
  * slot sort (0 auto = bucket + local for two-digit keys, 1 one-sweep passes with decoupled
  * look-back, 2 bucket + local, 3 histogram / column-scan / scatter digit passes),

@@ -751,7 +751,7 @@ def test_switch_small_batch_paths_agree(seed):
     assert stream.shape[0] <= 4096
     want_pk, want_act = orc.Switch(V, num_slots=num_slots, switch_id=1).run(stream, stride=o.nga_stride(V))
     outs = []
-    for small, tiny in ((True, 2048), (True, 0), (False, 0)):
+    for small, tiny in ((2048, 2048), (2048, 0), (False, 0)):
         sw = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
         d = dev(stream)
         try:

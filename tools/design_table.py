@@ -102,8 +102,8 @@ def row_cells(tag):
         "`ina_switch_process`, small batches":
             ", ".join(f"{k.split(': ')[1].split(' NGA')[0]} packets {r['us']:.1f} µs"
                       for k, r in ((r['kernel'], r) for r in small))
-            + " (up to 128 packets ONE launch -- sort and run in one workgroup, `tools/lab/tiny_lab.py`; up to "
-              "2,048 the one-workgroup sort + run kernel: 2 launches; the bucket sort above)",
+            + " (up to 128 packets ONE launch -- sort and run in one workgroup; up to 768 the one-workgroup "
+              "sort + run kernel: 2 launches; the bucket sort above -- thresholds from `tools/lab/tiny_lab.py`)",
         "INA packet path step, steady state, PS fused":
             (lambda r: f"{r['us']:.0f} µs per step = {r['aggregated_GBps']:,.0f} GB/s of worker gradients; "
                        f"{r['GB/s'] / 1e3:.1f} TB/s = {100 * r['frac']:.0f} % of peak for the path's bytes")(

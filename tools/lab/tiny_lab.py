@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Lab: small switch batches (NGA-32, 16,384-slot pool, 8 workers per slot) through the
-one-launch path (k_switch_tiny: sort + run in one workgroup) against the two-launch
-one-workgroup sort + run kernel, per batch size; interleaved, HIP events, median.
+"""Lab: small switch batches (NGA-32, 16,384-slot pool, 8 workers per slot) per batch size
+through the one-launch path (k_switch_tiny: sort + run in one workgroup), the two-launch
+one-workgroup sort + run kernel, and the multi-launch bucket sort + run kernel;
+interleaved, HIP events, median.
 
   python tools/lab/tiny_lab.py
 """
@@ -19,7 +20,7 @@ from ina_amd import ops  # noqa: E402
 dev = torch.device("cuda")
 V, W, slots = 32, 8, 16384
 g = torch.Generator(device=dev).manual_seed(5)
-sizes = [16, 64, 128, 256, 512, 1024, 2048]
+sizes = [16, 64, 128, 256, 512, 1024, 2048, 4096]
 streams = {}
 for n in sizes:
     per = max(1, n // W)
@@ -28,12 +29,15 @@ for n in sizes:
     streams[n] = torch.cat([ops.pack_nga(v, V, w + 1, W, 1, 1, num_slots=slots) for w, v in enumerate(vals)])
 sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
 acts = torch.empty(max(s.shape[0] for s in streams.values()), dtype=torch.uint8, device=dev)
-times = {(n, t): [] for n in sizes for t in (0, 2048)}
+MODES = {"one launch": dict(switch_small_sort=2048, switch_tiny_max=2048),
+         "two launches": dict(switch_small_sort=2048, switch_tiny_max=0),
+         "bucket sort": dict(switch_small_sort=False, switch_tiny_max=0)}
+times = {(n, t): [] for n in sizes for t in MODES}
 ref = {}
 for _ in range(int(os.environ.get("ROUNDS", 8))):
     for n in sizes:
-        for t in (0, 2048):
-            ops.set_tuning(switch_tiny_max=t)
+        for t, kw in MODES.items():
+            ops.set_tuning(**kw)
             st = streams[n]
             a = acts[: st.shape[0]]
             for _ in range(5):
@@ -45,9 +49,8 @@ for _ in range(int(os.environ.get("ROUNDS", 8))):
                 times[(n, t)].append(e0.elapsed_time(e1) * 1e3)
             if (n, t) not in ref:
                 ref[(n, t)] = a.clone()
-ops.set_tuning(switch_tiny_max=128)
+ops.set_tuning(switch_small_sort=True, switch_tiny_max=128)
 for n in sizes:
-    assert torch.equal(ref[(n, 0)], ref[(n, 2048)]), n
-print(json.dumps({f"{n} packets": {"two launches us": round(statistics.median(times[(n, 0)]), 1),
-                                   "one launch us": round(statistics.median(times[(n, 2048)]), 1)}
+    assert all(torch.equal(ref[(n, "one launch")], ref[(n, t)]) for t in MODES), n
+print(json.dumps({f"{n} packets": {t: round(statistics.median(times[(n, t)]), 1) for t in MODES}
                   for n in sizes}, indent=1))
