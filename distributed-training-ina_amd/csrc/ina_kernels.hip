@@ -1252,6 +1252,41 @@ __global__ __launch_bounds__(kBlock) void k_pack_c128(const uint32_t* __restrict
     }
 }
 
+// 4 consecutive words per thread: one 16-byte store (the buffer is 16-byte aligned), the
+// words' sources found from one 32-bit divide (4-byte gradient loads).  ResNet-50's 199,665
+// packets: 38.7 -> 35.7 us against a word per thread; one word per thread over a covering
+// grid 46.7 us, 8 words per thread 48.8 us (tools/lab/c128_lab.py, profiles/r02/lab/c128_lab.log)
+template <int X>
+__global__ __launch_bounds__(kBlock) void k_pack_c128_x4(const uint32_t* __restrict__ g, uint32_t total,
+                                                         uint32_t bitmap, uint32_t agg, int tensor_index,
+                                                         uint32_t* __restrict__ out) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t t0 = X * c;
+    if (t0 >= total) return;
+    uint32_t p = t0 / 131u, w = t0 - p * 131u;
+    uint32_t r[X];
+#pragma unroll
+    for (int i = 0; i < X; ++i) {
+        uint32_t v = 0;
+        if (t0 + i < total) {
+            if (w == 0) v = bitmap;
+            else if (w == 1) v = agg;
+            else if (w == 2) v = (uint32_t)(tensor_index + (int)p);
+            else v = g[(size_t)p * 128 + (w - 3)];
+        }
+        r[i] = bswap(v);
+        if (++w == 131u) { w = 0; ++p; }
+    }
+    if (t0 + X <= total) {
+#pragma unroll
+        for (int i = 0; i < X; i += 4)
+            *reinterpret_cast<u32x4*>(out + t0 + i) = u32x4{r[i], r[i + 1], r[i + 2], r[i + 3]};
+    } else {
+        for (uint32_t i = 0; t0 + i < total; ++i) out[t0 + i] = r[i];
+    }
+}
+
+
 // ===========================================================================
 // 7. checksum: sum_i x[i]*(2i+1) mod 2^32 -- wave shuffle + LDS block reduce
 // ===========================================================================
@@ -1738,9 +1773,15 @@ int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id, uint3
     // 1 << (worker_id-1): x86 masks the shift count (communicator.cc:18, UB for 0)
     uint32_t bitmap = 1u << ((unsigned)(worker_id - 1) & 31u);
     size_t total = (size_t)packet_num * 131;
-    hipLaunchKernelGGL(k_pack_c128, dim3(grid_for(total, 1)), dim3(kBlock), 0, hs(stream), gradient,
-                       (size_t)packet_num, bitmap, aggregator_index, tensor_index,
-                       reinterpret_cast<uint32_t*>(pkts));
+    if (total < 0xFFFFFF00u && aligned16(pkts)) {
+        hipLaunchKernelGGL(k_pack_c128_x4<4>, dim3((unsigned)((total / 4 + kBlock) / kBlock)), dim3(kBlock), 0,
+                           hs(stream), gradient, (uint32_t)total, bitmap, aggregator_index, tensor_index,
+                           reinterpret_cast<uint32_t*>(pkts));
+    } else {
+        hipLaunchKernelGGL(k_pack_c128, dim3(grid_for(total, 1)), dim3(kBlock), 0, hs(stream), gradient,
+                           (size_t)packet_num, bitmap, aggregator_index, tensor_index,
+                           reinterpret_cast<uint32_t*>(pkts));
+    }
     return check_launch("pack_c128");
 }
 

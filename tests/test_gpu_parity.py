@@ -442,6 +442,21 @@ def test_pack_c128_matches_reference_bytes(case):
     assert got.tobytes() == b"".join(pkts)
 
 
+@pytest.mark.parametrize("packet_num", [1, 2, 3, 7, 1000, 199_665])
+@pytest.mark.parametrize("offset", [0, 4, 12])
+def test_pack_c128_paths_vs_oracle(packet_num, offset):
+    """C-128 packing into 16-byte aligned buffers (4 words per thread, one 16-byte store)
+    and into 4-byte aligned ones (a word per thread) equals the oracle's communicator.cc
+    restatement, ragged word counts (131 * packet_num) and ResNet-50's packet count included."""
+    rng = np.random.default_rng(packet_num + offset)
+    g = rng.integers(0, 1 << 32, packet_num * 128, dtype=np.uint32)
+    want = orc.pack_c128(g, packet_num, 3, 7, 10)
+    buf = torch.zeros(packet_num * 524 + 16, dtype=torch.uint8, device=DEV)
+    out = buf[offset: offset + packet_num * 524].view(packet_num, 524)
+    got = host(ops().pack_c128(dev(g.view(np.int32)), packet_num, 3, 7, 10, out=out))
+    assert np.array_equal(got.reshape(-1), np.asarray(want, np.uint8).reshape(-1))
+
+
 def test_send_gradients_fd_over_socketpair():
     """The host send path (legacy send_gradients body) delivers exactly the reference's
     packet_t datagrams, one per packet, over a datagram socket."""
