@@ -321,6 +321,30 @@ def run_extra(dev):
                      acks_and_slots_ok=ok,
                      note="ina_switch_process_apply(keep_forwarded=0): bytes = the steady-state row's "
                           "minus the PS's re-read of completed packets and their write-back"))
+    # the same step recorded once as a hipGraph and replayed: the step's 15 launches (8
+    # worker packs, the descriptor pass, the switch's 5 sort/run launches, ...) leave the
+    # CPU and the launch queue
+    try:
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            ina_step_fused()
+        torch.cuda.current_stream().wait_stream(cap)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ina_step_fused()
+        t = _time(graph.replay, reps=5, warm=1)
+        graph.replay()
+        torch.cuda.synchronize()
+        ok = bool((acts2[npk:] == 1).sum() == npk) and bool((acts2[:npk] == 3).all())
+        rows.append(_row("INA packet path step, steady state, PS fused, replayed as a hipGraph",
+                         t, fused_bytes, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
+                         acks_and_slots_ok=ok, note="torch.cuda.CUDAGraph capture of the row above"))
+        del graph
+    except Exception as e:                       # reported, not fatal: the eager row stands
+        rows.append({"kernel": "INA packet path step, steady state, PS fused, replayed as a hipGraph",
+                     "error": repr(e)[:300]})
     del xs, glob_p, upd, big, ack_rows, rows_w2, acts2, sw2, sw3, desc_big, desc_ack, desc_w2
 
     # small batches through the switch (P4 format: NGA-32, 16,384-slot pool): latency of
