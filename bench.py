@@ -26,6 +26,9 @@ Multi-GPU:
     dequantise -> all_gather(fp32) (ina_amd.dist.ShardedAggregator), with per-
     phase times, the xGMI bytes per rank and a parity check of the aggregate.
   --mode sharded makes config 5 the headline line instead.
+  * "switch_c3" (N = 1) -- the packet-stream switch (ina_switch_process) on
+    config 3 as 819,200 NGA-256 packets, worker-major and round-robin arrival, with its
+    own roofline fraction on its algorithmic bytes.
 
 Extra rows (not the headline): --extra writes per-kernel timings of the other
 configs (fused quantise+reduce C2, int16 C4, pack/unpack, PS combine, end-to-end
@@ -80,6 +83,8 @@ def parse(argv=None):
     ap.add_argument("--wire", choices=("i32", "i16"), default="i32",
                     help="config-5 wire: int32, or the int16 saturating wire (config 4 rule)")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 sub-measurement")
+    ap.add_argument("--no-switch", action="store_true",
+                    help="skip the packet-stream switch sub-measurement (config 3 as NGA-256 packets)")
     ap.add_argument("--check-launch", action="store_true",
                     help="launcher self-check: start the ranks, form the group, assert its size, "
                          "print one JSON line; no GPU work (runs on CPU with gloo)")
@@ -346,6 +351,60 @@ def measure_c5(args, rank, world, dev, warmup=2):
     }
 
 
+# -- the packet-stream switch on config 3 ----------------------------------------
+def measure_switch(dev, reps=10, warm=2):
+    """ina_switch_process over config 3 as NGA-256 packets: 8 workers x 102,400 packets
+    (2^17-slot pool, keys from the pack kernels' descriptors), in worker-major and in
+    round-robin arrival (a NIC interleaving the workers).  HIP events on the launch stream
+    around each call; the replayed batch completes every slot again, so no state reset
+    sits in the timed region.  Algorithmic bytes: every packet read, the completing 1/W
+    written back, each slot's registers + count + frag written, one action byte per packet."""
+    from ina_amd import ops
+    W, n, V, slots = W_WORKERS, N_VALUES, V_SLOT, 1 << 17
+    g = torch.Generator(device=dev)
+    g.manual_seed(4242)
+    packed = []
+    for w in range(W):
+        b = torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
+        packed.append(ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots, desc=True))
+        del b
+    stream = torch.cat([p for p, _ in packed])
+    desc = torch.cat([d for _, d in packed])
+    del packed
+    npk_all, stride = stream.shape
+    npk = npk_all // W
+    sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
+    acts = torch.empty(npk_all, dtype=torch.uint8, device=dev)
+    algo = npk_all * stride + npk * stride + npk * (4 * V + 5) + npk_all
+    s = torch.cuda.current_stream(dev)
+    res = {"workload": "C3 as NGA-256 packets: 8 workers x 102,400 packets (819,200), 2^17-slot "
+                       "pool, keys from descriptors; ina_switch_process incl. its slot sort",
+           "algorithmic_bytes": algo}
+    order = {"worker_major": None,
+             "round_robin": torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1)}
+    for name, perm in order.items():
+        st, ds = (stream, desc) if perm is None else (stream[perm], desc[perm])
+        for _ in range(warm):
+            sw.process(st, acts, desc=ds)
+        evs = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            sw.process(st, acts, desc=ds)
+            e1.record(s)
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        us = statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3
+        done = int((acts == 1).sum())
+        res[name] = {"us": round(us, 2), "achieved_GBps": round(algo / us / 1e3, 1),
+                     "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
+                     "ok": done == npk}
+        del st, ds
+    del stream, desc, sw, acts
+    torch.cuda.empty_cache()
+    return res
+
+
 # -- modes ---------------------------------------------------------------------------------------
 def run_check_launch(args, rank, world, backend):
     import torch.distributed as dist
@@ -453,6 +512,8 @@ def run_reduce(args, rank, world, dev, backend):
     torch.cuda.empty_cache()
     if not args.no_c5:
         line["sharded_c5"] = measure_c5(args, rank, world, dev)
+    if not args.no_switch and rank == 0 and world == 1:
+        line["switch_c3"] = measure_switch(dev)
     return line
 
 

@@ -1,5 +1,5 @@
 """bench.py's output contract (one JSON line with the driver's keys, roofline,
-cpu_baseline and sharded_c5 objects) on short runs; the bench runs as a child process.
+cpu_baseline, sharded_c5 and switch_c3 objects) on short runs; the bench runs as a child process.
 The two-rank rehearsal puts both ranks on the one GPU of the test box with a gloo group
 (bench.py --gpus 2 launching its own ranks, INA_BENCH_BACKEND=gloo): the launcher, the
 group-size assertion, the per-rank slot ranges and the config-5 path through
@@ -52,6 +52,11 @@ def test_bench_json_line_contract():
     assert "workload" in d["config"]
     c5 = d["sharded_c5"]
     assert c5["parity_spot_check"] is True and c5["rccl_world"] == 1 and c5["values_per_rank"] == 1 << 22
+    sw = d["switch_c3"]                          # the packet-stream switch, measured live
+    assert sw["algorithmic_bytes"] == 819_200 * 1040 + 102_400 * (1040 + 1029) + 819_200
+    for order in ("worker_major", "round_robin"):
+        assert sw[order]["ok"] is True and sw[order]["slots_completed"] == 102_400
+        assert 0 < sw[order]["frac"] < 1
 
 
 @pytest.mark.gpu
