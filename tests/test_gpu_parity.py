@@ -859,7 +859,7 @@ def test_switch_config3_full_size_shuffled_arrival():
 
 @pytest.mark.parametrize("keep", [True, False])
 @pytest.mark.parametrize("V,W,per,tail", [(32, 4, 60, 11), (256, 8, 700, 0), (32, 3, 3000, 5),
-                                          (64, 16, 200, 37)])
+                                          (64, 16, 200, 37), (32, 2, 30, 3), (256, 3, 30, 0)])   # last two: <= 128-packet batches (one launch)
 def test_switch_process_apply_equals_two_steps(V, W, per, tail, keep):
     """ina_switch_process_apply (the PS on the switch's GPU) == ina_switch_process then
     ina_apply_completed_nga: same actions, switch registers, parameter update (bit for bit)
