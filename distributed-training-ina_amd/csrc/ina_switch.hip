@@ -1255,6 +1255,23 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
     }
 }
 
+// XCD-aware window map: blocks b and b + 8 share an XCD (and its L2), so logical block
+// (b % 8) * G/8 + b / 8 gives each XCD one contiguous run of sorted positions -- a slot's
+// neighbours, whose rows share their boundary 128-byte lines, are then gathered through
+// the same L2 (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"; speed only)
+#ifndef INA_SWITCH_XCD
+#define INA_SWITCH_XCD 1
+#endif
+__device__ __forceinline__ size_t switch_block_index() {
+#if INA_SWITCH_XCD
+    const uint32_t G = gridDim.x, b = blockIdx.x, x = b & 7u;
+    const uint32_t per = G >> 3, rem = G & 7u;
+    return (size_t)x * per + (x < rem ? x : rem) + (b >> 3);
+#else
+    return blockIdx.x;
+#endif
+}
+
 template <bool kPs>
 __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? INA_SWITCH_WAVES : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts, size_t npk,
@@ -1268,7 +1285,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
     switch_run2_body<kPs>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps,
-                          (size_t)blockIdx.x * (kSwBlock / 64) + wave_in_block(),
+                          switch_block_index() * (kSwBlock / 64) + wave_in_block(),
                           ((size_t)gridDim.x * kSwBlock) >> 6);
 }
 

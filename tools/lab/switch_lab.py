@@ -23,6 +23,8 @@ bufs = [torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, 
         for _ in range(W)]
 src = torch.cat([ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots) for w, b in enumerate(bufs)])
 del bufs
+if os.environ.get("ORDER", "wm") == "rr":      # a NIC's round-robin interleave of the workers
+    src = src.view(W, -1, src.shape[1]).transpose(0, 1).reshape(-1, src.shape[1]).contiguous()
 npk, stride = src.shape
 
 
