@@ -351,6 +351,75 @@ def measure_c5(args, rank, world, dev, warmup=2):
     }
 
 
+def measure_c5_layout_b(args, rank, world, dev, warmup=2):
+    """Layout B of config 5 (ina_amd.dist.RangeAggregator): the same W = world buckets of
+    n values, but already split by range -- rank r holds every worker's slice of range r
+    (n values in all) -- so the step is a local fused quantise + reduce, a decode, and
+    one all-gather (no reduce-scatter).  Per-phase HIP-event times; parity: the shard's
+    first 64 Ki values against the per-slice device quantise summed on the host."""
+    from ina_amd import ops
+    from ina_amd.dist import RangeAggregator
+    n = args.c5_values
+    k = 16 if args.wire == "i32" else 20
+    agg = RangeAggregator(n, k=k, device=dev, wire=args.wire, V=V_SLOT)
+    lo, hi = agg.range
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000 + rank)
+    slices = [torch.randn(hi - lo, device=dev, generator=g) * 1e-2 for _ in range(world)]
+    for _ in range(warmup):
+        agg(slices)
+    steps = args.c5_steps
+    stream = torch.cuda.current_stream(dev)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        agg(slices)
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    barrier(world)
+    ev[0].record(stream)
+    m = agg._reduce(slices)
+    if m:
+        ops.dequantize(agg.sum_shard[:m], k, out=agg.f_shard[:m])
+    ev[1].record(stream)
+    from ina_amd.dist import all_gather_shards
+    if world > 1:
+        all_gather_shards(agg.f_shard, agg.plan, agg.group, out=agg.full)
+        if args.wire == "i16":
+            all_gather_shards(agg.ovf_shard, agg.plan, agg.group, out=agg.ovf_full)
+    ev[2].record(stream)
+    torch.cuda.synchronize()
+    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(2)]
+    c = min(m, 1 << 16)
+    ok = True
+    if c:
+        agg(slices)
+        got = agg.full[lo:lo + c].clone()
+        heads = [t[:c].contiguous() for t in slices]
+        if args.wire == "i32":
+            wsum = torch.stack([ops.quantize(h, k) for h in heads]).to(torch.int64).sum(0)
+            wsum = ((wsum + (1 << 31)) % (1 << 32) - (1 << 31)).to(torch.int32)
+            want = ops.dequantize(wsum.contiguous(), k)
+        else:
+            wsum = torch.stack([ops.quantize_i16_wire(h, k) for h in heads]).sum(0, dtype=torch.int32)
+            _, want, _ = ops.i16_wire_finish(wsum.contiguous(), k, V_SLOT, want_out16=False)
+        ok = bool(torch.equal(got, want))
+    parity = all_ranks_true(ok, world)
+    ag = (world - 1) * agg.plan.padded * 4 // world
+    return {
+        "value": round(world * n * 4 * steps / elapsed / 1e9, 2), "unit": "GB/s",
+        "ms_per_step": round(elapsed / steps * 1e3, 3),
+        "workload": (f"C5 layout B: {world} workers x {n} values, rank r holds every worker's "
+                     f"slice of range r ({agg.plan.shard} values each): fused quantise + reduce "
+                     f"({args.wire}) -> dequantise -> all_gather(fp32)"),
+        "phase_ms": {"reduce_decode": round(phase[0] * 1e3, 3), "all_gather": round(phase[1] * 1e3, 3)},
+        "xgmi": {"ag_recv_bytes_per_rank": ag,
+                 "ag_busbw_GBps": round(ag / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None},
+        "parity_spot_check": parity,
+    }
+
+
 # -- the packet-stream switch on config 3 (SURVEY 8f-1) ----------------------------------------
 def measure_switch(dev, reps=10, warm=2):
     """ina_switch_process over config 3 as NGA-256 packets: 8 workers x 102,400 packets
@@ -420,6 +489,8 @@ def run_check_launch(args, rank, world, backend):
 
 def run_sharded_headline(args, rank, world, dev, backend):
     c5 = measure_c5(args, rank, world, dev)
+    torch.cuda.empty_cache()
+    c5_b = measure_c5_layout_b(args, rank, world, dev)
     return {
         "metric": c5["metric"], "value": c5["value"], "unit": "GB/s",
         "n_gpus": world, "steps": c5["steps"], "warmup": c5["warmup"],
@@ -431,6 +502,7 @@ def run_sharded_headline(args, rank, world, dev, backend):
         "rccl_world": world, "backend": backend,
         "phase_ms": c5["phase_ms"], "xgmi": c5["xgmi"],
         "parity_spot_check": c5["parity_spot_check"],
+        "layout_b": c5_b,
     }
 
 
@@ -512,6 +584,8 @@ def run_reduce(args, rank, world, dev, backend):
     torch.cuda.empty_cache()
     if not args.no_c5:
         line["sharded_c5"] = measure_c5(args, rank, world, dev)
+        torch.cuda.empty_cache()
+        line["sharded_c5"]["layout_b"] = measure_c5_layout_b(args, rank, world, dev)
     if not args.no_switch and rank == 0 and world == 1:
         line["switch_c3"] = measure_switch(dev)
     return line

@@ -1,6 +1,6 @@
 """Multi-GPU aggregation of one bucket that outgrows a GPU (BASELINE config 5).
 
-Layout A of SURVEY.md 8e: every rank is one worker holding its full fp32
+Layout A of SURVEY.md 8e (ShardedAggregator): every rank is one worker holding its full fp32
 gradient bucket.  Each rank quantises its bucket on its GPU, RCCL reduce-scatters
 the integers with SUM over xGMI, the owner of each shard decodes it, and an
 all-gather returns the full aggregate to every rank (the PS broadcast).  The
@@ -19,6 +19,11 @@ Two wires:
          ngaa_h overflow bit, headers.p4:30) -- bit-identical to the single-GPU
          ina_quantize_reduce_f32_i16_sat over the same W buckets.  The flags are
          all-gathered next to the values.
+
+Layout B (RangeAggregator): the workers' buckets arrive already split by range -- rank
+r holds every worker's slice of slot range r -- so each rank reduces its W slices
+locally with the fused quantise + reduce kernel (no reduce-scatter), decodes, and one
+all-gather returns the full aggregate; the xGMI traffic is that all-gather alone.
 
 Shards are contiguous slot ranges padded to `align` values (default 1024 values =
 4 KiB, rounded up to a whole number of V-value slots), so no slot straddles two
@@ -171,3 +176,86 @@ class ShardedAggregator:
             return s
         out16, _, _ = ops.i16_wire_finish(s, self.k, self.V, overflow=self.ovf_shard, want_y=False)
         return out16
+
+
+class RangeAggregator:
+    """Layout B of SURVEY.md 8e: rank r holds the W workers' fp32 slices of its own range
+    `plan.range_of(r)` (the workers sent slot range r to GPU r: per-slot independence,
+    ngaa.p4:87-168).  __call__ reduces them on this GPU -- the fused quantise + wrapping
+    int32 sum (processor.p4:14-24), or on wire="i16" the int16 saturating sum with its
+    per-slot overflow flags (headers.p4:30) -- dequantises, and all-gathers the fp32
+    aggregate (and the flags) to every rank.  Each rank's shard is bit-identical to the
+    single-GPU ina_quantize_reduce_f32_i32 / _i16_sat over the same W buckets, since the
+    ranges hold whole slots.
+    """
+
+    def __init__(self, n: int, k: int = 16, group=None, device=None, align: int = 1024,
+                 wire: str = "i32", V: int = 256):
+        if wire not in ("i32", "i16"):
+            raise ValueError("wire must be 'i32' or 'i16'")
+        if V <= 0:
+            raise ValueError("V must be > 0")
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if wire == "i16":
+            align = align * V // math.gcd(align, V)        # ranges hold whole slots
+        self.plan = ShardPlan(n, self.world, align)
+        self.k, self.group, self.wire, self.V = k, group, wire, V
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.lo, self.hi = self.plan.range_of(self.rank)
+        sdt = torch.int32 if wire == "i32" else torch.int16
+        self.sum_shard = torch.zeros(self.plan.shard, dtype=sdt, device=dev)
+        self.f_shard = torch.zeros(self.plan.shard, dtype=torch.float32, device=dev)   # pad stays 0
+        # one rank: the gather is an identity, so the decode writes the aggregate in place
+        self.full = self.f_shard if self.world == 1 else torch.empty(self.plan.padded, dtype=torch.float32,
+                                                                     device=dev)
+        if wire == "i16":
+            self.slots_per_shard = self.plan.shard // V
+            self.ovf_shard = torch.zeros(self.slots_per_shard, dtype=torch.uint8, device=dev)
+            self.ovf_full = self.ovf_shard if self.world == 1 else torch.empty(
+                self.slots_per_shard * self.world, dtype=torch.uint8, device=dev)
+
+    @property
+    def range(self):
+        """(lo, hi): the values of the bucket whose worker slices this rank holds."""
+        return self.lo, self.hi
+
+    @property
+    def overflow(self) -> torch.Tensor:
+        """Per-slot overflow flags of the last i16 aggregation (ceil(n / V) bytes)."""
+        if self.wire != "i16":
+            raise AttributeError("overflow flags exist only on the i16 wire")
+        return self.ovf_full[: -(-self.plan.n // self.V)]
+
+    def _reduce(self, slices) -> int:
+        m = self.hi - self.lo
+        if isinstance(slices, torch.Tensor):
+            slices = list(slices.unbind(0)) if slices.dim() > 1 else [slices]
+        slices = [t.reshape(-1) for t in slices]
+        if not slices or any(t.numel() != m for t in slices):
+            raise ValueError(f"every worker slice must hold this rank's {m} values")
+        if m == 0:                    # more ranks than ranges: nothing here, zeros gathered
+            return 0
+        if self.wire == "i32":
+            ops.quantize_reduce(slices, self.k, out=self.sum_shard[:m])
+        else:
+            ops.quantize_reduce_i16(slices, self.k, self.V, out=self.sum_shard[:m],
+                                    overflow=self.ovf_shard[: -(-m // self.V)])
+        return m
+
+    def __call__(self, slices) -> torch.Tensor:
+        """W fp32 slices of this rank's range -> fp32 [n] aggregate on every rank."""
+        m = self._reduce(slices)
+        if m:
+            ops.dequantize(self.sum_shard[:m], self.k, out=self.f_shard[:m])
+        if self.world > 1:
+            all_gather_shards(self.f_shard, self.plan, self.group, out=self.full)
+            if self.wire == "i16":
+                all_gather_shards(self.ovf_shard, self.plan, self.group, out=self.ovf_full)
+        return self.full[: self.plan.n]
+
+    def aggregate_int(self, slices) -> torch.Tensor:
+        """W fp32 slices -> this rank's integer aggregate (int32 wrapped, or int16
+        saturated with its slot flags in `ovf_shard`), no gather."""
+        m = self._reduce(slices)
+        return self.sum_shard[:m]

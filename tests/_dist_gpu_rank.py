@@ -2,7 +2,7 @@
 torch.distributed.run.  Every rank lives on cuda:0 and the group is gloo (one GPU cannot
 host two RCCL ranks), so the collectives stage through host memory while quantise,
 wire decode and dequantise run as the libina.so kernels: the product path of
-ina_amd.dist.ShardedAggregator at world size > 1.  Writes its aggregate to
+ina_amd.dist.ShardedAggregator (layout A) or RangeAggregator (layout B) at world size > 1.  Writes its aggregate to
 OUT/rank<r>.npz for the test to compare with the oracle."""
 import argparse
 import os
@@ -38,15 +38,23 @@ def main():
     ap.add_argument("--V", type=int, default=256)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--layout", choices=("A", "B"), default="A")
+    ap.add_argument("--workers", type=int, default=0, help="layout B: W buckets (default: world)")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     from ina_amd import _lib
-    from ina_amd.dist import ShardedAggregator
+    from ina_amd.dist import RangeAggregator, ShardedAggregator
     dev = torch.device("cuda", 0)
-    x = torch.from_numpy(bucket(rank, a.size, a.wire)).to(dev)
-    agg = ShardedAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V)
+    if a.layout == "A":
+        x = torch.from_numpy(bucket(rank, a.size, a.wire)).to(dev)
+        agg = ShardedAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V)
+    else:                                      # every worker's slice of this rank's range
+        agg = RangeAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V)
+        lo, hi = agg.range
+        x = [torch.from_numpy(bucket(w, a.size, a.wire)[lo:hi].copy()).to(dev)
+             for w in range(a.workers or world)]
     for _ in range(a.steps):                   # buffers are reused across calls
         full = agg(x)
     torch.cuda.synchronize()

@@ -148,3 +148,21 @@ def test_i16_wire_oracle_identity():
         o16, y, ovf = orc.i16_wire_finish(s.astype(np.int32), k, V)
         w16, wovf = orc.quantize_reduce_i16_sat(xs, k, V)
         assert np.array_equal(o16, w16) and np.array_equal(ovf, wovf)
+
+
+def test_range_aggregator_host_checks():
+    """Layout B's host side without a GPU: one rank owns the whole range; worker slices of
+    the wrong length and unknown wires are refused before any kernel runs."""
+    from ina_amd.dist import RangeAggregator
+    agg = RangeAggregator(5000, device=torch.device("cpu"))
+    assert agg.range == (0, 5000) and agg.plan.padded >= 5000
+    with pytest.raises(ValueError):
+        agg.aggregate_int([torch.zeros(4999), torch.zeros(5000)])
+    with pytest.raises(ValueError):
+        agg([])
+    with pytest.raises(ValueError):
+        RangeAggregator(10, wire="i8", device=torch.device("cpu"))
+    a16 = RangeAggregator(3000, wire="i16", V=100, device=torch.device("cpu"))
+    assert a16.plan.shard % 100 == 0 and a16.ovf_shard.numel() == a16.plan.shard // 100
+    with pytest.raises(AttributeError):
+        _ = agg.overflow

@@ -52,6 +52,7 @@ def test_bench_json_line_contract():
     assert "workload" in d["config"]
     c5 = d["sharded_c5"]
     assert c5["parity_spot_check"] is True and c5["rccl_world"] == 1 and c5["values_per_rank"] == 1 << 22
+    assert c5["layout_b"]["parity_spot_check"] is True and c5["layout_b"]["value"] > 0
     sw = d["switch_c3"]                          # the packet-stream switch, measured live
     assert sw["algorithmic_bytes"] == 819_200 * 1040 + 102_400 * (1040 + 1029) + 819_200
     for order in ("worker_major", "round_robin"):
@@ -67,6 +68,7 @@ def test_bench_sharded_mode_line():
                        "--wire", wire))
         assert d["n_gpus"] == 1 and d["value"] > 0 and d["parity_spot_check"] is True, wire
         assert d["config"]["values_per_worker"] == 1 << 22
+        assert d["layout_b"]["parity_spot_check"] is True, wire
 
 
 @pytest.mark.gpu
@@ -80,6 +82,9 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     c5 = d["sharded_c5"]
     assert c5["rccl_world"] == 2 and c5["parity_spot_check"] is True
     assert c5["xgmi"]["rs_send_bytes_per_rank"] == c5["shard_values"] * 4
+    assert c5["layout_b"]["parity_spot_check"] is True
+    assert c5["layout_b"]["xgmi"]["ag_recv_bytes_per_rank"] == c5["shard_values"] * 4
     d = _line(_run("--gpus", "2", "--mode", "sharded", "--wire", "i16", "--c5-values", "1000003",
                    "--c5-steps", "2", env={"INA_BENCH_BACKEND": "gloo"}, timeout=400))
     assert d["n_gpus"] == 2 and d["parity_spot_check"] is True
+    assert d["layout_b"]["parity_spot_check"] is True

@@ -5,6 +5,8 @@ quantise / wire decode / dequantise through libina.so.  Every rank's full aggreg
 compared bit for bit with the oracle's single-bucket path over all ranks' buckets:
   i32: dequantize_i32(quantize_reduce_i32)           (the switch's wrapping slot sum)
   i16: dequantize_i16(quantize_reduce_i16_sat) + the per-slot overflow flags
+Layout B (RangeAggregator: every worker's slice of a rank's range on that rank, a local
+fused quantise + reduce, an all-gather) against the same oracle.
 Plus config 5 at its full size on one rank (1 GiB bucket), checked on a strided sample."""
 import os
 import socket
@@ -26,10 +28,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(tmp_path, world, n, wire, k, V=256):
+def _run_ranks(tmp_path, world, n, wire, k, V=256, layout="A", workers=0):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", RANK_SCRIPT,
-           "--size", str(n), "--wire", wire, "--k", str(k), "--V", str(V), "--out", str(tmp_path)]
+           "--size", str(n), "--wire", wire, "--k", str(k), "--V", str(V), "--out", str(tmp_path),
+           "--layout", layout, "--workers", str(workers)]
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     return [dict(np.load(os.path.join(tmp_path, f"rank{i}.npz"))) for i in range(world)]
@@ -58,6 +61,39 @@ def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V):
     k = 11
     res = _run_ranks(tmp_path, world, n, "i16", k, V)
     want16, want_ovf = orc.quantize_reduce_i16_sat([bucket(r, n, "i16") for r in range(world)], k, V)
+    assert want_ovf.any() and not want_ovf.all()
+    want = orc.dequantize_i16(want16, k)
+    for r, d in enumerate(res):
+        assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
+        assert np.array_equal(d["ovf"], want_ovf), f"rank {r}"
+        lo, hi = d["range"]
+        assert np.array_equal(d["shard"], want16[lo:hi])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,W", [(2, 1_000_003, 2), (3, 70_001, 5), (8, 400_001, 8), (8, 3000, 3)])
+def test_range_layout_b_i32_device_kernels(tmp_path, world, n, W):
+    """Layout B: each rank reduces the W workers' slices of its own range (fused quantise +
+    reduce kernel), decodes, all-gathers -- the same bits as the single-bucket path."""
+    from oracle import oracle as orc
+    k = 20
+    res = _run_ranks(tmp_path, world, n, "i32", k, layout="B", workers=W)
+    want_int = orc.quantize_reduce_i32([bucket(w, n, "i32") for w in range(W)], k)
+    want = orc.dequantize_i32(want_int, k)
+    for r, d in enumerate(res):
+        assert d["lib"][0].endswith("libina.so")
+        assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
+        lo, hi = d["range"]
+        assert np.array_equal(d["shard"], want_int[lo:hi])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,V,W", [(2, 1_000_003, 256, 2), (3, 50_000, 32, 4), (8, 200_000, 32, 8)])
+def test_range_layout_b_i16_device_kernels(tmp_path, world, n, V, W):
+    from oracle import oracle as orc
+    k = 11
+    res = _run_ranks(tmp_path, world, n, "i16", k, V, layout="B", workers=W)
+    want16, want_ovf = orc.quantize_reduce_i16_sat([bucket(w, n, "i16") for w in range(W)], k, V)
     assert want_ovf.any() and not want_ovf.all()
     want = orc.dequantize_i16(want16, k)
     for r, d in enumerate(res):
