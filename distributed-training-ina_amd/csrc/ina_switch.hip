@@ -929,7 +929,9 @@ static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWI
 #ifndef INA_SWITCH_WAVES_RUN
 #define INA_SWITCH_WAVES_RUN 7
 #endif
-// occupancy target of k_switch_run2 (waves per SIMD); 4 fits its registers, 5 spills 4
+// occupancy floor of k_switch_run2<true> (waves per SIMD): the compiler then takes 75 VGPRs
+// = 6 waves, no scratch; forcing 7 (72 VGPRs, 12 B/lane scratch) ran 1 % slower
+// (profiles/r02/lab/fuse_lab_waves.log)
 #ifndef INA_SWITCH_WAVES
 #define INA_SWITCH_WAVES 4
 #endif

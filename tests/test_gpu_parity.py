@@ -212,7 +212,7 @@ def test_quantize_dequantize_round_trip_bound():
 # --------------------------------------------------------------------------------------
 # fused quantise + reduce (configs 2 and 4) and the int16 narrow reduce
 # --------------------------------------------------------------------------------------
-@pytest.mark.parametrize("W", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("W", [1, 2, 3, 4, 8, 16])
 @pytest.mark.parametrize("n", [5, 1024, 50003])
 def test_quantize_reduce_i32(W, n):
     rng = np.random.default_rng(W + n)
@@ -221,7 +221,7 @@ def test_quantize_reduce_i32(W, n):
     assert np.array_equal(got, orc.quantize_reduce_i32(bufs, 16))
 
 
-@pytest.mark.parametrize("W", [3, 4, 8, 16])
+@pytest.mark.parametrize("W", [1, 3, 4, 8, 16])
 @pytest.mark.parametrize("V", [32, 256, 96])
 def test_quantize_reduce_i16(W, V):
     rng = np.random.default_rng(W * V)
