@@ -892,6 +892,9 @@ constexpr uint32_t kSelWire = 0x07000102u;   // perm(next, v): {v.b2, v.b1, v.b0
 #ifndef INA_UNPACK_U
 #define INA_UNPACK_U 1
 #endif
+#ifndef INA_UNPACK_HDR_SPLIT
+#define INA_UNPACK_HDR_SPLIT 1
+#endif
 
 template <typename Src, int U>
 __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, NgaHdr h,
@@ -1040,6 +1043,19 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_flat(const uint8_t* __res
     const int lane = threadIdx.x & 63;
     const uint32_t wave0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
     const u32x4* ch = reinterpret_cast<const u32x4*>(pkts);
+#if INA_UNPACK_HDR_SPLIT
+    // header fields by a thread per packet: consecutive lanes store consecutive SoA
+    // entries.  The chunk-0 lane's six narrow stores (one packet per wave, every field
+    // line written from many waves) cost 13 % (profiles/r01/lab/unpack_out_lab.log);
+    // this pass: 42.6 -> 39.3 us, a separate header kernel 42.0 (profiles/r02/lab/unpack_hdr_lab.log)
+    if (hdr) {
+        const uint32_t np = nch / C;
+        for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < np; p += gs) {
+            const u32x4 hv = ch[(size_t)p * C];
+            nga_store_header(f, p, hv.x, hv.y, hv.z, hv.w);
+        }
+    }
+#endif
     for (uint32_t base = wave0; base < nch; base += U * gs) {
         u32x4 a[U];
         uint32_t pw0[U];
@@ -1058,7 +1074,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_flat(const uint8_t* __res
             if (t >= nch) continue;
             const uint32_t p = t / C, c = t - p * C;
             if (c == 0) {
-                if (hdr) nga_store_header(f, p, a[u].x, a[u].y, a[u].z, a[u].w);
+                if (hdr && !INA_UNPACK_HDR_SPLIT) nga_store_header(f, p, a[u].x, a[u].y, a[u].z, a[u].w);
             } else if (c <= L && vals) {
                 u32x4 o;
                 o.x = __builtin_amdgcn_perm(a[u].x, pw, kSelBE);

@@ -131,7 +131,7 @@ NOTES = {
     "`k_pack_nga_flat<SrcQ32>`": "; was 80.9 µs (48 %) as a thread-per-chunk kernel that re-read and re-quantised a 5th value per chunk",
     "`k_apply_completed_nga`": "; was 98.6 µs (40 %) as one lane group per packet over every packet",
     "`k_absmax_f32`": " at 256 workgroups; 86 µs at 8192 (one atomicMax per workgroup on one word); a read-before-atomic skip changed nothing at 256 and larger grids stay slower with it (`profiles/r02/lab/absmax_skip_lab.log`)",
-    "`k_unpack_nga_flat`": "; a thread-per-output-chunk variant (unbroken store stream, header chunks skipped by the loads) was 3 % faster without the header fields and 4 % slower with them (`profiles/r01/lab/unpack_out_lab.log`)",
+    "`k_unpack_nga_flat`": "; the SoA header fields by a thread-per-packet pass inside the kernel (coalesced stores) instead of six narrow stores from each packet's chunk-0 lane: 42.6 -> 39.3 us (`profiles/r02/lab/unpack_hdr_lab.log`); a thread-per-output-chunk variant (unbroken store stream, header chunks skipped by the loads) was 3 % faster without the header fields and 4 % slower with them (`profiles/r01/lab/unpack_out_lab.log`)",
     "`k_pack_c128`": ": 4 wire words per thread with one 16-byte store (4-byte gradient loads, one 32-bit divide by 131), 38.7 -> 35.7 µs against a word per thread (`profiles/r02/lab/c128_lab.log`); round 1's aligned-8-word-window variant was slower, 41.6 µs",
 }
 

@@ -44,10 +44,12 @@ ref = None
 for nm, lib, _ in libs:
     assert run(lib, "pack") == 0 and run(lib, "unpack") == 0
     torch.cuda.synchronize()
-    got = (out_pk.clone(), vals.clone())
+    got = (out_pk.clone(), vals.clone()) + tuple(f[k].clone() for k in sorted(f))
+    for t in f.values():
+        t.fill_(0x5A)                            # the next variant must write every field
     if ref is None:
         ref = got
-    assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1]), nm
+    assert all(torch.equal(a, b) for a, b in zip(ref, got)), nm
 del ref
 for _ in range(int(os.environ.get("ROUNDS", 8))):
     for nm, lib, ts in libs:
