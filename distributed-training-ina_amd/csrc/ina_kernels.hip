@@ -892,6 +892,9 @@ constexpr uint32_t kSelWire = 0x07000102u;   // perm(next, v): {v.b2, v.b1, v.b0
 #ifndef INA_UNPACK_U
 #define INA_UNPACK_U 1
 #endif
+#ifndef INA_PACK_DESC_SPLIT
+#define INA_PACK_DESC_SPLIT 1
+#endif
 #ifndef INA_UNPACK_HDR_SPLIT
 #define INA_UNPACK_HDR_SPLIT 1
 #endif
@@ -907,6 +910,22 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, Nga
     const uint32_t wave0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
     const size_t V = (size_t)h.V;
     u32x4* ch = reinterpret_cast<u32x4*>(pkts);
+#if INA_PACK_DESC_SPLIT
+    // descriptors (header bytes 4..11) depend on the packet number alone: a thread per
+    // packet writes them, consecutive lanes consecutive entries (coalesced), instead of one
+    // 8-byte store from each packet's chunk-0 lane (the unpack header fields' pattern)
+    if (desc) {
+        const uint32_t np = nch / C;
+        const uint32_t count = h.flags_count_sw & 0xFFu, sw = (h.flags_count_sw >> 16) & 0xFFu;
+        for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < np; p += gs) {
+            const uint32_t seq = h.seq0 + p;
+            const uint32_t bi = bswap(seq % h.num_slots), bf = bswap(seq);
+            uint32_t flags = (h.flags_count_sw >> 8) & 0xFFu;
+            if (ovf && ovf[p]) flags |= INA_FLAG_OVERFLOW;
+            desc[p] = u32x2{count | (flags << 8) | (bi << 16), (bi >> 16) | (sw << 16) | (bf << 24)};
+        }
+    }
+#endif
     for (uint32_t base = wave0; base < nch; base += U * gs) {
         u32x4 v[U];
         uint32_t nx0[U];
@@ -950,7 +969,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, Nga
                 o.y = count | (flags << 8) | (bi << 16);
                 o.z = (bi >> 16) | (sw << 16) | (bf << 24);
                 o.w = (bf >> 8) | (nx & 0xFF000000u);        // value 0's top byte at byte 15
-                if (desc) desc[p] = u32x2{o.y, o.z};          // header bytes 4..11 (ina.h)
+                if (desc && !INA_PACK_DESC_SPLIT) desc[p] = u32x2{o.y, o.z};   // header bytes 4..11 (ina.h)
             } else if (c <= L) {
                 o.x = __builtin_amdgcn_perm(v[u].y, v[u].x, kSelWire);
                 o.y = __builtin_amdgcn_perm(v[u].z, v[u].y, kSelWire);

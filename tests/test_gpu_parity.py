@@ -709,6 +709,16 @@ def test_pack_descriptors_are_header_bytes(V, stride_kind):
     x = dev(rng.standard_normal(n).astype(np.float32))
     pk2, d2 = o.quantize_pack_nga(x, 16, V, 2, 3, 1, 9, stride=stride, desc=True)
     assert np.array_equal(host(d2), host(pk2)[:, 4:12].copy().view(np.int64).reshape(-1))
+    # per-slot overflow bits in the flags byte, and batches split into packet ranges
+    ovf = dev((rng.random(-(-n // V)) < 0.5).astype(np.uint8))
+    try:
+        for chunks in (2**31 - 1, 3 * (stride // 16) + 1):
+            o.set_tuning(launch_chunks=chunks)
+            pk3, d3 = o.pack_nga(vals, V, 5, 3, 2, 4_000_000_000, num_slots=1000, stride=stride,
+                                 overflow=ovf, desc=True)
+            assert np.array_equal(host(d3), host(pk3)[:, 4:12].copy().view(np.int64).reshape(-1)), chunks
+    finally:
+        o.set_tuning(launch_chunks=2**31 - 1)
 
 
 @pytest.mark.parametrize("write_dropped", [True, False])

@@ -29,12 +29,18 @@ st = torch.cuda.current_stream().cuda_stream
 libs = []
 for p in sys.argv[1:]:
     lib = C.CDLL(p)
-    for nm in ("ina_unpack_nga", "ina_pack_nga"):
+    for nm in ("ina_unpack_nga", "ina_pack_nga", "ina_pack_nga_desc"):
         getattr(lib, nm).argtypes = _lib.SIGNATURES[nm]
-    libs.append((os.path.basename(p), lib, {"pack": [], "unpack": []}))
+    libs.append((os.path.basename(p), lib, {"pack": [], "pack_desc": [], "unpack": []}))
+
+
+desc = torch.empty(npk, dtype=torch.int64, device=dev)
 
 
 def run(lib, which):
+    if which == "pack_desc":
+        return lib.ina_pack_nga_desc(x.data_ptr(), n, C.byref(prm), None, out_pk.data_ptr(), stride,
+                                     desc.data_ptr(), st)
     if which == "pack":
         return lib.ina_pack_nga(x.data_ptr(), n, C.byref(prm), None, out_pk.data_ptr(), stride, st)
     return lib.ina_unpack_nga(pk.data_ptr(), npk, V, stride, C.byref(fs), vals.data_ptr(), st)
@@ -42,9 +48,13 @@ def run(lib, which):
 
 ref = None
 for nm, lib, _ in libs:
+    assert run(lib, "pack_desc") == 0
+    torch.cuda.synchronize()
+    got_d = (out_pk.clone(), desc.clone())
+    desc.fill_(0)
     assert run(lib, "pack") == 0 and run(lib, "unpack") == 0
     torch.cuda.synchronize()
-    got = (out_pk.clone(), vals.clone()) + tuple(f[k].clone() for k in sorted(f))
+    got = (out_pk.clone(), vals.clone()) + tuple(f[k].clone() for k in sorted(f)) + got_d
     for t in f.values():
         t.fill_(0x5A)                            # the next variant must write every field
     if ref is None:
@@ -53,7 +63,7 @@ for nm, lib, _ in libs:
 del ref
 for _ in range(int(os.environ.get("ROUNDS", 8))):
     for nm, lib, ts in libs:
-        for which in ("pack", "unpack"):
+        for which in ("pack", "pack_desc", "unpack"):
             evs = []
             for _ in range(4):
                 ops.checksum(flush)
@@ -65,4 +75,4 @@ for _ in range(int(os.environ.get("ROUNDS", 8))):
             torch.cuda.synchronize()
             ts[which] += [a.elapsed_time(b) * 1e3 for a, b in evs[1:]]
 for nm, _, ts in libs:
-    print(f"{nm:22s} pack {statistics.median(ts['pack']):6.1f} us   unpack {statistics.median(ts['unpack']):6.1f} us")
+    print(f"{nm:22s} " + "   ".join(f"{k} {statistics.median(v):6.1f} us" for k, v in ts.items()))
