@@ -49,7 +49,7 @@ class Variant:
         self.q16 = torch.empty(n, dtype=torch.int16, device=dev)
         self.fq16 = torch.empty((n + 255) // 256, dtype=torch.uint8, device=dev)
         self.t = {"quantize": [], "dequantize": [], "ps_apply": [], "qreduce_C2": [], "combine": [],
-                  "combine_ina": [], "qreduce_C4": [], "quantize16": []}
+                  "combine_ina": [], "qreduce_C4": [], "quantize16": [], "quantize16_noflags": []}
         for key, env in ((5, "COMBINE_BLOCKS"), (6, "COMBINE_INA_BLOCKS"), (4, "STREAM_BLOCKS")):
             if os.environ.get(env):
                 self.lib.ina_set_tuning(key, int(os.environ[env]))
@@ -76,6 +76,10 @@ class Variant:
     def quantize16(self):
         return self.lib.ina_quantize_f32_i16_sat(x.data_ptr(), self.q16.data_ptr(), n, K16 + 2, 256,
                                                  self.fq16.data_ptr(), st)
+
+    def quantize16_noflags(self):
+        return self.lib.ina_quantize_f32_i16_sat(x.data_ptr(), self.q16.data_ptr(), n, K16 + 2, 256,
+                                                 None, st)
 
     def ps_apply(self):
         return self.lib.ina_ps_apply_i32(local.data_ptr(), q.data_ptr(), 16, 0.1, self.oa.data_ptr(), n, st)
