@@ -1363,13 +1363,19 @@ __device__ __forceinline__ float absdiff(float x, const float* base, size_t i) {
     return fabsf(base ? __fsub_rn(x, base[i]) : x);
 }
 
+#ifndef INA_ABSMAX_U
+#define INA_ABSMAX_U 4
+#endif
+#ifndef INA_ABSMAX_BLOCKS
+#define INA_ABSMAX_BLOCKS kFaninBlocks
+#endif
 __global__ __launch_bounds__(kBlock) void k_absmax_f32(const float* __restrict__ x,
                                                        const float* __restrict__ base, size_t n,
                                                        int vec, uint32_t* __restrict__ out) {
     __shared__ float part[kBlock / 64];
     const size_t n4 = vec ? n / 4 : 0;
     float m = 0.0f;
-    chunk_loop<4>(n4, [&]<int UU>(size_t i, size_t st) {
+    chunk_loop<INA_ABSMAX_U>(n4, [&]<int UU>(size_t i, size_t st) {
         f32x4 a[UU], b[UU];
 #pragma unroll
         for (int u = 0; u < UU; ++u) {
@@ -1831,9 +1837,11 @@ int ina_absmax_f32(const float* x, const float* base, size_t n, float* out_dev, 
     if (n == 0) return INA_OK;
     if (!x) return set_error(INA_EINVAL, "null pointer%s", "");
     const int vec = aligned16(x) && (!base || aligned16(base));
-    // every block ends in one atomicMax on the same word (~11 ns each, serialised), so the
-    // grid stays small: 256 workgroups 38 us, 2048 47 us, 8192 86 us (ResNet-50 delta)
-    hipLaunchKernelGGL(k_absmax_f32, dim3(grid_for(vec ? n / 4 + 1 : n, 4, kFaninBlocks)), dim3(kBlock), 0,
+    // every block ends in one atomicMax on the same word (~11 ns each, serialised, and all
+    // blocks end together), so the grid stays small: 256 workgroups 38 us, 2048 47 us, 8192
+    // 86 us (ResNet-50 delta); 8 or 16 chunks in flight per lane instead of 4 were slower
+    // (profiles/r02/lab/absmax_geometry_lab.log)
+    hipLaunchKernelGGL(k_absmax_f32, dim3(grid_for(vec ? n / 4 + 1 : n, INA_ABSMAX_U, INA_ABSMAX_BLOCKS)), dim3(kBlock), 0,
                        s, x, base, n, vec, reinterpret_cast<uint32_t*>(out_dev));
     return check_launch("absmax_f32");
 }
