@@ -26,9 +26,12 @@ Multi-GPU:
     dequantise -> all_gather(fp32) (ina_amd.dist.ShardedAggregator), with per-
     phase times, the xGMI bytes per rank and a parity check of the aggregate.
   --mode sharded makes config 5 the headline line instead.
-  * "switch_c3" (N = 1) -- the packet-stream switch (ina_switch_process) on
+  * "switch_c3" -- the packet-stream switch (ina_switch_process) on
     config 3 as 819,200 NGA-256 packets, worker-major and round-robin arrival, with its
-    own roofline fraction on its algorithmic bytes.
+    own roofline fraction on its algorithmic bytes; at N > 1 every rank switches its own
+    bucket (max-over-ranks time, aggregate bytes/s).
+  * "sharded_c5.layout_b" -- config 5 when the workers' slices arrive split by range
+    (ina_amd.dist.RangeAggregator): local fused quantise + reduce, one all-gather.
 
 Extra rows (not the headline): --extra writes per-kernel timings of the other
 configs (fused quantise+reduce C2, int16 C4, pack/unpack, PS combine, end-to-end
@@ -421,17 +424,19 @@ def measure_c5_layout_b(args, rank, world, dev, warmup=2):
 
 
 # -- the packet-stream switch on config 3 ----------------------------------------
-def measure_switch(dev, reps=10, warm=2):
+def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
     """ina_switch_process over config 3 as NGA-256 packets: 8 workers x 102,400 packets
     (2^17-slot pool, keys from the pack kernels' descriptors), in worker-major and in
     round-robin arrival (a NIC interleaving the workers).  HIP events on the launch stream
     around each call; the replayed batch completes every slot again, so no state reset
     sits in the timed region.  Algorithmic bytes: every packet read, the completing 1/W
-    written back, each slot's registers + count + frag written, one action byte per packet."""
+    written back, each slot's registers + count + frag written, one action byte per packet.
+    At N > 1 every rank runs its own switch on its own bucket (slots are independent,
+    ngaa.p4:87-168): `us` is the max over ranks, `aggregate_GBps` all ranks' bytes / that."""
     from ina_amd import ops
     W, n, V, slots = W_WORKERS, N_VALUES, V_SLOT, 1 << 17
     g = torch.Generator(device=dev)
-    g.manual_seed(4242)
+    g.manual_seed(4242 + rank)
     packed = []
     for w in range(W):
         b = torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
@@ -448,13 +453,14 @@ def measure_switch(dev, reps=10, warm=2):
     s = torch.cuda.current_stream(dev)
     res = {"workload": "C3 as NGA-256 packets: 8 workers x 102,400 packets (819,200), 2^17-slot "
                        "pool, keys from descriptors; ina_switch_process incl. its slot sort",
-           "algorithmic_bytes": algo}
+           "algorithmic_bytes": algo, "ranks": world}
     order = {"worker_major": None,
              "round_robin": torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1)}
     for name, perm in order.items():
         st, ds = (stream, desc) if perm is None else (stream[perm], desc[perm])
         for _ in range(warm):
             sw.process(st, acts, desc=ds)
+        barrier(world)
         evs = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -463,11 +469,13 @@ def measure_switch(dev, reps=10, warm=2):
             e1.record(s)
             evs.append((e0, e1))
         torch.cuda.synchronize()
-        us = statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3
+        us = max_over_ranks(statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3, world)
         done = int((acts == 1).sum())
         res[name] = {"us": round(us, 2), "achieved_GBps": round(algo / us / 1e3, 1),
                      "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
-                     "ok": done == npk}
+                     "ok": all_ranks_true(done == npk, world)}
+        if world > 1:
+            res[name]["aggregate_GBps"] = round(world * algo / us / 1e3, 1)
         del st, ds
     del stream, desc, sw, acts
     torch.cuda.empty_cache()
@@ -586,8 +594,8 @@ def run_reduce(args, rank, world, dev, backend):
         line["sharded_c5"] = measure_c5(args, rank, world, dev)
         torch.cuda.empty_cache()
         line["sharded_c5"]["layout_b"] = measure_c5_layout_b(args, rank, world, dev)
-    if not args.no_switch and rank == 0 and world == 1:
-        line["switch_c3"] = measure_switch(dev)
+    if not args.no_switch:
+        line["switch_c3"] = measure_switch(dev, rank=rank, world=world)
     return line
 
 

@@ -84,6 +84,9 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert c5["xgmi"]["rs_send_bytes_per_rank"] == c5["shard_values"] * 4
     assert c5["layout_b"]["parity_spot_check"] is True
     assert c5["layout_b"]["xgmi"]["ag_recv_bytes_per_rank"] == c5["shard_values"] * 4
+    sw = d["switch_c3"]                          # every rank switched its own bucket
+    assert sw["ranks"] == 2 and sw["worker_major"]["ok"] is True and sw["round_robin"]["ok"] is True
+    assert sw["worker_major"]["aggregate_GBps"] > 0
     d = _line(_run("--gpus", "2", "--mode", "sharded", "--wire", "i16", "--c5-values", "1000003",
                    "--c5-steps", "2", env={"INA_BENCH_BACKEND": "gloo"}, timeout=400))
     assert d["n_gpus"] == 2 and d["parity_spot_check"] is True

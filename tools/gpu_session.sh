@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; the script stops at the first crash,
 # abort or timeout (only an ordinary pytest failure, rc 1, lets it continue).
 # usage: tools/gpu_session.sh TAG [stages...]   stages: smoke test bench prof pmc extra swprof
-#        config1 rehearse sharded swlab pathprof
+#        config1 rehearse rehearse8 sharded swlab pathprof
 set -u
 TAG=${1:-r02}; shift || true
 STAGES=${*:-"smoke test bench prof pmc extra"}
@@ -54,6 +54,11 @@ for st in $STAGES; do
       INA_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 5 \
         --c5-values 67108864 > "$OUT/rehearse2.json" 2> "$OUT/rehearse2.err"
       rc=$?; cat "$OUT/rehearse2.json"; tail -3 "$OUT/rehearse2.err"; [ $rc -ne 0 ] && fatal rehearse $rc ;;
+    rehearse8)
+      # bench.py --gpus 8 the way the driver's scale run starts it, 8 ranks on one GPU over gloo
+      INA_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 8 --steps 10 --warmup 3 \
+        --c5-values 16777216 --c5-steps 3 > "$OUT/rehearse8.json" 2> "$OUT/rehearse8.err"
+      rc=$?; tail -c 600 "$OUT/rehearse8.json"; tail -3 "$OUT/rehearse8.err"; [ $rc -ne 0 ] && fatal rehearse8 $rc ;;
     sharded)
       for wire in i32 i16; do
         timeout -k 10 400 python bench.py --mode sharded --wire $wire > "$OUT/sharded1_$wire.json" 2> "$OUT/sharded1_$wire.err"

@@ -20,6 +20,7 @@ cp "$S/bench_extra.json" "$D/bench_extra.json"
 # optional stages
 [ -f "$S/pytest_gpu.log" ] && cp "$S/pytest_gpu.log" "$D/pytest_gpu.log"
 [ -f "$S/rehearse2.json" ] && cp "$S/rehearse2.json" "$D/rehearse_2ranks_gloo.json"
+[ -f "$S/rehearse8.json" ] && grep '^{' "$S/rehearse8.json" > "$D/rehearse_8ranks_gloo.json"
 [ -f "$S/sharded1_i32.json" ] && cp "$S/sharded1_i32.json" "$D/sharded_c5_1gpu_i32.json"
 [ -f "$S/sharded1_i16.json" ] && cp "$S/sharded1_i16.json" "$D/sharded_c5_1gpu_i16.json"
 [ -f "$S/config1.log" ] && cp "$S/config1.log" "$D/config1_loopback.log"
