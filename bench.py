@@ -428,9 +428,10 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
     """ina_switch_process over config 3 as NGA-256 packets: 8 workers x 102,400 packets
     (2^17-slot pool, keys from the pack kernels' descriptors), in worker-major and in
     round-robin arrival (a NIC interleaving the workers).  HIP events on the launch stream
-    around each call; the replayed batch completes every slot again, so no state reset
-    sits in the timed region.  Algorithmic bytes: every packet read, the completing 1/W
-    written back, each slot's registers + count + frag written, one action byte per packet.
+    around `reps` back-to-back calls (the headline's method); the replayed batch completes
+    every slot again, so no state reset sits in the timed region.  Algorithmic bytes: every
+    packet read, the completing 1/W written back, each slot's registers + count + frag
+    written, one action byte per packet.
     At N > 1 every rank runs its own switch on its own bucket (slots are independent,
     ngaa.p4:87-168): `us` is the max over ranks, `aggregate_GBps` all ranks' bytes / that."""
     from ina_amd import ops
@@ -461,6 +462,18 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
         for _ in range(warm):
             sw.process(st, acts, desc=ds)
         barrier(world)
+        # like the headline's avg_launch_us: one event pair around `reps` back-to-back calls
+        # (a pair per call adds ~7 us of event overhead, tools/lab/event_overhead_lab.py;
+        # reported beside it as us_event_pair_per_call)
+        per_rep = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                sw.process(st, acts, desc=ds)
+            e1.record(s)
+            torch.cuda.synchronize()
+            per_rep.append(e0.elapsed_time(e1) * 1e3 / reps)
         evs = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -469,11 +482,12 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
             e1.record(s)
             evs.append((e0, e1))
         torch.cuda.synchronize()
-        us = max_over_ranks(statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3, world)
+        us = max_over_ranks(statistics.median(per_rep), world)
+        us_pair = max_over_ranks(statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3, world)
         done = int((acts == 1).sum())
         res[name] = {"us": round(us, 2), "achieved_GBps": round(algo / us / 1e3, 1),
                      "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
-                     "ok": all_ranks_true(done == npk, world)}
+                     "ok": all_ranks_true(done == npk, world), "us_event_pair_per_call": round(us_pair, 2)}
         if world > 1:
             res[name]["aggregate_GBps"] = round(world * algo / us / 1e3, 1)
         del st, ds
