@@ -88,7 +88,8 @@ def test_range_layout_b_i32_device_kernels(tmp_path, world, n, W):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n,V,W", [(2, 1_000_003, 256, 2), (3, 50_000, 32, 4), (8, 200_000, 32, 8)])
+@pytest.mark.parametrize("world,n,V,W", [(2, 1_000_003, 256, 2), (3, 50_000, 32, 4), (8, 200_000, 32, 8),
+                                         (3, 300_001, 100, 3)])
 def test_range_layout_b_i16_device_kernels(tmp_path, world, n, V, W):
     from oracle import oracle as orc
     k = 11
