@@ -951,9 +951,9 @@ static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWI
 #define INA_SWITCH_TAIL_NT 0
 #endif
 // the batch's action bytes leave in one store (lane b: packet b) instead of one per packet:
-// 241.7 -> 234.9 us for the switch alone, but with the PS step fused the extra registers
-// cost an occupancy step (72 -> 78 VGPRs: 264.6 -> 289.1 us), so only without it
-// (profiles/r02/lab/switch_lab_actbatch.log)
+// 241.7 -> 234.9 us for the switch alone (profiles/r02/lab/switch_lab_actbatch.log); with
+// the PS step fused, once that kernel sat at 75 VGPRs / 6 waves either way, 294.3 -> 291.0
+// us (fuse_lab_actbatch_ps.log; at the time of the first lab it cost an occupancy step)
 #ifndef INA_SWITCH_ACT_BATCH
 #define INA_SWITCH_ACT_BATCH 1
 #endif
@@ -1016,7 +1016,7 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                                  uint8_t* __restrict__ actions, uint32_t win,
                                                  uint32_t kmask, const PsFuse& ps, size_t wave,
                                                  size_t nwaves) {
-    constexpr bool kActBatch = INA_SWITCH_ACT_BATCH && !kPs;
+    constexpr bool kActBatch = INA_SWITCH_ACT_BATCH;
     const int lane = threadIdx.x & 63;
     const int V = st.V;
     const int L = V >> 2;                       // lanes holding values
