@@ -790,6 +790,32 @@ def test_switch_small_batch_paths_agree(seed):
     assert np.array_equal(outs[0][2], outs[1][2]) and np.array_equal(outs[0][2], outs[2][2])
 
 
+@pytest.mark.parametrize("num_slots", [16384, 1 << 17])
+def test_switch_state_across_batch_paths(num_slots):
+    """One switch, one register state, a sequence of batches whose sizes walk across the
+    default path thresholds (<= 128 packets: one launch; 129..768: one-workgroup sort +
+    run kernel; above: the bucket sort) and back: every batch's actions and packets and
+    the final registers equal the P4 restatement fed the same sequence."""
+    rng = np.random.default_rng(num_slots)
+    o = ops()
+    V, W = 32, 8
+    stride = o.nga_stride(V)
+    sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
+    sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+    for used in (10, 50, 500, 16, 17, 96, 97, 3000, 1, 200):     # x W = 8 packets per slot
+        stream = make_stream(rng, V, used, W, num_slots, stride=stride, idx_hi=2 * 4096)
+        assert stream.shape[0] == used * W
+        want_pk, want_act = sw_orc.run(stream, stride=stride)
+        d = dev(stream)
+        act = sw_dev.process(d)
+        assert np.array_equal(host(act), want_act), used
+        assert np.array_equal(host(d), want_pk), used
+    cnt, frag, regs = sw_orc.registers()
+    assert np.array_equal(host(sw_dev.count), cnt)
+    assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+    assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+
+
 def test_switch_collision_free_equals_bulk_reduce():
     """Stateful device switch over a full W-worker stream == the bulk sum-reduce."""
     rng = np.random.default_rng(77)
