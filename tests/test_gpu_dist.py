@@ -140,6 +140,27 @@ def test_c5_full_size_one_rank_strided_sample():
 
 
 @pytest.mark.gpu
+def test_c5_layout_b_full_size_one_rank_strided_sample():
+    """Layout B at config 5's size on one rank: two workers' 1 GiB fp32 slices (the whole
+    range) through RangeAggregator's fused quantise + reduce and decode; every 4099th
+    value plus the last 10,000 against the oracle."""
+    import torch
+    from ina_amd.dist import RangeAggregator
+    from oracle import oracle as orc
+    n, dev = 268_435_456, torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000)
+    xs = [torch.randn(n, device=dev, generator=g) * 1e-2 for _ in range(2)]
+    idx = np.concatenate([np.arange(0, n, 4099), np.arange(n - 10_000, n)])
+    tidx = torch.from_numpy(idx).to(dev)
+    agg = RangeAggregator(n, k=16, device=dev)
+    assert agg.range == (0, n)
+    y = agg(xs)
+    want = orc.dequantize_i32(orc.quantize_reduce_i32([x[tidx].cpu().numpy() for x in xs], 16), 16)
+    assert np.array_equal(y[tidx].cpu().numpy(), want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 3, 4, 255, 1000, 65_536, 1_000_003])
 @pytest.mark.parametrize("V", [32, 256, 100, 512])
 def test_i16_wire_kernels_vs_oracle(n, V):
