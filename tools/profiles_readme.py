@@ -65,7 +65,7 @@ of the headline bench on fresh boxes: {"; ".join(drivers) if drivers else "none 
 | `{RD}/kernel_stats_switch.csv` | rocprofv3 stats of `tools/prof_switch.py` (device switch on 819,200 NGA-256 packets, keys from the pack kernels' descriptors): `k_switch_run2` {sw[run2]['avg_us']} us, keys {sw[keys]['avg_us']} us, sort {sort_us:.1f} us |
 | `{RD}/switch_pmc_FETCH_SIZE.csv`, `{RD}/switch_pmc_WRITE_SIZE.csv`, `{RD}/traffic_switch.json` | PMC passes over the same program; per-kernel HBM bytes and rates computed by `tools/switch_traffic.py` (run kernel {(sw[run2]['hbm_read_bytes'] + sw[run2]['hbm_write_bytes']) / 1e9:.2f} GB at {sw[run2]['TB_per_s']} TB/s) |
 {rows}
-| `{RD}/lab/*` | interleaved A/B labs of this round (`tools/lab/`): slot sort variants (r01 passes, one-sweep, bucket + local), bucket workgroup waves, foreign-bucket skip, batched action stores, run-kernel window/batch/occupancy/prefetch/register-store policy, the run kernel's gather floor (`gather_lab.json`), switch arrival orders, the XCD-aware window map (`switch_lab_xcd.log`, and the same map on the flat packet kernels, `flat_lab_xcd.log`), head-chunk load policy, fused-PS occupancy and row prefetch, unpack header fields and pack descriptors as coalesced passes (`unpack_hdr_lab.log`, `pack_desc_lab.log`), elementwise and packet-kernel grid caps, absmax geometry, HIP-event overhead, lab buffer-placement check, a 300-seed switch fuzz on the final code (`fuzz_many.log`) |
+| `{RD}/lab/*` | interleaved A/B labs of this round (`tools/lab/`): slot sort variants (r01 passes, one-sweep, bucket + local), bucket workgroup waves, foreign-bucket skip, batched action stores, run-kernel window/batch/occupancy/prefetch/register-store policy, the run kernel's gather floor (`gather_lab.json`), switch arrival orders, the XCD-aware window map (`switch_lab_xcd.log`, and the same map on the flat packet kernels, `flat_lab_xcd.log`), head-chunk load policy, fused-PS occupancy and row prefetch, unpack header fields and pack descriptors as coalesced passes (`unpack_hdr_lab.log`, `pack_desc_lab.log`), elementwise and packet-kernel grid caps, absmax geometry, HIP-event overhead, lab buffer-placement check, a 600-seed switch fuzz on the final code (`fuzz_many.log`) |
 | `r01/` | round 1: the same files for round 1's code, its labs (`r01/lab/`), the per-box bench spread (`r01/bench_boxes.json`) |
 """
 open(os.path.join(P, "README.md"), "w").write(txt)
