@@ -269,10 +269,12 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
 
 # -- config 5: sharded over RCCL --------------------------------------------------------------
 def measure_c5(args, rank, world, dev, warmup=2):
-    """quantise -> reduce_scatter(int32, SUM) -> dequantise -> all_gather(fp32) of one
-    n-value fp32 bucket per rank; per-phase HIP-event times on the launch stream."""
+    """quantise -> reduce_scatter(int32, SUM) -> decode -> all_gather of one n-value fp32
+    bucket per rank (the i32 wire gathers fp32; the i16 wire gathers the saturated int16
+    sums + slot flags and dequantises after); per-phase HIP-event times on the launch
+    stream."""
     from ina_amd import ops
-    from ina_amd.dist import ShardedAggregator, all_gather_shards, reduce_scatter_sum
+    from ina_amd.dist import ShardedAggregator, all_gather_shards
     n = args.c5_values
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
@@ -290,27 +292,22 @@ def measure_c5(args, rank, world, dev, warmup=2):
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
 
-    # per-phase breakdown (one more pass, events between the phases)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    # per-phase breakdown (one more pass, events between the aggregator's own phases)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     barrier(world)
     ev[0].record(stream)
-    agg._quantize(bucket)
+    agg.phase_quantize(bucket)
     ev[1].record(stream)
-    if world > 1:
-        reduce_scatter_sum(agg.q, agg.plan, agg.group, out=agg.sum_shard)
+    agg.phase_reduce_scatter()
     ev[2].record(stream)
-    src = agg.sum_shard if world > 1 else agg.q
-    dst = agg.f_shard if world > 1 else agg.full
-    ovf = (agg.ovf_shard if world > 1 else agg.ovf_full) if args.wire == "i16" else None
-    agg._decode(src, dst, ovf)
+    agg.phase_decode()
     ev[3].record(stream)
-    if world > 1:
-        all_gather_shards(agg.f_shard, agg.plan, agg.group, out=agg.full)
-        if ovf is not None:
-            all_gather_shards(agg.ovf_shard, agg.plan, agg.group, out=agg.ovf_full)
+    agg.phase_all_gather()
     ev[4].record(stream)
+    agg.phase_expand()
+    ev[5].record(stream)
     torch.cuda.synchronize()
-    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(4)]
+    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(5)]
 
     # parity: the aggregate's first 64 Ki values == decode(sum over ranks of the
     # per-rank wire of those values), the per-rank wires all-gathered
@@ -334,7 +331,8 @@ def measure_c5(args, rank, world, dev, warmup=2):
 
     G = world
     S = agg.plan.padded * 4
-    xgmi = (G - 1) * S // G
+    xgmi = (G - 1) * S // G                # int32 wire words reduce-scattered
+    ag = agg.gather_bytes                  # fp32 (i32 wire) or int16 + flags (i16 wire)
     t_step = elapsed / steps
     return {
         "value": round(world * n * 4 * steps / elapsed / 1e9, 2), "unit": "GB/s",
@@ -342,14 +340,15 @@ def measure_c5(args, rank, world, dev, warmup=2):
         "ms_per_step": round(t_step * 1e3, 3), "steps": steps, "warmup": warmup,
         "workload": (f"C5: {n} fp32 values ({n * 4 / 2 ** 30:.2f} GiB) per rank, quantise "
                      f"({args.wire} wire, k={k}) -> reduce_scatter(int32, SUM) -> "
-                     f"{'dequantise' if args.wire == 'i32' else 'saturate once + dequantise'}"
-                     f" -> all_gather(fp32)"),
+                     + ("dequantise -> all_gather(fp32)" if args.wire == "i32" else
+                        "saturate once -> all_gather(int16 + slot flags) -> dequantise")),
         "values_per_rank": n, "shard_values": agg.plan.shard, "rccl_world": world,
         "phase_ms": {"quantize": round(phase[0] * 1e3, 3), "reduce_scatter": round(phase[1] * 1e3, 3),
-                     "decode": round(phase[2] * 1e3, 3), "all_gather": round(phase[3] * 1e3, 3)},
-        "xgmi": {"rs_send_bytes_per_rank": xgmi, "ag_recv_bytes_per_rank": xgmi,
+                     "decode": round(phase[2] * 1e3, 3), "all_gather": round(phase[3] * 1e3, 3),
+                     "expand": round(phase[4] * 1e3, 3)},
+        "xgmi": {"rs_send_bytes_per_rank": xgmi, "ag_recv_bytes_per_rank": ag,
                  "rs_busbw_GBps": round(xgmi / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None,
-                 "ag_busbw_GBps": round(xgmi / phase[3] / 1e9, 1) if world > 1 and phase[3] > 0 else None},
+                 "ag_busbw_GBps": round(ag / phase[3] / 1e9, 1) if world > 1 and phase[3] > 0 else None},
         "parity_spot_check": parity,
     }
 
@@ -379,21 +378,17 @@ def measure_c5_layout_b(args, rank, world, dev, warmup=2):
         agg(slices)
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     barrier(world)
     ev[0].record(stream)
-    m = agg._reduce(slices)
-    if m:
-        ops.dequantize(agg.sum_shard[:m], k, out=agg.f_shard[:m])
+    m = agg.phase_reduce_decode(slices)
     ev[1].record(stream)
-    from ina_amd.dist import all_gather_shards
-    if world > 1:
-        all_gather_shards(agg.f_shard, agg.plan, agg.group, out=agg.full)
-        if args.wire == "i16":
-            all_gather_shards(agg.ovf_shard, agg.plan, agg.group, out=agg.ovf_full)
+    agg.phase_all_gather()
     ev[2].record(stream)
+    agg.phase_expand()
+    ev[3].record(stream)
     torch.cuda.synchronize()
-    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(2)]
+    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(3)]
     c = min(m, 1 << 16)
     ok = True
     if c:
@@ -409,14 +404,16 @@ def measure_c5_layout_b(args, rank, world, dev, warmup=2):
             _, want, _ = ops.i16_wire_finish(wsum.contiguous(), k, V_SLOT, want_out16=False)
         ok = bool(torch.equal(got, want))
     parity = all_ranks_true(ok, world)
-    ag = (world - 1) * agg.plan.padded * 4 // world
+    ag = agg.gather_bytes
     return {
         "value": round(world * n * 4 * steps / elapsed / 1e9, 2), "unit": "GB/s",
         "ms_per_step": round(elapsed / steps * 1e3, 3),
         "workload": (f"C5 layout B: {world} workers x {n} values, rank r holds every worker's "
                      f"slice of range r ({agg.plan.shard} values each): fused quantise + reduce "
-                     f"({args.wire}) -> dequantise -> all_gather(fp32)"),
-        "phase_ms": {"reduce_decode": round(phase[0] * 1e3, 3), "all_gather": round(phase[1] * 1e3, 3)},
+                     f"({args.wire}) -> " + ("dequantise -> all_gather(fp32)" if args.wire == "i32" else
+                                         "all_gather(int16 + slot flags) -> dequantise")),
+        "phase_ms": {"reduce_decode": round(phase[0] * 1e3, 3), "all_gather": round(phase[1] * 1e3, 3),
+                     "expand": round(phase[2] * 1e3, 3)},
         "xgmi": {"ag_recv_bytes_per_rank": ag,
                  "ag_busbw_GBps": round(ag / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None},
         "parity_spot_check": parity,

@@ -17,13 +17,16 @@ Two wires:
          carries the exact int16 sum and the count of saturating ranks together,
          and the owner saturates once and sets the per-slot overflow flag (the
          ngaa_h overflow bit, headers.p4:30) -- bit-identical to the single-GPU
-         ina_quantize_reduce_f32_i16_sat over the same W buckets.  The flags are
-         all-gathered next to the values.
+         ina_quantize_reduce_f32_i16_sat over the same W buckets.  The all-gather
+         then moves the saturated int16 sums (2 bytes a value, half of fp32's xGMI
+         bytes) and the flags, and every rank dequantises the gathered int16 vector
+         (an HBM pass of 6 bytes a value, cheap next to the xGMI bytes it saves).
 
 Layout B (RangeAggregator): the workers' buckets arrive already split by range -- rank
 r holds every worker's slice of slot range r -- so each rank reduces its W slices
 locally with the fused quantise + reduce kernel (no reduce-scatter), decodes, and one
-all-gather returns the full aggregate; the xGMI traffic is that all-gather alone.
+all-gather returns the full aggregate; the xGMI traffic is that all-gather alone (fp32
+on the i32 wire; the int16 sums + flags, decoded after the gather, on the i16 wire).
 
 Shards are contiguous slot ranges padded to `align` values (default 1024 values =
 4 KiB, rounded up to a whole number of V-value slots), so no slot straddles two
@@ -92,6 +95,11 @@ def all_gather_shards(shard: torch.Tensor, plan: ShardPlan, group=None, out=None
         dist.all_gather_into_tensor(h, shard.contiguous().cpu().view(torch.uint8), group=group)
         out.copy_(h.view(out.dtype).view(out.shape))
         return out
+    if shard.dtype == torch.int16:
+        # RCCL has no int16 type; a gather only moves bytes, so int16 goes as its uint8 view
+        dist.all_gather_into_tensor(out.view(torch.uint8), shard.contiguous().view(torch.uint8),
+                                    group=group)
+        return out
     dist.all_gather_into_tensor(out, shard, group=group)
     return out
 
@@ -127,6 +135,9 @@ class ShardedAggregator:
             self.ovf_shard = torch.empty(self.slots_per_shard, dtype=torch.uint8, device=dev)
             self.ovf_full = torch.empty(self.slots_per_shard * self.world, dtype=torch.uint8,
                                         device=dev)
+            if self.world > 1:        # the gather moves int16 sums, decoded afterwards
+                self.s16_shard = torch.empty(self.plan.shard, dtype=torch.int16, device=dev)
+                self.s16_full = torch.empty(self.plan.padded, dtype=torch.int16, device=dev)
 
     @property
     def overflow(self) -> torch.Tensor:
@@ -134,6 +145,48 @@ class ShardedAggregator:
         if self.wire != "i16":
             raise AttributeError("overflow flags exist only on the i16 wire")
         return self.ovf_full[: -(-self.plan.n // self.V)]
+
+    @property
+    def gather_bytes(self) -> int:
+        """Bytes one all-gather step brings to each rank over xGMI (values + flags)."""
+        if self.world == 1:
+            return 0
+        per = self.plan.shard * (2 if self.wire == "i16" else 4)
+        if self.wire == "i16":
+            per += self.slots_per_shard
+        return (self.world - 1) * per
+
+    # The step's phases, in order (bench.py times each one between HIP events).
+    def phase_quantize(self, grad: torch.Tensor):
+        self._quantize(grad)
+
+    def phase_reduce_scatter(self):
+        if self.world > 1:
+            reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
+
+    def phase_decode(self):
+        """The owner's decode of its shard (one rank: the whole bucket)."""
+        if self.world == 1:
+            self._decode(self.q, self.full, self.ovf_full if self.wire == "i16" else None)
+        elif self.wire == "i32":
+            ops.dequantize(self.sum_shard, self.k, out=self.f_shard)
+        else:
+            ops.i16_wire_finish(self.sum_shard, self.k, self.V, out16=self.s16_shard,
+                                overflow=self.ovf_shard, want_y=False)
+
+    def phase_all_gather(self):
+        if self.world == 1:
+            return
+        if self.wire == "i32":
+            all_gather_shards(self.f_shard, self.plan, self.group, out=self.full)
+        else:
+            all_gather_shards(self.s16_shard, self.plan, self.group, out=self.s16_full)
+            all_gather_shards(self.ovf_shard, self.plan, self.group, out=self.ovf_full)
+
+    def phase_expand(self):
+        """i16 wire at world > 1: dequantise the gathered int16 sums on every rank."""
+        if self.world > 1 and self.wire == "i16":
+            ops.dequantize(self.s16_full, self.k, out=self.full)
 
     def _quantize(self, grad: torch.Tensor):
         n = self.plan.n
@@ -152,19 +205,14 @@ class ShardedAggregator:
             ops.i16_wire_finish(src, self.k, self.V, y=y, overflow=ovf, want_out16=False)
 
     def __call__(self, grad: torch.Tensor) -> torch.Tensor:
-        """fp32 [n] local bucket -> fp32 [n] dequantised sum over all ranks."""
-        n = self.plan.n
-        self._quantize(grad)
-        ovf_full = self.ovf_full if self.wire == "i16" else None
-        if self.world == 1:      # the collectives are identities: quantise -> decode
-            self._decode(self.q, self.full, ovf_full)
-            return self.full[:n]
-        reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
-        self._decode(self.sum_shard, self.f_shard, self.ovf_shard if ovf_full is not None else None)
-        all_gather_shards(self.f_shard, self.plan, self.group, out=self.full)
-        if ovf_full is not None:
-            all_gather_shards(self.ovf_shard, self.plan, self.group, out=ovf_full)
-        return self.full[:n]
+        """fp32 [n] local bucket -> fp32 [n] dequantised sum over all ranks (one rank:
+        the collectives are identities, quantise -> decode)."""
+        self.phase_quantize(grad)
+        self.phase_reduce_scatter()
+        self.phase_decode()
+        self.phase_all_gather()
+        self.phase_expand()
+        return self.full[: self.plan.n]
 
     def aggregate_int(self, grad: torch.Tensor) -> torch.Tensor:
         """fp32 [n] -> this rank's integer shard of the aggregate (no gather): the
@@ -214,6 +262,8 @@ class RangeAggregator:
             self.ovf_shard = torch.zeros(self.slots_per_shard, dtype=torch.uint8, device=dev)
             self.ovf_full = self.ovf_shard if self.world == 1 else torch.empty(
                 self.slots_per_shard * self.world, dtype=torch.uint8, device=dev)
+            if self.world > 1:        # the gather moves the int16 sums, decoded afterwards
+                self.s16_full = torch.empty(self.plan.padded, dtype=torch.int16, device=dev)
 
     @property
     def range(self):
@@ -243,15 +293,43 @@ class RangeAggregator:
                                     overflow=self.ovf_shard[: -(-m // self.V)])
         return m
 
+    @property
+    def gather_bytes(self) -> int:
+        """Bytes the all-gather brings to each rank over xGMI (values + flags)."""
+        if self.world == 1:
+            return 0
+        per = self.plan.shard * (2 if self.wire == "i16" else 4)
+        if self.wire == "i16":
+            per += self.slots_per_shard
+        return (self.world - 1) * per
+
+    # The step's phases, in order (bench.py times each one between HIP events).
+    def phase_reduce_decode(self, slices) -> int:
+        """Local fused quantise + reduce; on the i32 wire (or one rank) also the decode."""
+        m = self._reduce(slices)
+        if m and (self.wire == "i32" or self.world == 1):
+            ops.dequantize(self.sum_shard[:m], self.k, out=self.f_shard[:m])
+        return m
+
+    def phase_all_gather(self):
+        if self.world == 1:
+            return
+        if self.wire == "i32":
+            all_gather_shards(self.f_shard, self.plan, self.group, out=self.full)
+        else:
+            all_gather_shards(self.sum_shard, self.plan, self.group, out=self.s16_full)
+            all_gather_shards(self.ovf_shard, self.plan, self.group, out=self.ovf_full)
+
+    def phase_expand(self):
+        """i16 wire at world > 1: dequantise the gathered int16 sums on every rank."""
+        if self.world > 1 and self.wire == "i16":
+            ops.dequantize(self.s16_full, self.k, out=self.full)
+
     def __call__(self, slices) -> torch.Tensor:
         """W fp32 slices of this rank's range -> fp32 [n] aggregate on every rank."""
-        m = self._reduce(slices)
-        if m:
-            ops.dequantize(self.sum_shard[:m], self.k, out=self.f_shard[:m])
-        if self.world > 1:
-            all_gather_shards(self.f_shard, self.plan, self.group, out=self.full)
-            if self.wire == "i16":
-                all_gather_shards(self.ovf_shard, self.plan, self.group, out=self.ovf_full)
+        self.phase_reduce_decode(slices)
+        self.phase_all_gather()
+        self.phase_expand()
         return self.full[: self.plan.n]
 
     def aggregate_int(self, slices) -> torch.Tensor:

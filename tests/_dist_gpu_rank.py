@@ -58,7 +58,8 @@ def main():
     for _ in range(a.steps):                   # buffers are reused across calls
         full = agg(x)
     torch.cuda.synchronize()
-    res = {"full": full.cpu().numpy(), "world": np.array([world])}
+    res = {"full": full.cpu().numpy(), "world": np.array([world]),
+           "gather_bytes": np.array([agg.gather_bytes, agg.plan.shard])}
     if a.wire == "i16":
         res["ovf"] = agg.overflow.cpu().numpy()
     shard = agg.aggregate_int(x)

@@ -1,7 +1,7 @@
 """One RCCL rank (backend nccl, world size 1), launched by torch.distributed.run from
 tests/test_gpu_dist.py: the collective calls the config-5 path makes at N > 1 --
-reduce_scatter_tensor(int32, SUM), all_gather_into_tensor of fp32 values and uint8
-slot flags, all_reduce(float64, MAX/MIN) of bench.py's max-over-ranks timing -- issued
+reduce_scatter_tensor(int32, SUM), all_gather_into_tensor of fp32 values, int16 sums
+(the i16 wire) and uint8 slot flags, all_reduce(float64, MAX/MIN) of bench.py's max-over-ranks timing -- issued
 through RCCL on this image, with a device-kernel quantise/dequantise around them.  At
 world size 1 every collective is a copy, so results are checked exactly; what this run
 proves is that RCCL initialises with device_id and takes these dtypes and calls here."""
@@ -32,6 +32,11 @@ def main():
     full = torch.empty_like(y)
     dist.all_gather_into_tensor(full, y)
     assert torch.equal(full, ops.dequantize(q, k))
+    s16 = (torch.arange(4096, device=dev, dtype=torch.int32) * 37 - 70000).clamp(-32768, 32767)
+    s16 = s16.to(torch.int16)
+    f16 = torch.empty_like(s16)       # RCCL has no int16: dist.all_gather_shards' uint8 view
+    dist.all_gather_into_tensor(f16.view(torch.uint8), s16.view(torch.uint8))
+    assert torch.equal(f16, s16)
     flags = (torch.arange(4096, device=dev) % 3 == 0).to(torch.uint8)
     fo = torch.empty_like(flags)
     dist.all_gather_into_tensor(fo, flags)

@@ -91,3 +91,6 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
                    "--c5-steps", "2", env={"INA_BENCH_BACKEND": "gloo"}, timeout=400))
     assert d["n_gpus"] == 2 and d["parity_spot_check"] is True
     assert d["layout_b"]["parity_spot_check"] is True
+    shard = d["config"]["shard_values"]          # the i16 wire gathers int16 sums + slot flags
+    assert d["xgmi"]["ag_recv_bytes_per_rank"] == 2 * shard + shard // 256
+    assert d["xgmi"]["rs_send_bytes_per_rank"] == 4 * shard

@@ -52,6 +52,8 @@ def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n):
         assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want_int[lo:hi])
+        gb, shard = (int(v) for v in d["gather_bytes"])      # fp32 aggregate gathered
+        assert gb == (world - 1) * 4 * shard
 
 
 @pytest.mark.gpu
@@ -68,6 +70,8 @@ def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V):
         assert np.array_equal(d["ovf"], want_ovf), f"rank {r}"
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want16[lo:hi])
+        gb, shard = (int(v) for v in d["gather_bytes"])      # int16 sums + flags gathered
+        assert gb == (world - 1) * (2 * shard + shard // V)
 
 
 @pytest.mark.gpu
@@ -85,6 +89,8 @@ def test_range_layout_b_i32_device_kernels(tmp_path, world, n, W):
         assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want_int[lo:hi])
+        gb, shard = (int(v) for v in d["gather_bytes"])      # fp32 aggregate gathered
+        assert gb == (world - 1) * 4 * shard
 
 
 @pytest.mark.gpu
@@ -102,6 +108,8 @@ def test_range_layout_b_i16_device_kernels(tmp_path, world, n, V, W):
         assert np.array_equal(d["ovf"], want_ovf), f"rank {r}"
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want16[lo:hi])
+        gb, shard = (int(v) for v in d["gather_bytes"])      # int16 sums + flags gathered
+        assert gb == (world - 1) * (2 * shard + shard // V)
 
 
 @pytest.mark.gpu
@@ -203,7 +211,7 @@ def test_i16_wire_kernels_vs_oracle(n, V):
 def test_rccl_world1_collectives_on_this_image():
     """The config-5 collectives through RCCL itself (backend nccl, one rank: one GPU
     cannot host two RCCL ranks), so the N > 1 bench's calls -- process group with
-    device_id, reduce_scatter_tensor(int32, SUM), all_gather_into_tensor (fp32, uint8),
+    device_id, reduce_scatter_tensor(int32, SUM), all_gather_into_tensor (fp32, int16, uint8),
     all_reduce(float64, MAX/MIN) -- are known to run on this ROCm/RCCL image."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
