@@ -268,11 +268,12 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
 
 
 # -- config 5: sharded over RCCL --------------------------------------------------------------
-def measure_c5(args, rank, world, dev, warmup=2):
+def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag"):
     """quantise -> reduce_scatter(int32, SUM) -> decode -> all_gather of one n-value fp32
     bucket per rank (the i32 wire gathers fp32; the i16 wire gathers the saturated int16
     sums + slot flags and dequantises after); per-phase HIP-event times on the launch
-    stream."""
+    stream.  collective="allreduce": one all-reduce of the integer wire, every rank
+    decodes the whole bucket (phase "reduce_scatter" is then the all-reduce)."""
     from ina_amd import ops
     from ina_amd.dist import ShardedAggregator, all_gather_shards
     n = args.c5_values
@@ -280,7 +281,7 @@ def measure_c5(args, rank, world, dev, warmup=2):
     g.manual_seed(1000 + rank)
     bucket = torch.randn(n, device=dev, generator=g) * 1e-2
     k = 16 if args.wire == "i32" else 20
-    agg = ShardedAggregator(n, k=k, device=dev, wire=args.wire, V=V_SLOT)
+    agg = ShardedAggregator(n, k=k, device=dev, wire=args.wire, V=V_SLOT, collective=collective)
     for _ in range(warmup):
         agg(bucket)
     steps = args.c5_steps
@@ -339,16 +340,23 @@ def measure_c5(args, rank, world, dev, warmup=2):
         "metric": "aggregated-gradient GB/s (config 5: fp32 bucket per rank, sharded over RCCL)",
         "ms_per_step": round(t_step * 1e3, 3), "steps": steps, "warmup": warmup,
         "workload": (f"C5: {n} fp32 values ({n * 4 / 2 ** 30:.2f} GiB) per rank, quantise "
-                     f"({args.wire} wire, k={k}) -> reduce_scatter(int32, SUM) -> "
-                     + ("dequantise -> all_gather(fp32)" if args.wire == "i32" else
-                        "saturate once -> all_gather(int16 + slot flags) -> dequantise")),
+                     f"({args.wire} wire, k={k}) -> "
+                     + ("all_reduce(int32, SUM) -> decode the whole bucket on every rank"
+                        if collective == "allreduce" else
+                        "reduce_scatter(int32, SUM) -> "
+                        + ("dequantise -> all_gather(fp32)" if args.wire == "i32" else
+                           "saturate once -> all_gather(int16 + slot flags) -> dequantise"))),
         "values_per_rank": n, "shard_values": agg.plan.shard, "rccl_world": world,
+        "collective": collective,
         "phase_ms": {"quantize": round(phase[0] * 1e3, 3), "reduce_scatter": round(phase[1] * 1e3, 3),
                      "decode": round(phase[2] * 1e3, 3), "all_gather": round(phase[3] * 1e3, 3),
                      "expand": round(phase[4] * 1e3, 3)},
-        "xgmi": {"rs_send_bytes_per_rank": xgmi, "ag_recv_bytes_per_rank": ag,
-                 "rs_busbw_GBps": round(xgmi / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None,
-                 "ag_busbw_GBps": round(ag / phase[3] / 1e9, 1) if world > 1 and phase[3] > 0 else None},
+        "xgmi": ({"rs_send_bytes_per_rank": xgmi, "ag_recv_bytes_per_rank": ag,
+                  "rs_busbw_GBps": round(xgmi / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None,
+                  "ag_busbw_GBps": round(ag / phase[3] / 1e9, 1) if world > 1 and phase[3] > 0 else None}
+                 if collective == "rs_ag" else
+                 {"allreduce_bytes_per_rank": 2 * xgmi,     # nccl-tests busbw: 2(G-1)/G x S / t
+                  "allreduce_busbw_GBps": round(2 * xgmi / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None}),
         "parity_spot_check": parity,
     }
 
@@ -510,6 +518,10 @@ def run_sharded_headline(args, rank, world, dev, backend):
     c5 = measure_c5(args, rank, world, dev)
     torch.cuda.empty_cache()
     c5_b = measure_c5_layout_b(args, rank, world, dev)
+    c5_ar = None
+    if world > 1:
+        torch.cuda.empty_cache()
+        c5_ar = measure_c5(args, rank, world, dev, collective="allreduce")
     return {
         "metric": c5["metric"], "value": c5["value"], "unit": "GB/s",
         "n_gpus": world, "steps": c5["steps"], "warmup": c5["warmup"],
@@ -522,6 +534,7 @@ def run_sharded_headline(args, rank, world, dev, backend):
         "phase_ms": c5["phase_ms"], "xgmi": c5["xgmi"],
         "parity_spot_check": c5["parity_spot_check"],
         "layout_b": c5_b,
+        "allreduce": c5_ar,
     }
 
 
@@ -605,6 +618,9 @@ def run_reduce(args, rank, world, dev, backend):
         line["sharded_c5"] = measure_c5(args, rank, world, dev)
         torch.cuda.empty_cache()
         line["sharded_c5"]["layout_b"] = measure_c5_layout_b(args, rank, world, dev)
+        if world > 1:
+            torch.cuda.empty_cache()
+            line["sharded_c5"]["allreduce"] = measure_c5(args, rank, world, dev, collective="allreduce")
     if not args.no_switch:
         line["switch_c3"] = measure_switch(dev, rank=rank, world=world)
     return line

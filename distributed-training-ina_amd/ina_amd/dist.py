@@ -81,6 +81,20 @@ def reduce_scatter_sum(x_padded: torch.Tensor, plan: ShardPlan, group=None, out=
     return out
 
 
+def all_reduce_sum(x: torch.Tensor, group=None):
+    """int32 in place -> the element-wise sum over ranks (RCCL all-reduce; host-staged
+    with gloo and device tensors)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return x
+    if x.is_cuda and _host_staged(group):
+        h = x.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        x.copy_(h)
+        return x
+    dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group)
+    return x
+
+
 def all_gather_shards(shard: torch.Tensor, plan: ShardPlan, group=None, out=None):
     """[count] per rank -> [world * count] (count = plan.shard values, or its slot flags)."""
     out = torch.empty(plan.world * shard.numel(), dtype=shard.dtype, device=shard.device) \
@@ -110,12 +124,20 @@ class ShardedAggregator:
     wire="i32": __call__ returns the dequantised fp32 sum over ranks.
     wire="i16": the same from the int16 saturating path; `overflow` then holds the
     per-slot flags (ceil(n / V) bytes) of the last call.
+    collective="rs_ag" (default): reduce-scatter the integer wire, the owner decodes its
+    shard, all-gather.  collective="allreduce": one RCCL all-reduce of the integer wire
+    (the same (G-1)/G bytes each way per rank inside one collective) and every rank
+    decodes the whole bucket.  Both give the same bits; which one xGMI runs faster is
+    measured by bench.py at N > 1 (sharded_c5 / sharded_c5.allreduce).
     """
 
     def __init__(self, n: int, k: int = 16, group=None, device=None, align: int = 1024,
-                 wire: str = "i32", V: int = 256):
+                 wire: str = "i32", V: int = 256, collective: str = "rs_ag"):
         if wire not in ("i32", "i16"):
             raise ValueError("wire must be 'i32' or 'i16'")
+        if collective not in ("rs_ag", "allreduce"):
+            raise ValueError("collective must be 'rs_ag' or 'allreduce'")
+        self.collective = collective
         if V <= 0:
             raise ValueError("V must be > 0")
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -135,7 +157,7 @@ class ShardedAggregator:
             self.ovf_shard = torch.empty(self.slots_per_shard, dtype=torch.uint8, device=dev)
             self.ovf_full = torch.empty(self.slots_per_shard * self.world, dtype=torch.uint8,
                                         device=dev)
-            if self.world > 1:        # the gather moves int16 sums, decoded afterwards
+            if self.world > 1 and collective == "rs_ag":   # gather int16 sums, decode after
                 self.s16_shard = torch.empty(self.plan.shard, dtype=torch.int16, device=dev)
                 self.s16_full = torch.empty(self.plan.padded, dtype=torch.int16, device=dev)
 
@@ -148,9 +170,12 @@ class ShardedAggregator:
 
     @property
     def gather_bytes(self) -> int:
-        """Bytes one all-gather step brings to each rank over xGMI (values + flags)."""
+        """Bytes one all-gather step brings to each rank over xGMI (values + flags);
+        with collective="allreduce" the all-reduce's gather half (int32 wire words)."""
         if self.world == 1:
             return 0
+        if self.collective == "allreduce":
+            return (self.world - 1) * self.plan.shard * 4
         per = self.plan.shard * (2 if self.wire == "i16" else 4)
         if self.wire == "i16":
             per += self.slots_per_shard
@@ -161,12 +186,18 @@ class ShardedAggregator:
         self._quantize(grad)
 
     def phase_reduce_scatter(self):
-        if self.world > 1:
+        """The integer collective: reduce-scatter, or the whole all-reduce."""
+        if self.world == 1:
+            return
+        if self.collective == "allreduce":
+            all_reduce_sum(self.q, self.group)
+        else:
             reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
 
     def phase_decode(self):
-        """The owner's decode of its shard (one rank: the whole bucket)."""
-        if self.world == 1:
+        """The owner's decode of its shard (one rank, or after an all-reduce: the whole
+        bucket on every rank)."""
+        if self.world == 1 or self.collective == "allreduce":
             self._decode(self.q, self.full, self.ovf_full if self.wire == "i16" else None)
         elif self.wire == "i32":
             ops.dequantize(self.sum_shard, self.k, out=self.f_shard)
@@ -175,7 +206,7 @@ class ShardedAggregator:
                                 overflow=self.ovf_shard, want_y=False)
 
     def phase_all_gather(self):
-        if self.world == 1:
+        if self.world == 1 or self.collective == "allreduce":
             return
         if self.wire == "i32":
             all_gather_shards(self.f_shard, self.plan, self.group, out=self.full)
@@ -185,7 +216,7 @@ class ShardedAggregator:
 
     def phase_expand(self):
         """i16 wire at world > 1: dequantise the gathered int16 sums on every rank."""
-        if self.world > 1 and self.wire == "i16":
+        if self.world > 1 and self.wire == "i16" and self.collective == "rs_ag":
             ops.dequantize(self.s16_full, self.k, out=self.full)
 
     def _quantize(self, grad: torch.Tensor):

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--layout", choices=("A", "B"), default="A")
     ap.add_argument("--workers", type=int, default=0, help="layout B: W buckets (default: world)")
+    ap.add_argument("--collective", choices=("rs_ag", "allreduce"), default="rs_ag")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -49,7 +50,8 @@ def main():
     dev = torch.device("cuda", 0)
     if a.layout == "A":
         x = torch.from_numpy(bucket(rank, a.size, a.wire)).to(dev)
-        agg = ShardedAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V)
+        agg = ShardedAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V,
+                                collective=a.collective)
     else:                                      # every worker's slice of this rank's range
         agg = RangeAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V)
         lo, hi = agg.range

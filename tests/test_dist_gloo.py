@@ -28,7 +28,7 @@ def _worker(rank, world, port, n, k, results):
     for p in (REPO, PKG_ROOT):
         if p not in sys.path:
             sys.path.insert(0, p)
-    from ina_amd.dist import ShardPlan, all_gather_shards, reduce_scatter_sum
+    from ina_amd.dist import ShardPlan, all_gather_shards, all_reduce_sum, reduce_scatter_sum
     from oracle import oracle as orc
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -41,7 +41,9 @@ def _worker(rank, world, port, n, k, results):
         qp[:n] = torch.from_numpy(q)
         shard = reduce_scatter_sum(qp, plan)
         full = all_gather_shards(shard, plan)
-        results[rank] = (shard.numpy().copy(), full[:n].numpy().copy(), plan.range_of(rank))
+        ar = all_reduce_sum(qp.clone())              # the collective="allreduce" variant
+        results[rank] = (shard.numpy().copy(), full[:n].numpy().copy(), plan.range_of(rank),
+                         ar[:n].numpy().copy())
     finally:
         dist.destroy_process_group()
 
@@ -57,8 +59,9 @@ def test_sharded_integer_aggregate_gloo(world, n):
                            .astype(np.float32), k) for r in range(world)]
     want = orc.sum_reduce_i32(qs)
     for r in range(world):
-        shard, full, (lo, hi) = results[r]
+        shard, full, (lo, hi), ar = results[r]
         assert np.array_equal(full, want)
+        assert np.array_equal(ar, want)
         assert np.array_equal(shard[: hi - lo], want[lo:hi])
         assert not shard[hi - lo:].any()        # padding stays zero
 
@@ -80,7 +83,7 @@ def _worker_i16(rank, world, port, n, k, V, results):
         if p not in sys.path:
             sys.path.insert(0, p)
     import math
-    from ina_amd.dist import ShardPlan, all_gather_shards, reduce_scatter_sum
+    from ina_amd.dist import ShardPlan, all_gather_shards, all_reduce_sum, reduce_scatter_sum
     from oracle import oracle as orc
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -166,3 +169,6 @@ def test_range_aggregator_host_checks():
     assert a16.plan.shard % 100 == 0 and a16.ovf_shard.numel() == a16.plan.shard // 100
     with pytest.raises(AttributeError):
         _ = agg.overflow
+    from ina_amd.dist import ShardedAggregator
+    with pytest.raises(ValueError):
+        ShardedAggregator(10, device=torch.device("cpu"), collective="tree")

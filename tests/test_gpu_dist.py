@@ -28,22 +28,23 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(tmp_path, world, n, wire, k, V=256, layout="A", workers=0):
+def _run_ranks(tmp_path, world, n, wire, k, V=256, layout="A", workers=0, collective="rs_ag"):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", RANK_SCRIPT,
            "--size", str(n), "--wire", wire, "--k", str(k), "--V", str(V), "--out", str(tmp_path),
-           "--layout", layout, "--workers", str(workers)]
+           "--layout", layout, "--workers", str(workers), "--collective", collective]
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     return [dict(np.load(os.path.join(tmp_path, f"rank{i}.npz"))) for i in range(world)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n", [(2, 1_000_003), (3, 70_001), (2, 1), (8, 400_001)])
-def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n):
+@pytest.mark.parametrize("world,n,coll", [(2, 1_000_003, "rs_ag"), (3, 70_001, "rs_ag"), (2, 1, "rs_ag"),
+                                          (8, 400_001, "rs_ag"), (3, 70_001, "allreduce")])
+def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n, coll):
     from oracle import oracle as orc
     k = 20
-    res = _run_ranks(tmp_path, world, n, "i32", k)
+    res = _run_ranks(tmp_path, world, n, "i32", k, collective=coll)
     want_int = orc.quantize_reduce_i32([bucket(r, n, "i32") for r in range(world)], k)
     want = orc.dequantize_i32(want_int, k)
     for r, d in enumerate(res):
@@ -52,16 +53,18 @@ def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n):
         assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want_int[lo:hi])
-        gb, shard = (int(v) for v in d["gather_bytes"])      # fp32 aggregate gathered
+        gb, shard = (int(v) for v in d["gather_bytes"])      # fp32 aggregate (or int32 wire) gathered
         assert gb == (world - 1) * 4 * shard
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n,V", [(2, 1_000_003, 256), (3, 50_000, 32), (2, 300, 100), (8, 200_000, 32)])
-def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V):
+@pytest.mark.parametrize("world,n,V,coll", [(2, 1_000_003, 256, "rs_ag"), (3, 50_000, 32, "rs_ag"),
+                                            (2, 300, 100, "rs_ag"), (8, 200_000, 32, "rs_ag"),
+                                            (3, 50_000, 32, "allreduce")])
+def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V, coll):
     from oracle import oracle as orc
     k = 11
-    res = _run_ranks(tmp_path, world, n, "i16", k, V)
+    res = _run_ranks(tmp_path, world, n, "i16", k, V, collective=coll)
     want16, want_ovf = orc.quantize_reduce_i16_sat([bucket(r, n, "i16") for r in range(world)], k, V)
     assert want_ovf.any() and not want_ovf.all()
     want = orc.dequantize_i16(want16, k)
@@ -71,7 +74,7 @@ def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V):
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want16[lo:hi])
         gb, shard = (int(v) for v in d["gather_bytes"])      # int16 sums + flags gathered
-        assert gb == (world - 1) * (2 * shard + shard // V)
+        assert gb == (world - 1) * (2 * shard + shard // V if coll == "rs_ag" else 4 * shard)
 
 
 @pytest.mark.gpu
