@@ -60,6 +60,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 W_WORKERS = 8
 N_VALUES = 26_214_400        # 100 MiB of int32 per worker (config 3)
 C5_VALUES = 268_435_456      # 1 GiB of fp32 per worker (config 5)
+C5_CHUNKS = 4                # pipelined config-5 variant at N > 1: 256 MiB chunks
 V_SLOT = 256
 ROTATE = 2                   # input sets alternated per step (943 MB each > 256 MB MALL)
 
@@ -268,12 +269,14 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
 
 
 # -- config 5: sharded over RCCL --------------------------------------------------------------
-def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag"):
+def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag", chunks=1):
     """quantise -> reduce_scatter(int32, SUM) -> decode -> all_gather of one n-value fp32
     bucket per rank (the i32 wire gathers fp32; the i16 wire gathers the saturated int16
     sums + slot flags and dequantises after); per-phase HIP-event times on the launch
     stream.  collective="allreduce": one all-reduce of the integer wire, every rank
-    decodes the whole bucket (phase "reduce_scatter" is then the all-reduce)."""
+    decodes the whole bucket (phase "reduce_scatter" is then the all-reduce).
+    chunks > 1: the pipelined step (ShardedAggregator(chunks=C)); its phases overlap, so
+    only the step time is reported."""
     from ina_amd import ops
     from ina_amd.dist import ShardedAggregator, all_gather_shards
     n = args.c5_values
@@ -281,7 +284,8 @@ def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag"):
     g.manual_seed(1000 + rank)
     bucket = torch.randn(n, device=dev, generator=g) * 1e-2
     k = 16 if args.wire == "i32" else 20
-    agg = ShardedAggregator(n, k=k, device=dev, wire=args.wire, V=V_SLOT, collective=collective)
+    agg = ShardedAggregator(n, k=k, device=dev, wire=args.wire, V=V_SLOT, collective=collective,
+                            chunks=chunks)
     for _ in range(warmup):
         agg(bucket)
     steps = args.c5_steps
@@ -294,21 +298,23 @@ def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag"):
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
 
     # per-phase breakdown (one more pass, events between the aggregator's own phases)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    barrier(world)
-    ev[0].record(stream)
-    agg.phase_quantize(bucket)
-    ev[1].record(stream)
-    agg.phase_reduce_scatter()
-    ev[2].record(stream)
-    agg.phase_decode()
-    ev[3].record(stream)
-    agg.phase_all_gather()
-    ev[4].record(stream)
-    agg.phase_expand()
-    ev[5].record(stream)
-    torch.cuda.synchronize()
-    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(5)]
+    phase = None
+    if agg.chunks == 1:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        barrier(world)
+        ev[0].record(stream)
+        agg.phase_quantize(bucket)
+        ev[1].record(stream)
+        agg.phase_reduce_scatter()
+        ev[2].record(stream)
+        agg.phase_decode()
+        ev[3].record(stream)
+        agg.phase_all_gather()
+        ev[4].record(stream)
+        agg.phase_expand()
+        ev[5].record(stream)
+        torch.cuda.synchronize()
+        phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(5)]
 
     # parity: the aggregate's first 64 Ki values == decode(sum over ranks of the
     # per-rank wire of those values), the per-rank wires all-gathered
@@ -335,6 +341,18 @@ def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag"):
     xgmi = (G - 1) * S // G                # int32 wire words reduce-scattered
     ag = agg.gather_bytes                  # fp32 (i32 wire) or int16 + flags (i16 wire)
     t_step = elapsed / steps
+    if phase is None:                      # pipelined: the step time and its bytes only
+        rs = (G - 1) * agg.chunks * agg.sc * 4
+        return {
+            "value": round(world * n * 4 * steps / elapsed / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(t_step * 1e3, 3), "steps": steps, "warmup": warmup,
+            "workload": (f"C5 pipelined: the same step in {agg.chunks} chunks, chunk c+1's "
+                         f"quantise under chunk c's reduce_scatter (async RCCL work)"),
+            "collective": collective, "chunks": agg.chunks,
+            "xgmi": {"rs_send_bytes_per_rank": rs, "ag_recv_bytes_per_rank": ag,
+                     "busbw_GBps": round((rs + ag) / t_step / 1e9, 1) if world > 1 else None},
+            "parity_spot_check": parity,
+        }
     return {
         "value": round(world * n * 4 * steps / elapsed / 1e9, 2), "unit": "GB/s",
         "metric": "aggregated-gradient GB/s (config 5: fp32 bucket per rank, sharded over RCCL)",
@@ -518,10 +536,12 @@ def run_sharded_headline(args, rank, world, dev, backend):
     c5 = measure_c5(args, rank, world, dev)
     torch.cuda.empty_cache()
     c5_b = measure_c5_layout_b(args, rank, world, dev)
-    c5_ar = None
+    c5_ar = c5_pl = None
     if world > 1:
         torch.cuda.empty_cache()
         c5_ar = measure_c5(args, rank, world, dev, collective="allreduce")
+        torch.cuda.empty_cache()
+        c5_pl = measure_c5(args, rank, world, dev, chunks=C5_CHUNKS)
     return {
         "metric": c5["metric"], "value": c5["value"], "unit": "GB/s",
         "n_gpus": world, "steps": c5["steps"], "warmup": c5["warmup"],
@@ -535,6 +555,7 @@ def run_sharded_headline(args, rank, world, dev, backend):
         "parity_spot_check": c5["parity_spot_check"],
         "layout_b": c5_b,
         "allreduce": c5_ar,
+        "pipelined": c5_pl,
     }
 
 
@@ -621,6 +642,8 @@ def run_reduce(args, rank, world, dev, backend):
         if world > 1:
             torch.cuda.empty_cache()
             line["sharded_c5"]["allreduce"] = measure_c5(args, rank, world, dev, collective="allreduce")
+            torch.cuda.empty_cache()
+            line["sharded_c5"]["pipelined"] = measure_c5(args, rank, world, dev, chunks=C5_CHUNKS)
     if not args.no_switch:
         line["switch_c3"] = measure_switch(dev, rank=rank, world=world)
     return line

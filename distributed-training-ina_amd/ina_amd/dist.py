@@ -64,21 +64,26 @@ def _host_staged(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
-def reduce_scatter_sum(x_padded: torch.Tensor, plan: ShardPlan, group=None, out=None):
-    """int32 [padded] -> this rank's [shard] of the element-wise sum over ranks."""
+def reduce_scatter_sum(x_padded: torch.Tensor, plan: ShardPlan, group=None, out=None,
+                       async_op: bool = False):
+    """int32 [padded] -> this rank's [shard] of the element-wise sum over ranks.  With
+    async_op the RCCL work handle is returned as well ((out, work); work is None when
+    the call completed synchronously): the collective runs on RCCL's stream and the
+    caller's stream waits for it only at work.wait()."""
     if x_padded.numel() != plan.padded:
         raise ValueError("input must be padded to plan.padded")
     out = torch.empty(plan.shard, dtype=x_padded.dtype, device=x_padded.device) if out is None else out
+    work = None
     if plan.world == 1:
         out.copy_(x_padded)
-        return out
-    if x_padded.is_cuda and _host_staged(group):
+    elif x_padded.is_cuda and _host_staged(group):
         h = torch.empty(plan.shard, dtype=x_padded.dtype)
         dist.reduce_scatter_tensor(h, x_padded.cpu(), op=dist.ReduceOp.SUM, group=group)
         out.copy_(h)
-        return out
-    dist.reduce_scatter_tensor(out, x_padded, op=dist.ReduceOp.SUM, group=group)
-    return out
+    else:
+        work = dist.reduce_scatter_tensor(out, x_padded, op=dist.ReduceOp.SUM, group=group,
+                                          async_op=async_op)
+    return (out, work) if async_op else out
 
 
 def all_reduce_sum(x: torch.Tensor, group=None):
@@ -95,27 +100,33 @@ def all_reduce_sum(x: torch.Tensor, group=None):
     return x
 
 
-def all_gather_shards(shard: torch.Tensor, plan: ShardPlan, group=None, out=None):
-    """[count] per rank -> [world * count] (count = plan.shard values, or its slot flags)."""
+def all_gather_shards(shard: torch.Tensor, plan: ShardPlan, group=None, out=None,
+                      async_op: bool = False):
+    """[count] per rank -> [world * count] (count = plan.shard values, or its slot flags).
+    async_op: returns (out, work) as reduce_scatter_sum does."""
     out = torch.empty(plan.world * shard.numel(), dtype=shard.dtype, device=shard.device) \
         if out is None else out
+    work = None
     if plan.world == 1:
         out.copy_(shard)
-        return out
-    if _host_staged(group):
+    elif _host_staged(group):
         # gloo gathers bytes: an all-gather only moves data, so any dtype (gloo has no
         # int16) goes through as its uint8 view, bit for bit
         h = torch.empty(out.numel() * out.element_size(), dtype=torch.uint8)
         dist.all_gather_into_tensor(h, shard.contiguous().cpu().view(torch.uint8), group=group)
         out.copy_(h.view(out.dtype).view(out.shape))
-        return out
-    if shard.dtype == torch.int16:
+    elif shard.dtype == torch.int16:
         # RCCL has no int16 type; a gather only moves bytes, so int16 goes as its uint8 view
-        dist.all_gather_into_tensor(out.view(torch.uint8), shard.contiguous().view(torch.uint8),
-                                    group=group)
-        return out
-    dist.all_gather_into_tensor(out, shard, group=group)
-    return out
+        work = dist.all_gather_into_tensor(out.view(torch.uint8), shard.contiguous().view(torch.uint8),
+                                           group=group, async_op=async_op)
+    else:
+        work = dist.all_gather_into_tensor(out, shard, group=group, async_op=async_op)
+    return (out, work) if async_op else out
+
+
+def _wait(work):
+    if work is not None:
+        work.wait()          # the caller's stream waits for RCCL's; the host does not block
 
 
 class ShardedAggregator:
@@ -129,14 +140,20 @@ class ShardedAggregator:
     (the same (G-1)/G bytes each way per rank inside one collective) and every rank
     decodes the whole bucket.  Both give the same bits; which one xGMI runs faster is
     measured by bench.py at N > 1 (sharded_c5 / sharded_c5.allreduce).
+    chunks=C > 1 (rs_ag, world > 1): the bucket is cut into C contiguous chunks, each
+    reduce-scattered and all-gathered on its own (async RCCL work), so chunk c+1's
+    quantise runs under chunk c's reduce-scatter and the decodes under the later
+    collectives; same bits (integer sums are order-free, the decode is elementwise).
     """
 
     def __init__(self, n: int, k: int = 16, group=None, device=None, align: int = 1024,
-                 wire: str = "i32", V: int = 256, collective: str = "rs_ag"):
+                 wire: str = "i32", V: int = 256, collective: str = "rs_ag", chunks: int = 1):
         if wire not in ("i32", "i16"):
             raise ValueError("wire must be 'i32' or 'i16'")
         if collective not in ("rs_ag", "allreduce"):
             raise ValueError("collective must be 'rs_ag' or 'allreduce'")
+        if chunks < 1 or (chunks > 1 and collective != "rs_ag"):
+            raise ValueError("chunks must be >= 1, and > 1 only with collective='rs_ag'")
         self.collective = collective
         if V <= 0:
             raise ValueError("V must be > 0")
@@ -148,25 +165,45 @@ class ShardedAggregator:
         self.plan = ShardPlan(n, self.world, align)
         self.k, self.group, self.wire, self.V = k, group, wire, V
         dev = device or torch.device("cuda", torch.cuda.current_device())
-        self.q = torch.zeros(self.plan.padded, dtype=torch.int32, device=dev)   # pad stays 0
+        self.chunks = chunks if self.world > 1 else 1
+        tot = self.plan.padded
+        if self.chunks > 1:
+            # chunk c = values [c*L, (c+1)*L), L = world * Sc; rank r owns [c*L + r*Sc, +Sc)
+            sc = -(-n // (self.world * self.chunks)) if n else 0
+            self.sc = max(-(-sc // align) * align, align)
+            self.cplan = ShardPlan(self.world * self.sc, self.world, align=self.sc)
+            self.cpad = self.chunks * self.cplan.padded
+            tot = max(tot, self.cpad)
+        # one allocation backs both the whole-bucket and the chunked views; pad stays 0
+        self._qbuf = torch.zeros(tot, dtype=torch.int32, device=dev)
+        self._fbuf = torch.empty(tot, dtype=torch.float32, device=dev)
+        self.q, self.full = self._qbuf[: self.plan.padded], self._fbuf[: self.plan.padded]
         self.sum_shard = torch.empty(self.plan.shard, dtype=torch.int32, device=dev)
         self.f_shard = torch.empty(self.plan.shard, dtype=torch.float32, device=dev)
-        self.full = torch.empty(self.plan.padded, dtype=torch.float32, device=dev)
         if wire == "i16":
             self.slots_per_shard = self.plan.shard // V
             self.ovf_shard = torch.empty(self.slots_per_shard, dtype=torch.uint8, device=dev)
-            self.ovf_full = torch.empty(self.slots_per_shard * self.world, dtype=torch.uint8,
-                                        device=dev)
+            self._obuf = torch.zeros(tot // V, dtype=torch.uint8, device=dev)
+            self.ovf_full = self._obuf[: self.slots_per_shard * self.world]
             if self.world > 1 and collective == "rs_ag":   # gather int16 sums, decode after
                 self.s16_shard = torch.empty(self.plan.shard, dtype=torch.int16, device=dev)
-                self.s16_full = torch.empty(self.plan.padded, dtype=torch.int16, device=dev)
+                self._s16buf = torch.empty(tot, dtype=torch.int16, device=dev)
+                self.s16_full = self._s16buf[: self.plan.padded]
+        if self.chunks > 1:
+            m = self.chunks * self.sc
+            self.sum_c = torch.empty(m, dtype=torch.int32, device=dev)
+            if wire == "i32":
+                self.f_c = torch.empty(m, dtype=torch.float32, device=dev)
+            else:
+                self.s16_c = torch.empty(m, dtype=torch.int16, device=dev)
+                self.ovf_c = torch.empty(m // V, dtype=torch.uint8, device=dev)
 
     @property
     def overflow(self) -> torch.Tensor:
         """Per-slot overflow flags of the last i16 aggregation (ceil(n / V) bytes)."""
         if self.wire != "i16":
             raise AttributeError("overflow flags exist only on the i16 wire")
-        return self.ovf_full[: -(-self.plan.n // self.V)]
+        return self._obuf[: -(-self.plan.n // self.V)]
 
     @property
     def gather_bytes(self) -> int:
@@ -174,11 +211,12 @@ class ShardedAggregator:
         with collective="allreduce" the all-reduce's gather half (int32 wire words)."""
         if self.world == 1:
             return 0
+        shard = self.chunks * self.sc if self.chunks > 1 else self.plan.shard
         if self.collective == "allreduce":
-            return (self.world - 1) * self.plan.shard * 4
-        per = self.plan.shard * (2 if self.wire == "i16" else 4)
+            return (self.world - 1) * shard * 4
+        per = shard * (2 if self.wire == "i16" else 4)
         if self.wire == "i16":
-            per += self.slots_per_shard
+            per += shard // self.V
         return (self.world - 1) * per
 
     # The step's phases, in order (bench.py times each one between HIP events).
@@ -235,9 +273,48 @@ class ShardedAggregator:
         else:
             ops.i16_wire_finish(src, self.k, self.V, y=y, overflow=ovf, want_out16=False)
 
+    def _call_chunked(self, grad: torch.Tensor) -> torch.Tensor:
+        n, L, sc, V = self.plan.n, self.cplan.padded, self.sc, self.V
+        if grad.numel() != n:
+            raise ValueError("bucket size changed")
+        x = grad.reshape(-1)
+        rs = []
+        for c in range(self.chunks):           # quantise chunk c, then its RS on RCCL's stream
+            lo, hi = c * L, min((c + 1) * L, n)
+            if hi > lo:
+                if self.wire == "i32":
+                    ops.quantize(x[lo:hi], self.k, out=self._qbuf[lo:hi])
+                else:
+                    ops.quantize_i16_wire(x[lo:hi], self.k, out=self._qbuf[lo:hi])
+            rs.append(reduce_scatter_sum(self._qbuf[c * L:(c + 1) * L], self.cplan, self.group,
+                                         out=self.sum_c[c * sc:(c + 1) * sc], async_op=True)[1])
+        ag = []
+        for c in range(self.chunks):           # decode shard c once its RS is done, gather it
+            _wait(rs[c])
+            part = self.sum_c[c * sc:(c + 1) * sc]
+            if self.wire == "i32":
+                ops.dequantize(part, self.k, out=self.f_c[c * sc:(c + 1) * sc])
+                ag.append(all_gather_shards(self.f_c[c * sc:(c + 1) * sc], self.cplan, self.group,
+                                            out=self._fbuf[c * L:(c + 1) * L], async_op=True)[1])
+            else:
+                o16 = self.s16_c[c * sc:(c + 1) * sc]
+                of = self.ovf_c[c * sc // V:(c + 1) * sc // V]
+                ops.i16_wire_finish(part, self.k, V, out16=o16, overflow=of, want_y=False)
+                ag.append(all_gather_shards(o16, self.cplan, self.group,
+                                            out=self._s16buf[c * L:(c + 1) * L], async_op=True)[1])
+                ag.append(all_gather_shards(of, self.cplan, self.group,
+                                            out=self._obuf[c * L // V:(c + 1) * L // V], async_op=True)[1])
+        for w in ag:
+            _wait(w)
+        if self.wire == "i16":
+            ops.dequantize(self._s16buf[: self.cpad], self.k, out=self._fbuf[: self.cpad])
+        return self._fbuf[:n]
+
     def __call__(self, grad: torch.Tensor) -> torch.Tensor:
         """fp32 [n] local bucket -> fp32 [n] dequantised sum over all ranks (one rank:
         the collectives are identities, quantise -> decode)."""
+        if self.chunks > 1:
+            return self._call_chunked(grad)
         self.phase_quantize(grad)
         self.phase_reduce_scatter()
         self.phase_decode()

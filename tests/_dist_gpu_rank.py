@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--layout", choices=("A", "B"), default="A")
     ap.add_argument("--workers", type=int, default=0, help="layout B: W buckets (default: world)")
     ap.add_argument("--collective", choices=("rs_ag", "allreduce"), default="rs_ag")
+    ap.add_argument("--chunks", type=int, default=1)
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -51,7 +52,7 @@ def main():
     if a.layout == "A":
         x = torch.from_numpy(bucket(rank, a.size, a.wire)).to(dev)
         agg = ShardedAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V,
-                                collective=a.collective)
+                                collective=a.collective, chunks=a.chunks)
     else:                                      # every worker's slice of this rank's range
         agg = RangeAggregator(a.size, k=a.k, device=dev, wire=a.wire, V=a.V)
         lo, hi = agg.range
@@ -61,7 +62,8 @@ def main():
         full = agg(x)
     torch.cuda.synchronize()
     res = {"full": full.cpu().numpy(), "world": np.array([world]),
-           "gather_bytes": np.array([agg.gather_bytes, agg.plan.shard])}
+           "gather_bytes": np.array([agg.gather_bytes, agg.plan.shard if getattr(agg, "chunks", 1) == 1
+                                     else agg.chunks * agg.sc])}
     if a.wire == "i16":
         res["ovf"] = agg.overflow.cpu().numpy()
     shard = agg.aggregate_int(x)

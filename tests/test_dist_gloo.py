@@ -172,3 +172,7 @@ def test_range_aggregator_host_checks():
     from ina_amd.dist import ShardedAggregator
     with pytest.raises(ValueError):
         ShardedAggregator(10, device=torch.device("cpu"), collective="tree")
+    with pytest.raises(ValueError):             # chunks pipeline the RS + AG pair only
+        ShardedAggregator(10, device=torch.device("cpu"), collective="allreduce", chunks=2)
+    one = ShardedAggregator(5000, device=torch.device("cpu"), chunks=4)
+    assert one.chunks == 1 and one.gather_bytes == 0      # one rank: nothing to pipeline

@@ -53,7 +53,7 @@ def test_bench_json_line_contract():
     c5 = d["sharded_c5"]
     assert c5["parity_spot_check"] is True and c5["rccl_world"] == 1 and c5["values_per_rank"] == 1 << 22
     assert c5["layout_b"]["parity_spot_check"] is True and c5["layout_b"]["value"] > 0
-    assert "allreduce" not in c5                 # one rank: no collective to compare
+    assert "allreduce" not in c5 and "pipelined" not in c5   # one rank: no collective to compare
     sw = d["switch_c3"]                          # the packet-stream switch, measured live
     assert sw["algorithmic_bytes"] == 819_200 * 1040 + 102_400 * (1040 + 1029) + 819_200
     for order in ("worker_major", "round_robin"):
@@ -88,6 +88,8 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     ar = c5["allreduce"]                         # the one-collective variant, same bits
     assert ar["collective"] == "allreduce" and ar["parity_spot_check"] is True
     assert ar["xgmi"]["allreduce_bytes_per_rank"] == 2 * c5["shard_values"] * 4
+    pl = c5["pipelined"]                         # chunked, async RCCL work, same bits
+    assert pl["chunks"] > 1 and pl["parity_spot_check"] is True
     sw = d["switch_c3"]                          # every rank switched its own bucket
     assert sw["ranks"] == 2 and sw["worker_major"]["ok"] is True and sw["round_robin"]["ok"] is True
     assert sw["worker_major"]["aggregate_GBps"] > 0
@@ -98,4 +100,4 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     shard = d["config"]["shard_values"]          # the i16 wire gathers int16 sums + slot flags
     assert d["xgmi"]["ag_recv_bytes_per_rank"] == 2 * shard + shard // 256
     assert d["xgmi"]["rs_send_bytes_per_rank"] == 4 * shard
-    assert d["allreduce"]["parity_spot_check"] is True
+    assert d["allreduce"]["parity_spot_check"] is True and d["pipelined"]["parity_spot_check"] is True

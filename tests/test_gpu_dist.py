@@ -28,11 +28,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(tmp_path, world, n, wire, k, V=256, layout="A", workers=0, collective="rs_ag"):
+def _run_ranks(tmp_path, world, n, wire, k, V=256, layout="A", workers=0, collective="rs_ag", chunks=1):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", RANK_SCRIPT,
            "--size", str(n), "--wire", wire, "--k", str(k), "--V", str(V), "--out", str(tmp_path),
-           "--layout", layout, "--workers", str(workers), "--collective", collective]
+           "--layout", layout, "--workers", str(workers), "--collective", collective,
+           "--chunks", str(chunks)]
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     return [dict(np.load(os.path.join(tmp_path, f"rank{i}.npz"))) for i in range(world)]
@@ -40,11 +41,16 @@ def _run_ranks(tmp_path, world, n, wire, k, V=256, layout="A", workers=0, collec
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,n,coll", [(2, 1_000_003, "rs_ag"), (3, 70_001, "rs_ag"), (2, 1, "rs_ag"),
-                                          (8, 400_001, "rs_ag"), (3, 70_001, "allreduce")])
+                                          (8, 400_001, "rs_ag"), (3, 70_001, "allreduce"),
+                                          (3, 70_001, "chunks3"), (2, 1, "chunks2"), (8, 400_001, "chunks4")])
 def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n, coll):
+    """Layout A, int32 wire: reduce-scatter + all-gather, the all-reduce variant, and the
+    pipelined chunks (chunksC: C async reduce-scatters / all-gathers)."""
     from oracle import oracle as orc
     k = 20
-    res = _run_ranks(tmp_path, world, n, "i32", k, collective=coll)
+    chunks = int(coll[6:]) if coll.startswith("chunks") else 1
+    res = _run_ranks(tmp_path, world, n, "i32", k, collective="rs_ag" if chunks > 1 else coll,
+                     chunks=chunks)
     want_int = orc.quantize_reduce_i32([bucket(r, n, "i32") for r in range(world)], k)
     want = orc.dequantize_i32(want_int, k)
     for r, d in enumerate(res):
@@ -60,11 +66,14 @@ def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n, coll):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,n,V,coll", [(2, 1_000_003, 256, "rs_ag"), (3, 50_000, 32, "rs_ag"),
                                             (2, 300, 100, "rs_ag"), (8, 200_000, 32, "rs_ag"),
-                                            (3, 50_000, 32, "allreduce")])
+                                            (3, 50_000, 32, "allreduce"), (3, 50_000, 32, "chunks4"),
+                                            (2, 300_001, 100, "chunks3")])
 def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V, coll):
     from oracle import oracle as orc
     k = 11
-    res = _run_ranks(tmp_path, world, n, "i16", k, V, collective=coll)
+    chunks = int(coll[6:]) if coll.startswith("chunks") else 1
+    res = _run_ranks(tmp_path, world, n, "i16", k, V, collective="rs_ag" if chunks > 1 else coll,
+                     chunks=chunks)
     want16, want_ovf = orc.quantize_reduce_i16_sat([bucket(r, n, "i16") for r in range(world)], k, V)
     assert want_ovf.any() and not want_ovf.all()
     want = orc.dequantize_i16(want16, k)
@@ -74,7 +83,7 @@ def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V, coll):
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want16[lo:hi])
         gb, shard = (int(v) for v in d["gather_bytes"])      # int16 sums + flags gathered
-        assert gb == (world - 1) * (2 * shard + shard // V if coll == "rs_ag" else 4 * shard)
+        assert gb == (world - 1) * (4 * shard if coll == "allreduce" else 2 * shard + shard // V)
 
 
 @pytest.mark.gpu
