@@ -38,8 +38,8 @@ for f in sorted(f for f in os.listdir(REPO) if re.fullmatch(r"BENCH_r\d+\.json",
     except Exception:
         pass
 opt = [(n, w) for n, w in (
-    ("rehearse_2ranks_gloo.json", "bench.py --gpus 2 with no launcher: it starts two ranks itself (torch.distributed.run), both on the box's one GPU over gloo -- the multi-rank timing, max-over-ranks and the config-5 sharded path with device quantise/decode (collectives staged through host memory)"),
-    ("rehearse_8ranks_gloo.json", "bench.py --gpus 8 starting its own 8 ranks, all on the box's one GPU over gloo: the N = 8 flow end to end (group-size assert, max-over-ranks timing, the 8-way config-5 shard plan, parity spot checks); throughput numbers are meaningless with 8 ranks on one GPU"),
+    ("rehearse_2ranks_gloo.json", "bench.py --gpus 2 with no launcher: it starts two ranks itself (torch.distributed.run), both on the box's one GPU over gloo -- the multi-rank timing, max-over-ranks and the config-5 sharded path with device quantise/decode (collectives staged through host memory), with its all-reduce and 4-chunk pipelined variants (session r02o)"),
+    ("rehearse_8ranks_gloo.json", "bench.py --gpus 8 starting its own 8 ranks, all on the box's one GPU over gloo: the N = 8 flow end to end (group-size assert, max-over-ranks timing, the 8-way config-5 shard plan, layout B, the all-reduce and pipelined variants, parity spot checks; session r02o); throughput numbers are meaningless with 8 ranks on one GPU"),
     ("bench_boxes.json", "the headline line on every box of this round's evidence sessions, next to the driver's round-1 line"),
     ("sharded_c5_1gpu_i32.json", "bench.py --mode sharded --wire i32: config 5 (1 GiB fp32 per rank) as the headline on one GPU; the collectives are identities at N = 1"),
     ("sharded_c5_1gpu_i16.json", "the same on the int16 saturating wire (q16 + saturation count in one int32 SUM, saturate once)"),
