@@ -41,6 +41,16 @@ def main():
     fo = torch.empty_like(flags)
     dist.all_gather_into_tensor(fo, flags)
     assert torch.equal(fo, flags)
+    # the pipelined variant's calls: async work on views into one buffer, waited later
+    buf = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    buf[n:] = q
+    part = torch.empty(n, dtype=torch.int32, device=dev)
+    w = dist.reduce_scatter_tensor(part, buf[n:], op=dist.ReduceOp.SUM, async_op=True)
+    w.wait()
+    fbuf = torch.zeros(2 * n, device=dev)
+    w = dist.all_gather_into_tensor(fbuf[n:], ops.dequantize(part, k), async_op=True)
+    w.wait()
+    assert torch.equal(fbuf[n:], y) and not fbuf[:n].any()
     t = torch.tensor([1.5], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
