@@ -176,3 +176,41 @@ def test_range_aggregator_host_checks():
         ShardedAggregator(10, device=torch.device("cpu"), collective="allreduce", chunks=2)
     one = ShardedAggregator(5000, device=torch.device("cpu"), chunks=4)
     assert one.chunks == 1 and one.gather_bytes == 0      # one rank: nothing to pipeline
+
+
+def _worker_chunk_plan(rank, world, port, results):
+    import math
+    import sys
+    for p in (REPO, PKG_ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from ina_amd.dist import ShardedAggregator
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = []
+        for n, wire, V, C in [(1, "i32", 256, 2), (1_000_003, "i32", 256, 4), (300_001, "i16", 100, 3),
+                              (268_435_456 // 64, "i16", 256, 4)]:
+            a = ShardedAggregator(n, device=torch.device("cpu"), wire=wire, V=V, chunks=C)
+            align = 1024 if wire == "i32" else 1024 * V // math.gcd(1024, V)
+            L = a.cplan.padded
+            out.append((a.chunks == C, a.cplan.shard == a.sc, a.sc % align == 0, L == world * a.sc,
+                        a.cpad == C * L >= n, (C - 1) * L < n or n < C * world * align,
+                        a._qbuf.numel() >= max(a.cpad, a.plan.padded),
+                        a.gather_bytes == (world - 1) * (C * a.sc * (4 if wire == "i32" else 2)
+                                                         + (0 if wire == "i32" else C * a.sc // V))))
+        results[rank] = out
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_chunk_plan_invariants_gloo():
+    """The pipelined layout-A plan at world 2 (host side, no kernels): every chunk is
+    world x Sc values, Sc a whole number of aligned slots, the chunks cover the bucket
+    without a wholly empty tail beyond the alignment, and the gather bytes add up."""
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker_chunk_plan, args=(2, _free_port(), results), nprocs=2, join=True)
+    for r in range(2):
+        for case in results[r]:
+            assert all(case), case
