@@ -150,7 +150,7 @@ int ina_sum_reduce_host_i32(const int32_t* const* host_bufs, int W, int32_t* hos
         if (k >= (size_t)kSlots) chk(hipStreamWaitEvent(cs, P.out_done[slot], 0));
         const int32_t* ptrs[INA_MAX_WORKERS];
         for (int w = 0; w < W; ++w) ptrs[w] = in_buf(slot, w);
-        if (int rc = ina_sum_reduce_i32(ptrs, W, out_buf(slot), len, stream)) {
+        if (int rc = ina::sum_reduce_i32_impl(ptrs, W, out_buf(slot), len, stream, true)) {
             drain();
             return rc;
         }

@@ -15,6 +15,8 @@ struct PtrPack {
 
 int set_error(int code, const char* fmt, const char* detail);
 int set_h2d_streams(int v);   // ina_host.cpp
+int sum_reduce_i32_impl(const int32_t* const* bufs, int W, int32_t* out, size_t n, ina_stream_t stream,
+                        bool host);   // ina_kernels.hip
 int set_small_sort(int v);    // ina_switch.hip
 int set_switch_win(int v);    // ina_switch.hip
 int set_ack_fast(int v);      // ina_switch.hip

@@ -231,9 +231,8 @@ __device__ __forceinline__ void chunk_loop(size_t n4, Body&& body) {
 // 1. W-way int32 sum-reduce (the headline kernel)
 // ===========================================================================
 template <int W, int U, bool NT>
-__global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_vec(PtrPack<int32_t> in,
-                                                               int32_t* __restrict__ out,
-                                                               size_t n4, size_t n) {
+__device__ __forceinline__ void sum_reduce_body(const PtrPack<int32_t>& in, int32_t* __restrict__ out,
+                                                size_t n4, size_t n) {
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * kBlock;
     size_t i = tid;
@@ -267,6 +266,23 @@ __global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_vec(PtrPack<int32_t> 
         for (int w = 1; w < W; ++w) a += (uint32_t)in.p[w][t];
         out[t] = (int32_t)a;
     }
+}
+
+template <int W, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_vec(PtrPack<int32_t> in,
+                                                               int32_t* __restrict__ out,
+                                                               size_t n4, size_t n) {
+    sum_reduce_body<W, U, NT>(in, out, n4, n);
+}
+
+// the same reduce launched by the PCIe pipeline (ina_sum_reduce_host_i32) on its chunks:
+// its own symbol only so that rocprof attributes the pipeline's launches apart from the
+// device-resident bulk reduce (same body, same geometry)
+template <int W, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_host_chunk_reduce_i32(PtrPack<int32_t> in,
+                                                                  int32_t* __restrict__ out,
+                                                                  size_t n4, size_t n) {
+    sum_reduce_body<W, U, NT>(in, out, n4, n);
 }
 
 // runtime-W vector kernel (W not in the specialised set)
@@ -310,14 +326,19 @@ __global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_scalar(PtrPack<int32_
 
 template <int W, int U>
 static void launch_reduce_w(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
-                            hipStream_t s) {
+                            hipStream_t s, bool host) {
     int cap = g_reduce_blocks.load();
     // 64 workgroups per worker stream, clamped to [256, 1024] -- except W = 16 (768: 3 per
     // CU beat 4, 278.8 vs 300.2 us) and W = 2 with one chunk (512); tools/lab/reduce_w_sweep.py
     if (cap <= 0)
         cap = W == 16 ? 768 : (W == 2 && U == 1) ? 512 : (W * 64 < 256 ? 256 : (W * 64 > 1024 ? 1024 : W * 64));
     unsigned g = grid_for(n4, U, cap);
-    if (g_nontemporal.load())
+    const bool nt = g_nontemporal.load();
+    if (host && nt)
+        hipLaunchKernelGGL((k_host_chunk_reduce_i32<W, U, true>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
+    else if (host)
+        hipLaunchKernelGGL((k_host_chunk_reduce_i32<W, U, false>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
+    else if (nt)
         hipLaunchKernelGGL((k_sum_reduce_i32_vec<W, U, true>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
     else
         hipLaunchKernelGGL((k_sum_reduce_i32_vec<W, U, false>), dim3(g), dim3(kBlock), 0, s, pk, out, n4, n);
@@ -325,13 +346,13 @@ static void launch_reduce_w(const PtrPack<int32_t>& pk, int32_t* out, size_t n4,
 
 template <int W>
 static void launch_reduce_u(const PtrPack<int32_t>& pk, int32_t* out, size_t n4, size_t n,
-                            hipStream_t s) {
+                            hipStream_t s, bool host) {
     int u = g_unroll.load();
     if (u == 0) u = W <= 4 ? 1 : 4;   // auto: 1 chunk per stream for W <= 4 (86.5 vs 90.4 us at W = 4)
     switch (u) {
-        case 1: launch_reduce_w<W, 1>(pk, out, n4, n, s); break;
-        case 2: launch_reduce_w<W, 2>(pk, out, n4, n, s); break;
-        default: launch_reduce_w<W, 4>(pk, out, n4, n, s); break;
+        case 1: launch_reduce_w<W, 1>(pk, out, n4, n, s, host); break;
+        case 2: launch_reduce_w<W, 2>(pk, out, n4, n, s, host); break;
+        default: launch_reduce_w<W, 4>(pk, out, n4, n, s, host); break;
     }
 }
 
@@ -1499,8 +1520,12 @@ int ina_set_tuning(int key, int value) {
     }
 }
 
-int ina_sum_reduce_i32(const int32_t* const* bufs, int W, int32_t* out, size_t n,
-                       ina_stream_t stream) {
+}  // extern "C"
+
+namespace ina {
+// host = true: the PCIe pipeline's chunks (k_host_chunk_reduce_i32, see above)
+int sum_reduce_i32_impl(const int32_t* const* bufs, int W, int32_t* out, size_t n,
+                        ina_stream_t stream, bool host) {
     if (n == 0) return INA_OK;
     PtrPack<int32_t> pk;
     bool al;
@@ -1513,17 +1538,25 @@ int ina_sum_reduce_i32(const int32_t* const* bufs, int W, int32_t* out, size_t n
     }
     size_t n4 = n / 4;
     switch (W) {
-        case 1: launch_reduce_u<1>(pk, out, n4, n, s); break;
-        case 2: launch_reduce_u<2>(pk, out, n4, n, s); break;
-        case 3: launch_reduce_u<3>(pk, out, n4, n, s); break;
-        case 4: launch_reduce_u<4>(pk, out, n4, n, s); break;
-        case 8: launch_reduce_u<8>(pk, out, n4, n, s); break;
-        case 16: launch_reduce_u<16>(pk, out, n4, n, s); break;
+        case 1: launch_reduce_u<1>(pk, out, n4, n, s, host); break;
+        case 2: launch_reduce_u<2>(pk, out, n4, n, s, host); break;
+        case 3: launch_reduce_u<3>(pk, out, n4, n, s, host); break;
+        case 4: launch_reduce_u<4>(pk, out, n4, n, s, host); break;
+        case 8: launch_reduce_u<8>(pk, out, n4, n, s, host); break;
+        case 16: launch_reduce_u<16>(pk, out, n4, n, s, host); break;
         default:
             hipLaunchKernelGGL(k_sum_reduce_i32_vec_dyn, dim3(grid_for(n4, 1)), dim3(kBlock), 0, s,
                                pk, W, out, n4, n);
     }
     return check_launch("sum_reduce_i32");
+}
+}  // namespace ina
+
+extern "C" {
+
+int ina_sum_reduce_i32(const int32_t* const* bufs, int W, int32_t* out, size_t n,
+                       ina_stream_t stream) {
+    return sum_reduce_i32_impl(bufs, W, out, n, stream, false);
 }
 
 int ina_quantize_f32_i32(const float* x, int32_t* q, size_t n, int k, ina_stream_t stream) {

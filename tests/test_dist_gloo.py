@@ -198,7 +198,10 @@ def _worker_chunk_plan(rank, world, port, results):
                         a.cpad == C * L >= n, (C - 1) * L < n or n < C * world * align,
                         a._qbuf.numel() >= max(a.cpad, a.plan.padded),
                         a.gather_bytes == (world - 1) * (C * a.sc * (4 if wire == "i32" else 2)
-                                                         + (0 if wire == "i32" else C * a.sc // V))))
+                                                         + (0 if wire == "i32" else C * a.sc // V)),
+                        not a._shard_bufs))    # whole-bucket shard buffers: lazy when chunked
+        full = ShardedAggregator(1000, device=torch.device("cpu"))      # unchunked: allocated up front
+        out.append((set(full._shard_bufs) == {"sum", "f"}, full.sum_shard.numel() == full.plan.shard))
         results[rank] = out
     finally:
         dist.destroy_process_group()

@@ -46,14 +46,34 @@ def test_bench_json_line_contract():
     assert rf["algorithmic_bytes_per_launch"] == 9 * 26_214_400 * 4
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["value"] > 0
-    assert cb["affinity_cores"] == len(os.sched_getaffinity(0)) and 1 <= cb["cores"] <= cb["affinity_cores"]
-    assert cb["value"] == max(cb["value_by_threads"].values())
+    aff = len(os.sched_getaffinity(0))
+    assert cb["affinity_cores"] == aff and 1 <= cb["cores"] <= aff      # cores = CPUs granted
+    assert str(cb["threads"]) in cb["value_by_threads"]                 # threads = best count
+    assert cb["value"] == max(cb["value_by_threads"].values()) == cb["value_by_threads"][str(cb["threads"])]
+    if cb["cgroup_cpu_quota"]:
+        assert cb["cores"] == min(aff, max(1, int(cb["cgroup_cpu_quota"])))
     assert cb["matches_gpu"] is True and cb["value_1core"] > 0
-    assert "workload" in d["config"]
+    assert "workload" in d["config"] and "independent replicas" in d["config"]["parallelism"]
+    # the single-GPU BASELINE configs 2 and 4 and the PCIe-inclusive rate, each with a
+    # roofline and a parity spot check
+    c2, c4, e2e = d["c2_fused"], d["c4_int16"], d["e2e_pcie"]
+    for leg, kern, algo in ((c2, "k_quant_reduce_i32<4>", 20 * 25_557_032),
+                            (c4, "k_quant_reduce_i16<16>", 66 * 25_557_032 + 99_833)):
+        rf = leg["roofline"]
+        assert leg["parity_spot_check"] is True and rf["bound"] == "hbm" and kern in rf["kernel"]
+        assert rf["algorithmic_bytes_per_launch"] == algo and 0 < rf["frac"] < 1
+        assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert c4["overflow_slots"] == c4["overflow_slots_injected"] > 0
+    assert e2e["parity_spot_check"] is True and e2e["roofline"]["bound"] == "pcie_h2d"
+    assert 0 < e2e["roofline"]["frac"] and e2e["roofline"]["peak"] > 0
     c5 = d["sharded_c5"]
     assert c5["parity_spot_check"] is True and c5["rccl_world"] == 1 and c5["values_per_rank"] == 1 << 22
     assert c5["layout_b"]["parity_spot_check"] is True and c5["layout_b"]["value"] > 0
     assert "allreduce" not in c5 and "pipelined" not in c5   # one rank: no collective to compare
+    for r in (c5["roofline"], c5["layout_b"]["roofline"]):   # one rank: no xGMI bytes, null fields
+        assert r["bound"] == "xgmi" and r["peak"] == 7 * 153.0
+        assert r["achieved"] is None and r["frac"] is None
+        assert all(p["frac"] > 0 for p in r["hbm_phases"].values())   # 16 MiB: may replay from MALL
     sw = d["switch_c3"]                          # the packet-stream switch, measured live
     assert sw["algorithmic_bytes"] == 819_200 * 1040 + 102_400 * (1040 + 1029) + 819_200
     for order in ("worker_major", "round_robin"):
@@ -80,6 +100,11 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
                    env={"INA_BENCH_BACKEND": "gloo"}, timeout=400))
     assert d["n_gpus"] == 2 and d["rccl_world"] == 2 and d["backend"] == "gloo"
     assert d["parity_spot_check"] is True and "cpu_baseline" not in d
+    assert "independent replicas x 2" in d["config"]["parallelism"]
+    rf = d["roofline"]                           # the slowest rank's launch: frac = min over ranks
+    assert rf["per_rank_frac_min"] == rf["frac"] <= rf["per_rank_frac_max"]
+    for leg in ("c2_fused", "c4_int16", "e2e_pcie"):
+        assert d[leg]["parity_spot_check"] is True, leg
     c5 = d["sharded_c5"]
     assert c5["rccl_world"] == 2 and c5["parity_spot_check"] is True
     assert c5["xgmi"]["rs_send_bytes_per_rank"] == c5["shard_values"] * 4
@@ -90,6 +115,14 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert ar["xgmi"]["allreduce_bytes_per_rank"] == 2 * c5["shard_values"] * 4
     pl = c5["pipelined"]                         # chunked, async RCCL work, same bits
     assert pl["chunks"] > 1 and pl["parity_spot_check"] is True
+    # every variant carries an xGMI roofline with the per-rank bytes it moved
+    assert c5["roofline"]["bytes_per_rank"] == 2 * c5["shard_values"] * 4
+    assert c5["layout_b"]["roofline"]["bytes_per_rank"] == c5["shard_values"] * 4
+    assert ar["roofline"]["bytes_per_rank"] == 2 * c5["shard_values"] * 4
+    assert pl["roofline"]["bytes_per_rank"] == pl["xgmi"]["rs_send_bytes_per_rank"] + pl["xgmi"]["ag_recv_bytes_per_rank"]
+    for r in (c5["roofline"], c5["layout_b"]["roofline"], ar["roofline"], pl["roofline"]):
+        assert r["bound"] == "xgmi" and r["achieved"] > 0 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert set(c5["roofline"]["hbm_phases"]) == {"quantize", "decode"}
     sw = d["switch_c3"]                          # every rank switched its own bucket
     assert sw["ranks"] == 2 and sw["worker_major"]["ok"] is True and sw["round_robin"]["ok"] is True
     assert sw["worker_major"]["aggregate_GBps"] > 0

@@ -104,3 +104,16 @@ def test_data_manager_byte_range_checks():
     assert _signed_byte("degree", -1) == 0xFF and _signed_byte("degree", 127) == 127
     with pytest.raises(ValueError):
         _signed_byte("degree", 128)
+
+
+def test_spawn_pools_start_warm():
+    """multi_process_send / multi_process_send_futures_P start their spawned workers and
+    run the warm-up initializer (HIP start-up + a barrier over every worker) before the
+    clock starts; the pools come up and drain here without a GPU."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    from ina_amd import communicator as cm
+    with cm._SPAWN.Pool(3, **cm._warm_pool_args(3)) as pool:
+        assert pool.map(cm._noop, range(3), chunksize=1) == [None] * 3
+    with ProcessPoolExecutor(max_workers=2, mp_context=cm._SPAWN, **cm._warm_pool_args(2)) as ex:
+        assert list(ex.map(cm._noop, range(2))) == [None, None]

@@ -84,3 +84,18 @@ def test_fused_quant_reduce_equals_composition():
     assert np.array_equal(f16, s16)
     anyq = np.any([o for _, o in q16], axis=0)
     assert np.array_equal(ovf.astype(bool), anyq | ovf_sum.astype(bool))
+
+
+@pytest.mark.parametrize("k", [0, 13, 16, -3])
+def test_bench_spot_check_quantisers_match_oracle(k):
+    """bench.py's C2 / C4 parity spot checks restate the quantiser in numpy; they must
+    agree with the oracle on the edge values and random magnitudes."""
+    import bench
+    rng = np.random.default_rng(k + 70)
+    x = np.concatenate([EDGE, (rng.standard_normal(5000) * 10.0 ** rng.integers(-6, 6, 5000))
+                        .astype(np.float32), EDGE / np.float32(2.0 ** k)])
+    assert np.array_equal(bench._np_q32(x, k), orc.quantize_i32(x, k).astype(np.int64))
+    q, sat = bench._np_q16(x, k)
+    qo, _ = orc.quantize_i16_sat(x, k, 1)
+    assert np.array_equal(q, qo.astype(np.int64))
+    assert np.array_equal(sat, np_q16(x, k)[1])

@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; the script stops at the first crash,
 # abort or timeout (only an ordinary pytest failure, rc 1, lets it continue).
 # usage: tools/gpu_session.sh TAG [stages...]   stages: smoke test bench prof pmc extra swprof
-#        config1 rehearse rehearse8 sharded swlab pathprof
+#        contract config1 rehearse rehearse8 sharded swlab pathprof
 set -u
 TAG=${1:-r02}; shift || true
 STAGES=${*:-"smoke test bench prof pmc extra"}
@@ -20,6 +20,9 @@ for st in $STAGES; do
     test)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -25 "$OUT/pytest_gpu.log"; ok_or_fail pytest $rc ;;
+    contract)
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_bench_contract.py -m gpu -v -rf --timeout 600 --timeout-method thread > "$OUT/contract.log" 2>&1
+      rc=$?; tail -8 "$OUT/contract.log"; ok_or_fail contract $rc ;;
     bench)
       timeout -k 10 400 python bench.py --steps 50 --warmup 10 > "$OUT/bench.json" 2> "$OUT/bench.err"
       rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -ne 0 ] && fatal bench $rc ;;
