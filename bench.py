@@ -571,11 +571,17 @@ def _sample_idx(n: int, step: int = 997) -> np.ndarray:
                                      np.arange(max(0, n - 4096), n)]))
 
 
-def _time_rotating(fn_for_set, rotate, steps, warm, stream):
+def _time_rotating(fn_for_set, rotate, steps, warm, stream, min_warm_s=0.05):
     """HIP events on the launch stream around `steps` back-to-back launches alternating
-    `rotate` input sets (the headline's method); returns the average launch in seconds."""
-    for i in range(warm):
+    `rotate` input sets (the headline's method); returns the average launch in seconds.
+    Warm-up: `warm` launches and at least `min_warm_s` of them, so the timed launches do
+    not start while the GPU's clocks are still ramping up from an idle phase."""
+    t0, i = time.perf_counter(), 0
+    while i < warm or time.perf_counter() - t0 < min_warm_s:
         fn_for_set(i % rotate)
+        i += 1
+        if i % 8 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -943,10 +949,12 @@ def run_reduce(args, rank, world, dev, backend):
                      "per_rank_frac_max": round(algo_bytes / best_avg_s / 1e9 / HBM_PEAK_GBS, 4)},
         "parity_spot_check": parity,
     }
+    cpu_in = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # timed last: a CPU phase of seconds leaves the GPU idle and its clocks low, and
+        # the GPU legs below would start inside that ramp
         s = min(args.cpu_sample, n)
-        host = [b[:s].cpu().numpy() for b in sets[last]]
-        line["cpu_baseline"] = cpu_baseline(args, host, outs[last][:s].cpu().numpy())
+        cpu_in = ([b[:s].cpu().numpy() for b in sets[last]], outs[last][:s].cpu().numpy())
     del sets, outs
     torch.cuda.empty_cache()
     if not args.no_c2:
@@ -966,6 +974,8 @@ def run_reduce(args, rank, world, dev, backend):
             line["sharded_c5"]["pipelined"] = measure_c5(args, rank, world, dev, chunks=C5_CHUNKS)
     if not args.no_switch:
         line["switch_c3"] = measure_switch(dev, rank=rank, world=world)
+    if cpu_in is not None:
+        line["cpu_baseline"] = cpu_baseline(args, *cpu_in)
     return line
 
 

@@ -1426,6 +1426,57 @@ __global__ __launch_bounds__(kBlock) void k_absmax_f32(const float* __restrict__
     }
 }
 
+// W workers in one pass (ina_absmax_multi_f32): a thread's 16-byte chunk of base is loaded
+// once and compared against the same chunk of every worker, 4 workers' loads in flight at
+// a time -- W + 1 streams instead of W launches of 2 (and no per-worker memset + launch)
+__global__ __launch_bounds__(kBlock) void k_absmax_multi_f32(PtrPack<float> xs, int W,
+                                                             const float* __restrict__ base, size_t n,
+                                                             int vec, uint32_t* __restrict__ out) {
+    __shared__ float part[kBlock / 64];
+    const size_t n4 = vec ? n / 4 : 0;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    float m = 0.0f;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
+        const f32x4 b = base ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base) + i)
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
+        int w = 0;
+        for (; w + 4 <= W; w += 4) {
+            f32x4 a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                a[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xs.p[w + u]) + i);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                m = fmaxf(m, fabsf(__fsub_rn(a[u].x, b.x)));
+                m = fmaxf(m, fabsf(__fsub_rn(a[u].y, b.y)));
+                m = fmaxf(m, fabsf(__fsub_rn(a[u].z, b.z)));
+                m = fmaxf(m, fabsf(__fsub_rn(a[u].w, b.w)));
+            }
+        }
+        for (; w < W; ++w) {
+            const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xs.p[w]) + i);
+            m = fmaxf(m, fabsf(__fsub_rn(a.x, b.x)));
+            m = fmaxf(m, fabsf(__fsub_rn(a.y, b.y)));
+            m = fmaxf(m, fabsf(__fsub_rn(a.z, b.z)));
+            m = fmaxf(m, fabsf(__fsub_rn(a.w, b.w)));
+        }
+    }
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        for (int w = 0; w < W; ++w) m = fmaxf(m, absdiff(xs.p[w][i], base, i));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = part[0];
+        for (int w = 1; w < kBlock / 64; ++w) r = fmaxf(r, part[w]);
+        atomicMax(out, __float_as_uint(r));
+    }
+}
+#ifndef INA_ABSMAX_MULTI_BLOCKS
+#define INA_ABSMAX_MULTI_BLOCKS 512
+#endif
+
 }  // namespace ina
 
 // ===========================================================================
@@ -1877,6 +1928,22 @@ int ina_absmax_f32(const float* x, const float* base, size_t n, float* out_dev, 
     hipLaunchKernelGGL(k_absmax_f32, dim3(grid_for(vec ? n / 4 + 1 : n, INA_ABSMAX_U, INA_ABSMAX_BLOCKS)), dim3(kBlock), 0,
                        s, x, base, n, vec, reinterpret_cast<uint32_t*>(out_dev));
     return check_launch("absmax_f32");
+}
+
+int ina_absmax_multi_f32(const float* const* xs, int W, const float* base, size_t n, float* out_dev,
+                         ina_stream_t stream) {
+    if (!out_dev) return set_error(INA_EINVAL, "null out%s", "");
+    PtrPack<float> pk;
+    bool al;
+    if (int rc = fill_pack(pk, xs, W, al)) return rc;
+    hipStream_t s = hs(stream);
+    if (hipMemsetAsync(out_dev, 0, sizeof(float), s) != hipSuccess)
+        return set_error(INA_EHIP, "memset absmax%s", "");
+    if (n == 0) return INA_OK;
+    const int vec = al && (!base || aligned16(base));
+    hipLaunchKernelGGL(k_absmax_multi_f32, dim3(grid_for(vec ? n / 4 + 1 : n, 1, INA_ABSMAX_MULTI_BLOCKS)),
+                       dim3(kBlock), 0, s, pk, W, base, n, vec, reinterpret_cast<uint32_t*>(out_dev));
+    return check_launch("absmax_multi_f32");
 }
 
 int ina_scale_for(float absmax, int W, int bits, int* k_out) {

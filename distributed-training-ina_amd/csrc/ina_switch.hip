@@ -4,9 +4,10 @@
 //
 // A batch of NGA-V packets in arrival order is grouped by aggregator slot with a
 // stable sort (slot, arrival) -- slots are independent in the P4 program, so per-slot
-// arrival order is all that matters: by default one global pass on the key's high digit
-// and one workgroup per bucket of slots on the low digit (k_rs_local), else LSD digit
-// passes or a one-workgroup bitonic sort for small batches.  Each slot's packets are
+// arrival order is all that matters: by default each chunk sorted by the key's high digit
+// (k_sort_chunks) and one workgroup per bucket of slots gathering its runs and sorting them
+// on the low digit (k_sort_buckets), else LSD digit passes or a one-workgroup bitonic sort
+// for small batches.  Each slot's packets are
 // then run through the register state machine by ONE wave (k_switch_run2): the slot's V
 // registers stay in VGPRs for the whole segment, lane l holds 16-byte chunk l of up to 8
 // packets at once, payload words at byte 15 + 4j are decoded with v_alignbyte from the
@@ -273,14 +274,14 @@ static std::atomic<int> g_small_sort{INA_SWITCH_SMALL_DEFAULT};
 #endif
 static std::atomic<int> g_switch_win{0};   // ina_set_tuning key 10: run-kernel window (0: auto)
 static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack lane path (0: off)
-// ina_set_tuning key 12, the slot sort: 0 auto (bucket + local for two-digit keys, else the
-// digit passes), 1 one-sweep, 2 bucket + local where it applies, 3 hist/colscan/scatter
-// digit passes (r01).  Bucket + local measured 265.3 -> 251.0 us against the digit passes
-// at 819,200 NGA-256 packets with descriptors (profiles/r02/lab/switch_sort_lab_hyb.json)
+// ina_set_tuning key 12, the slot sort: 0 auto (chunk + bucket sort for keys of one or two
+// digits, else the LSD digit passes), 3 the digit passes for every batch (the cross-check the
+// tests run both ways).  The one-sweep and round-2 bucket + local variants moved to tools/lab
+// (DESIGN.md section 4).
 static std::atomic<int> g_sort_mode{0};
-static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: sort tile rounds (0 auto, 4/8/16)
+static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: sort chunk rounds (0 auto, 4/8/16)
 int set_sort_mode(int v) {
-    if (v < 0 || v > 3) return INA_EINVAL;
+    if (v != 0 && v != 3) return INA_EINVAL;
     g_sort_mode = v;
     return INA_OK;
 }
@@ -495,297 +496,295 @@ __global__ __launch_bounds__(NW * 64) void k_rs_scatter(const uint32_t* __restri
     rs_tile_scatter<R, NW>(k, v, i0, n, shift, bits, base, dbase, kout, vout);
 }
 
-// ---- bucket + local slot sort (ina_set_tuning key 12 = 2) -----------------------------
-// Two-digit keys sorted MSD-first: ONE global pass (keys + histogram, column scan, scatter)
-// on the high digit leaves every bucket of 2^lbits consecutive slots contiguous and in
-// arrival order; then one workgroup per bucket sorts it stably on the low digit, the
-// bucket's whole tile staying in registers and LDS.  The permutation equals the LSD
-// passes' (stable by (high, low) digit, arrival order inside a slot), so the run kernel
-// sees the same arrays; the second pass's histogram and column-scan launches and its
-// global rank bookkeeping are gone.  A bucket larger than one tile (skewed slot use) is
-// sorted tile by tile: a counting sweep over the bucket first, then the tiles in order.
-#ifndef INA_LOCAL_WAVES
-#define INA_LOCAL_WAVES 16
+// ---- chunk + bucket slot sort (keys of one or two digits; the default) --------------------
+// Two launches instead of the digit passes' keys / column scan / scatter / bucket-local four:
+//   A  k_sort_chunks   one block per chunk of CH = 16 waves x 64 x R packets: the packets'
+//                      keys, and the chunk sorted STABLY by the key's high digit inside its
+//                      own range of the output (per-wave LDS digit counts, a block scan, the
+//                      ballot-ranked tile scatter), publishing per (digit, chunk) the run
+//                      length and the run's start inside the chunk (= the chunk's packets
+//                      in lower buckets).
+//   B  k_sort_buckets  one block per bucket (high digit): its row of run lengths gives where
+//                      each chunk's run goes inside the bucket, its row of run starts sums
+//                      to the bucket's place in the output (no block waits for another);
+//                      it gathers its runs in chunk order -- arrival order -- and sorts them
+//                      on the low digit in LDS (tile by tile after a counting sweep when
+//                      the bucket is larger than one tile).
+// The permutation equals the LSD passes' (stable by (high, low) digit, arrival order inside
+// a slot), so the run kernel sees the same arrays.  The bucket of foreign packets only (a
+// pool that is a multiple of 2^lb slots) is not gathered: B stores its size and the
+// register-resident run kernel stops before it.  Keys of one digit (pools < 512 slots) are
+// the same with lb = 0: B only gathers.
+#ifndef INA_BK_WAVES
+#define INA_BK_WAVES 16
 #endif
-constexpr int kLcWaves = INA_LOCAL_WAVES;           // waves per bucket workgroup
-constexpr int kLcRounds = 64 / kLcWaves > 4 ? 64 / kLcWaves : 4;   // tile = max(4096, 256 x waves) items
-template <int NW, int R>
-__global__ __launch_bounds__(NW * 64) void k_rs_local(const uint32_t* __restrict__ kin,
-                                                      const uint32_t* __restrict__ vin,
-                                                      uint32_t* __restrict__ kout,
-                                                      uint32_t* __restrict__ vout, int lbits,
-                                                      const uint32_t* __restrict__ totals,
-                                                      uint32_t skip) {
-    constexpr int kThr = NW * 64;
-    // the bucket holding nothing but foreign packets (sentinel key num_slots) is not sorted:
-    // they sort after every slot anyway and the run kernel skips them (nforeign)
-    if (blockIdx.x == skip) return;
-    constexpr int kDPT = (kRsBins + kThr - 1) / kThr;
-    __shared__ uint32_t base[NW][kRsBins];
-    __shared__ uint32_t gst[kRsBins];               // bucket digit counts, then output positions
-    __shared__ uint32_t red[NW];
-    const int lane = threadIdx.x & 63, wv = wave_in_block();
-    const uint32_t b = blockIdx.x;
-    // bucket start = sum of the earlier buckets' totals (high-digit pass)
-    uint32_t part = 0;
-    for (uint32_t d = threadIdx.x; d < b; d += kThr) part += totals[d];
-    part = __builtin_amdgcn_readlane(wave_incl_scan(part), 63);
-    if (lane == 0) red[wv] = part;
-    const uint32_t cnt = totals[b];
-    const uint32_t nb = 1u << lbits;
-    for (uint32_t d = threadIdx.x; d < nb; d += kThr) gst[d] = 0;
-    __syncthreads();
-    if (cnt == 0) return;                           // block-uniform
-    uint32_t s0 = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s0 += red[w];
-    constexpr uint32_t kTile = (uint32_t)kThr * (uint32_t)R;
-    const uint32_t ntile = (cnt + kTile - 1) / kTile;
-    const size_t n_end = (size_t)s0 + cnt;
-    if (ntile > 1) {                                // bucket digit totals -> output positions
-        for (size_t i = (size_t)s0 + (size_t)wv * 64 + (size_t)lane; i - (size_t)lane < n_end; i += kThr)
-            lds_count(gst, (i < n_end ? kin[i] : 0u) & (nb - 1), i < n_end);
-        __syncthreads();
-        if (wv == 0) {
-            uint32_t carry = s0;
-            for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
-                const uint32_t d = d0 + (uint32_t)lane;
-                const uint32_t t = d < nb ? gst[d] : 0u;
-                const uint32_t inc = wave_incl_scan(t);
-                if (d < nb) gst[d] = carry + inc - t;
-                carry += __builtin_amdgcn_readlane(inc, 63);
-            }
-        }
-    }
-    for (uint32_t t = 0; t < ntile; ++t) {
-        // the tile's items split evenly over the waves in order (wave w: rw rounds of 64
-        // consecutive items), so a 2,048-item bucket is 2 rounds per wave, not 8 of 4 waves
-        const uint32_t tn = min(kTile, cnt - t * kTile);
-        const int rw = (int)((tn + (uint32_t)kThr - 1) / (uint32_t)kThr);
-        const size_t i0 = (size_t)s0 + (size_t)t * kTile + (size_t)wv * 64 * (size_t)rw + (size_t)lane;
-        const size_t t_end = (size_t)s0 + (size_t)t * kTile + tn;
-        uint32_t k[R], v[R];
+constexpr int kBkWaves = INA_BK_WAVES;
+constexpr int kBkThr = kBkWaves * 64;
+constexpr int kBkMaxChunks = 4096;                  // B's LDS rows: up to 4096 x CH packets
+constexpr int kLcRounds = 64 / kBkWaves > 4 ? 64 / kBkWaves : 4;   // B's tile: max(4096, 256 x waves) items
+
+// key fields of R rounds of 64 packets (all loads issued first): slot index, switch id and
+// the PS-ack flag, from the batch's descriptors (header bytes 4..11) or the headers
+template <int R, bool kDesc>
+__device__ __forceinline__ void load_key_fields(const uint8_t* __restrict__ pkts, const uint2* __restrict__ desc,
+                                                size_t npk, size_t stride, size_t p0, uint32_t (&idx)[R],
+                                                uint32_t (&sid)[R], uint32_t (&ack)[R]) {
+    if (kDesc) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const size_t i = i0 + (size_t)r * 64;
-            const bool ok = r < rw && i < t_end;
-            k[r] = ok ? kin[i] : 0u;
-            v[r] = ok ? vin[i] : 0u;
+            const size_t p = p0 + (size_t)r * 64;
+            const uint2 d = p < npk ? desc[p] : uint2{0u, 0u};
+            idx[r] = __builtin_bswap32((d.x >> 16) | (d.y << 16));
+            sid[r] = (d.y >> 16) & 0xFFu;
+            ack[r] = (d.x >> 14) & 1u;                         // flags byte 5, bit 6
         }
-        for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
+    } else if ((stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t p = p0 + (size_t)r * 64;
+            uint32_t w1 = 0, w2 = 0;
+            if (p < npk) {
+                const uint32_t* pk = reinterpret_cast<const uint32_t*>(pkts + p * stride);
+                w1 = pk[1];
+                w2 = pk[2];
+            }
+            idx[r] = __builtin_bswap32((w1 >> 16) | (w2 << 16));
+            sid[r] = (w2 >> 16) & 0xFFu;
+            ack[r] = (w1 >> 14) & 1u;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t p = p0 + (size_t)r * 64;
+            idx[r] = p < npk ? rd_be32(pkts + p * stride + 6) : 0u;
+            sid[r] = p < npk ? pkts[p * stride + 10] : 0u;
+            ack[r] = p < npk ? (pkts[p * stride + 5] >> 6) & 1u : 0u;
+        }
+    }
+}
+
+// exclusive scan of one value per thread over the block (thread d = digit d; kRsBins <=
+// kBkThr, so one digit per thread), plus `carry`: wave DPP scans and one LDS exchange of the
+// wave totals instead of one wave walking the digits serially.  Call convergent.
+static_assert(kRsBins <= kBkThr, "one digit per thread");
+__device__ __forceinline__ uint32_t block_digit_scan(uint32_t x, uint32_t* wtot, uint32_t carry) {
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane == 63) wtot[wv] = inc;
+    __syncthreads();
+    uint32_t pre = carry;
+#pragma unroll
+    for (int w = 0; w < kBkWaves; ++w) pre += w < wv ? wtot[w] : 0u;
+    return pre + inc - x;
+}
+
+template <int R, bool kDesc>
+__global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restrict__ pkts,
+                                                        const uint2* __restrict__ desc, size_t npk,
+                                                        size_t stride, uint32_t num_slots, int switch_id,
+                                                        uint8_t* __restrict__ actions, int hbits, int lb,
+                                                        uint32_t* __restrict__ rcnt, uint32_t* __restrict__ rst,
+                                                        size_t nch, uint32_t* __restrict__ kout,
+                                                        uint32_t* __restrict__ vout, int ack_hint) {
+    __shared__ uint32_t base[kBkWaves][kRsBins];     // per-wave digit counts, then bases
+    __shared__ uint32_t gst[kRsBins];                 // the chunk's run starts (output positions)
+    __shared__ uint32_t wtot[kBkWaves];
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const size_t c = blockIdx.x;
+    const uint32_t nb = 1u << hbits;
+    for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
+    const size_t i0 = c * (size_t)(kBkThr * R) + (size_t)wv * (64 * R) + (size_t)lane;
+    uint32_t idx[R], sid[R], ack[R], k[R], v[R];
+    load_key_fields<R, kDesc>(pkts, desc, npk, stride, i0, idx, sid, ack);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const size_t p = i0 + (size_t)r * 64;
+        const bool mine = switch_id >= 0 && sid[r] == (uint32_t)(uint8_t)switch_id;
+        const uint32_t key = mine ? idx[r] % num_slots : num_slots;
+        // bit 31 carries "PS ack" through the sort (no digit reads it)
+        k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
+        v[r] = (uint32_t)p;
+        if (p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
+        lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
+    }
+    __syncthreads();
+    // thread d owns digit d: the chunk's count, its chunk-local run start (block scan)
+    const uint32_t d = threadIdx.x;
+    uint32_t tc = 0;
+    if (d < nb) {
+#pragma unroll
+        for (int w = 0; w < kBkWaves; ++w) tc += base[w][d];
+    }
+    const uint32_t ex = block_digit_scan(tc, wtot, 0u);
+    if (d < nb) {
+        rcnt[(size_t)d * nch + c] = tc;
+        rst[(size_t)d * nch + c] = ex;
+        gst[d] = (uint32_t)(c * (size_t)(kBkThr * R)) + ex;
+    }
+    __syncthreads();
+    rs_tile_scatter<R, kBkWaves>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
+}
+
+// positions of bucket items i[r] (0 <= i < the bucket's size) in A's output: the run of the
+// last chunk whose bucket offset is <= i (s_dst: exclusive prefix of the run lengths over the
+// nch chunks, then the bucket's size).  A branch-free binary search with a uniform step
+// sequence (top = the largest power of two < nch), the R searches interleaved so their LDS
+// reads are in flight together
+template <int R>
+__device__ __forceinline__ void bucket_src(const uint32_t* s_dst, const uint32_t* s_src, uint32_t nch,
+                                           uint32_t top, const uint32_t (&i)[R], uint32_t (&src)[R]) {
+    uint32_t lo[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) lo[r] = 0;
+    for (uint32_t step = top; step > 0; step >>= 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = lo[r] + step;
+            if (t < nch && s_dst[t] <= i[r]) lo[r] = t;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) src[r] = s_src[lo[r]] + (i[r] - s_dst[lo[r]]);
+}
+
+template <int R>
+__global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restrict__ kin,
+                                                         const uint32_t* __restrict__ vin,
+                                                         uint32_t* __restrict__ kout,
+                                                         uint32_t* __restrict__ vout,
+                                                         const uint32_t* __restrict__ rcnt,
+                                                         const uint32_t* __restrict__ rst, uint32_t nch,
+                                                         uint32_t CH, int lbits, uint32_t* __restrict__ nforeign,
+                                                         uint32_t skip) {
+    __shared__ uint32_t s_dst[kBkMaxChunks + 1], s_src[kBkMaxChunks];
+    __shared__ uint32_t base[kBkWaves][kRsBins];
+    __shared__ uint32_t gst[kRsBins];                 // bucket digit counts, then output positions
+    __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const uint32_t b = blockIdx.x;
+    // this bucket's run in every chunk: thread t owns chunks [t*per, t*per + per).  A chunk's
+    // run start rst[b][c] is the number of its packets in lower buckets, so the rst row also
+    // sums to the bucket's place in the output: no look-back over the other buckets
+    const uint32_t per = (nch + kBkThr - 1) / kBkThr;        // <= 4
+    const uint32_t c0 = threadIdx.x * per;
+    uint32_t part = 0, below = 0;
+    for (uint32_t q = 0; q < per; ++q) {
+        const uint32_t c = c0 + q;
+        if (c < nch) {
+            const uint32_t x = rcnt[(size_t)b * nch + c];
+            const uint32_t st0 = rst[(size_t)b * nch + c];
+            s_src[c] = c * CH + st0;
+            s_dst[c] = x;
+            part += x;
+            below += st0;
+        }
+    }
+    const uint32_t inc = wave_incl_scan(part);
+    const uint32_t bsum = wave_incl_scan(below);
+    if (lane == 63) {
+        red[wv] = inc;
+        red2[wv] = bsum;
+    }
+    __syncthreads();
+    uint32_t wpre = 0, total = 0, s0 = 0;
+#pragma unroll
+    for (int w = 0; w < kBkWaves; ++w) {
+        const uint32_t t = red[w];
+        wpre += w < wv ? t : 0u;
+        total += t;
+        s0 += red2[w];
+    }
+    uint32_t run = wpre + inc - part;                         // bucket offset of chunk c0's run
+    for (uint32_t q = 0; q < per; ++q) {
+        const uint32_t c = c0 + q;
+        if (c < nch) {
+            const uint32_t x = s_dst[c];
+            s_dst[c] = run;
+            run += x;
+        }
+    }
+    if (threadIdx.x == 0) s_dst[nch] = total;
+    __syncthreads();
+    const uint32_t cnt = total;
+    if (b == skip) {                                  // foreign packets only: left out, counted
+        if (threadIdx.x == 0) *nforeign = cnt;
+        return;
+    }
+    if (cnt == 0) return;                             // block-uniform
+    uint32_t top = 1;                                 // search steps: powers of two below nch
+    while (top * 2 < nch) top *= 2;
+    if (nch == 1) top = 0;
+    if (lbits == 0) {                                 // one-digit keys: the runs are the order
+        for (uint32_t i0 = threadIdx.x; i0 - threadIdx.x < cnt; i0 += kBkThr) {
+            const uint32_t ii[1] = {i0 < cnt ? i0 : 0u};
+            uint32_t src[1];
+            bucket_src<1>(s_dst, s_src, nch, top, ii, src);
+            if (i0 < cnt) {
+                kout[s0 + i0] = kin[src[0]];
+                vout[s0 + i0] = vin[src[0]];
+            }
+        }
+        return;
+    }
+    const uint32_t nb = 1u << lbits;
+    const uint32_t d = threadIdx.x;                   // thread d owns low digit d
+    if (d < nb) gst[d] = 0;
+    __syncthreads();
+    constexpr uint32_t kTile = (uint32_t)kBkThr * (uint32_t)R;
+    const uint32_t ntile = (cnt + kTile - 1) / kTile;
+    if (ntile > 1) {                                  // bucket digit totals -> output positions
+        for (uint32_t i = (uint32_t)wv * 64 + (uint32_t)lane; i - (uint32_t)lane < cnt; i += kBkThr) {
+            const bool ok = i < cnt;
+            const uint32_t ii[1] = {ok ? i : 0u};
+            uint32_t src[1];
+            bucket_src<1>(s_dst, s_src, nch, top, ii, src);
+            lds_count(gst, ok ? kin[src[0]] & (nb - 1) : 0u, ok);
+        }
+        __syncthreads();
+        const uint32_t x = d < nb ? gst[d] : 0u;
+        const uint32_t ex = block_digit_scan(x, red, s0);
+        if (d < nb) gst[d] = ex;
+    }
+    for (uint32_t t = 0; t < ntile; ++t) {
+        // the tile's items split evenly over the waves in order (wave w: rw rounds of 64)
+        const uint32_t tn = min(kTile, cnt - t * kTile);
+        const int rw = (int)((tn + (uint32_t)kBkThr - 1) / (uint32_t)kBkThr);
+        const uint32_t i0 = t * kTile + (uint32_t)wv * 64u * (uint32_t)rw + (uint32_t)lane;
+        const uint32_t t_end = t * kTile + tn;
+        uint32_t ii[R], src[R], k[R], v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t i = i0 + (uint32_t)r * 64u;
+            ii[r] = (r < rw && i < t_end) ? i : 0u;
+        }
+        bucket_src<R>(s_dst, s_src, nch, top, ii, src);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool ok = r < rw && i0 + (uint32_t)r * 64u < t_end;
+            k[r] = ok ? kin[src[r]] : 0u;
+            v[r] = ok ? vin[src[r]] : 0u;
+        }
+        for (uint32_t dd = lane; dd < nb; dd += 64) base[wv][dd] = 0;
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if (r < rw) lds_count(base[wv], k[r] & (nb - 1), i0 + (size_t)r * 64 < t_end);
+            if (r < rw) lds_count(base[wv], k[r] & (nb - 1), i0 + (uint32_t)r * 64u < t_end);
         __syncthreads();
-        uint32_t tc[kDPT];                          // this tile's count per digit
-#pragma unroll
-        for (int j = 0; j < kDPT; ++j) {
-            const uint32_t d = threadIdx.x + (uint32_t)j * kThr;
-            tc[j] = 0;
-            if (d < nb) {
-#pragma unroll
-                for (int w = 0; w < NW; ++w) tc[j] += base[w][d];
-                if (ntile == 1) gst[d] = tc[j];
-            }
-        }
-        if (ntile == 1) {                           // one tile: positions from its own counts
-            __syncthreads();
-            if (wv == 0) {
-                uint32_t carry = s0;
-                for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
-                    const uint32_t d = d0 + (uint32_t)lane;
-                    const uint32_t x = d < nb ? gst[d] : 0u;
-                    const uint32_t inc = wave_incl_scan(x);
-                    if (d < nb) gst[d] = carry + inc - x;
-                    carry += __builtin_amdgcn_readlane(inc, 63);
-                }
-            }
-        }
-        __syncthreads();
-        rs_tile_scatter<R, NW>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kDPT; ++j) {
-            const uint32_t d = threadIdx.x + (uint32_t)j * kThr;
-            if (d < nb) gst[d] += tc[j];
-        }
-    }
-}
-
-// ---- one-sweep slot sort (ina_set_tuning key 12 = 1; measured slower, kept for the lab)
-// The same stable LSD digit passes, without the per-pass histogram and column-scan
-// launches: the key pass also counts every pass's digits (one global histogram per pass,
-// LDS counts then one atomic per nonzero bin and block), and each digit pass is ONE
-// kernel whose blocks take tiles in ticket order (an atomic counter, so every tile a block
-// waits for has already started) and find their tile's offset per digit by decoupled
-// look-back over the earlier tiles' published counts.  Status word per (tile, digit):
-// bits 31..30 = 1 aggregate of the tile alone, 2 inclusive prefix through the tile; bits
-// 29..0 the count.  A word is self-contained (one 4-byte store), so the hand-off needs no
-// ordering: agent-scope stores (write-through) and agent-scope relaxed loads polled by the
-// waiting lanes (MI355X_MICROARCH.md, inter-workgroup visibility).  Launches per batch:
-// memset + keys + one per digit pass (2 at <= 2^18 slots) -- 4 instead of 6.  Measured at
-// 819,200 NGA-256 packets (profiles/r02/lab): each pass 26.5-27.8 us at 4,096-item tiles
-// (44 us at 1,024) against 17-18 us per scatter + 5-6 us per histogram / column scan:
-// 512 digits per tile make every tile's look-back a chain of dependent agent-scope polls,
-// so the launches it saves cost more than they did.
-constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsCnt = (1u << 30) - 1u;
-constexpr int kOsMaxPasses = 4;
-
-__device__ __forceinline__ void os_publish(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t os_poll(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// keys (slot, foreign sentinel, PS-ack bit 31) + every pass's global digit histogram, from
-// the packet headers or from the batch's descriptors (header bytes 4..11, include/ina.h)
-template <bool kDesc>
-__global__ __launch_bounds__(kRsBlock) void k_switch_keys_os(const uint8_t* __restrict__ pkts,
-                                                             const uint2* __restrict__ desc,
-                                                             size_t npk, size_t stride,
-                                                             uint32_t num_slots, int switch_id,
-                                                             uint32_t* __restrict__ keys,
-                                                             uint8_t* __restrict__ actions,
-                                                             int passes, int bits,
-                                                             uint32_t* __restrict__ ghist,
-                                                             int ack_hint) {
-    __shared__ uint32_t h[kOsMaxPasses * kRsBins];
-    const uint32_t nb = 1u << bits;
-    for (uint32_t d = threadIdx.x; d < (uint32_t)passes * nb; d += kRsBlock) h[d] = 0;
-    __syncthreads();
-    const bool al4 = (stride & 3) == 0 && ((uintptr_t)pkts & 3u) == 0;
-    const size_t gs = (size_t)gridDim.x * kRsBlock;
-    const size_t tid = (size_t)blockIdx.x * kRsBlock + threadIdx.x;
-    for (size_t w0 = tid & ~(size_t)63; w0 < npk; w0 += gs) {       // wave-uniform trip count
-        const size_t p = w0 + (threadIdx.x & 63);
-        const bool valid = p < npk;
-        uint32_t idx = 0, sid = 0, ack = 0;
-        if (!valid) {
-        } else if (kDesc) {
-            const uint2 d = desc[p];
-            idx = __builtin_bswap32((d.x >> 16) | (d.y << 16));
-            sid = (d.y >> 16) & 0xFFu;
-            ack = (d.x >> 14) & 1u;                                  // flags byte 5, bit 6
-        } else if (al4) {
-            const uint32_t* pk = reinterpret_cast<const uint32_t*>(pkts + p * stride);
-            const uint32_t w1 = pk[1], w2 = pk[2];
-            idx = __builtin_bswap32((w1 >> 16) | (w2 << 16));
-            sid = (w2 >> 16) & 0xFFu;
-            ack = (w1 >> 14) & 1u;
-        } else {
-            idx = rd_be32(pkts + p * stride + 6);
-            sid = pkts[p * stride + 10];
-            ack = (pkts[p * stride + 5] >> 6) & 1u;
-        }
-        const bool mine = switch_id >= 0 && sid == (uint32_t)(uint8_t)switch_id;
-        const uint32_t key = mine ? idx % num_slots : num_slots;
-        if (valid) {
-            keys[p] = key | ((ack_hint && mine && ack) ? kAckBit : 0u);
-            if (!mine) actions[p] = INA_ACT_FWD_OTHER;               // ngaa.p4:184-186
-        }
-        for (int q = 0; q < passes; ++q) lds_count(h + q * nb, (key >> (q * bits)) & (nb - 1), valid);
-    }
-    __syncthreads();
-    for (uint32_t d = threadIdx.x; d < (uint32_t)passes * nb; d += kRsBlock)
-        if (h[d]) atomicAdd(&ghist[d], h[d]);
-}
-
-// one digit pass: tile = 4 waves x 64 x R items, wave w owns the tile's w-th quarter in
-// rounds of 64 (the layout and in-round ballot ranks of k_rs_scatter)
-template <bool kIds, int R>
-__global__ __launch_bounds__(kRsBlock) void k_rs_onesweep(const uint32_t* __restrict__ kin,
-                                                          const uint32_t* __restrict__ vin,
-                                                          uint32_t* __restrict__ kout,
-                                                          uint32_t* __restrict__ vout, size_t n,
-                                                          int shift, int bits,
-                                                          const uint32_t* __restrict__ ghist,
-                                                          uint32_t* __restrict__ ticket,
-                                                          uint32_t* __restrict__ status) {
-    __shared__ uint32_t base[kRsWaves][kRsBins];   // per-wave counts, then per-wave bases
-    __shared__ uint32_t dbase[kRsBins];            // global digit base (scan of ghist)
-    __shared__ uint32_t tile_s;
-    const int lane = threadIdx.x & 63, wv = wave_in_block();
-    const uint32_t nb = 1u << bits;
-    if (threadIdx.x == 0) tile_s = atomicAdd(ticket, 1u);
-    for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
-    __syncthreads();
-    const size_t c = __builtin_amdgcn_readfirstlane(tile_s);
-    const size_t tile0 = c * (kRsWaves * 64 * R);
-    const size_t i0 = tile0 + (size_t)wv * (64 * R) + (size_t)lane;
-    uint32_t k[R], v[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const size_t i = i0 + (size_t)r * 64;
-        k[r] = i < n ? kin[i] : 0u;
-        v[r] = kIds ? (i < n ? vin[i] : 0u) : (uint32_t)i;
-    }
-    constexpr int kDPT = kRsBins / kRsBlock;         // digits per thread
-    uint32_t gh[kDPT];
-#pragma unroll
-    for (int j = 0; j < kDPT; ++j) {
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
-        gh[j] = d < nb ? ghist[d] : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r)              // this wave's digit counts
-        lds_count(base[wv], (k[r] >> shift) & (nb - 1), i0 + (size_t)r * 64 < n);
-#pragma unroll
-    for (int j = 0; j < kDPT; ++j) {
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
-        if (d < nb) dbase[d] = gh[j];
-    }
-    __syncthreads();
-    // publish this tile's counts, then look back for its offsets (my digits)
-    uint32_t cnt[kDPT], excl[kDPT];
-#pragma unroll
-    for (int j = 0; j < kDPT; ++j) {
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
-        cnt[j] = 0;
+        uint32_t tc = 0;                              // this tile's count of digit d
         if (d < nb) {
 #pragma unroll
-            for (int w = 0; w < kRsWaves; ++w) cnt[j] += base[w][d];
-            os_publish(status + c * nb + d, (c == 0 ? kOsInc : kOsAgg) | cnt[j]);
+            for (int w = 0; w < kBkWaves; ++w) tc += base[w][d];
         }
-    }
-    if (wv == 0) {                                   // digit bases: exclusive scan of ghist
-        uint32_t carry = 0;
-        for (uint32_t d0 = 0; d0 < nb; d0 += 64) {
-            const uint32_t d = d0 + (uint32_t)lane;
-            const uint32_t t = d < nb ? dbase[d] : 0u;
-            const uint32_t inc = wave_incl_scan(t);
-            if (d < nb) dbase[d] = carry + inc - t;
-            carry += __builtin_amdgcn_readlane(inc, 63);
+        if (ntile == 1) {                             // one tile: positions from its own counts
+            const uint32_t ex = block_digit_scan(tc, red, s0);
+            if (d < nb) gst[d] = ex;
         }
+        __syncthreads();
+        rs_tile_scatter<R, kBkWaves>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
+        __syncthreads();
+        if (d < nb) gst[d] += tc;
     }
-#pragma unroll
-    for (int j = 0; j < kDPT; ++j) {
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
-        excl[j] = 0;
-        if (d < nb && c > 0) {
-            size_t t = c - 1;
-            for (;;) {
-                const uint32_t sv = os_poll(status + t * nb + d);
-                if ((sv >> 30) == 0u) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl[j] += sv & kOsCnt;
-                if ((sv >> 30) == 2u || t == 0) break;
-                --t;
-            }
-            os_publish(status + c * nb + d, kOsInc | (excl[j] + cnt[j]));
-        }
-    }
-    __syncthreads();                                  // dbase scanned, base[][] counts final
-#pragma unroll
-    for (int j = 0; j < kDPT; ++j) {                 // the tile's first output position per digit
-        const uint32_t d = threadIdx.x + (uint32_t)j * kRsBlock;
-        if (d < nb) dbase[d] += excl[j];
-    }
-    __syncthreads();
-    rs_tile_scatter<R>(k, v, i0, n, shift, bits, base, dbase, kout, vout);
 }
 
 // 2. one wave per slot segment of the sorted stream
@@ -1340,29 +1339,37 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     return p;
 }
 
-static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
-    // sized for the SMALLEST chunk whatever tier npk falls in, so the scratch size is
-    // monotonic in npk: a buffer sized for a batch serves every smaller batch too
+// sort scratch after the four key / id arrays, sized for the SMALLEST chunk whatever tier
+// npk falls in (so the size is monotonic in npk: a buffer sized for a batch serves every
+// smaller batch): per (digit, chunk) counts -- the digit passes' histogram, or A's run
+// lengths -- and A's run starts, the digit passes' digit totals, and the size of the
+// foreign-only bucket B leaves out
+struct SortAux {
+    uint32_t* hist;               // [2^bits][nch]
+    uint32_t* rst;                // [2^bits][nch]
+    uint32_t* totals;             // [512]
+    uint32_t* nforeign;           // [1]
+};
+
+static size_t sort_hist_cap(size_t npk, uint32_t num_slots) {
     const SortPlan p = sort_plan(npk, num_slots);
     const size_t chunk = (size_t)kRsWaves * 64 * (size_t)INA_RS_ROUNDS_SMALL;
-    const size_t hist = ((size_t)1 << p.bits) * ((npk + chunk - 1) / chunk);
-    return align_up(hist * 4, 256) + align_up((size_t)kRsBins * 4, 256);
+    return ((size_t)1 << p.bits) * ((npk + chunk - 1) / chunk);
 }
 
-// one-sweep sort's auxiliary words, zeroed by one memset per batch: global digit
-// histograms [kOsMaxPasses][512], tickets (one per pass), status [passes][tiles][2^bits]
-constexpr size_t kOsHistBytes = (size_t)kOsMaxPasses * kRsBins * 4;
-constexpr int kOsMinRounds = 4;
-static size_t os_tiles(size_t npk, int rounds) {
-    const size_t tile = (size_t)kRsWaves * 64 * (size_t)rounds;
-    return (npk + tile - 1) / tile;
+static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
+    const size_t hist = align_up(sort_hist_cap(npk, num_slots) * 4, 256);
+    return 2 * hist + align_up((size_t)kRsBins * 4, 256) + 256;
 }
-static size_t os_aux_bytes(size_t npk, const SortPlan& p, int rounds) {
-    return kOsHistBytes + 256 + (size_t)p.passes * os_tiles(npk, rounds) * ((size_t)1 << p.bits) * 4;
-}
-static int os_rounds_for(size_t npk) {
-    if (const int r = g_os_rounds.load()) return r;
-    return npk <= (size_t)INA_RS_MID_ITEMS ? 4 : 8;
+
+static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
+    const size_t hist = align_up(sort_hist_cap(npk, num_slots) * 4, 256);
+    SortAux a;
+    a.hist = reinterpret_cast<uint32_t*>(aux);
+    a.rst = reinterpret_cast<uint32_t*>(aux + hist);
+    a.totals = reinterpret_cast<uint32_t*>(aux + 2 * hist);
+    a.nforeign = reinterpret_cast<uint32_t*>(aux + 2 * hist + align_up((size_t)kRsBins * 4, 256));
+    return a;
 }
 
 }  // namespace ina
@@ -1409,9 +1416,7 @@ extern "C" {
 
 size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots) {
     if (npkts == 0 || npkts > 0x7FFFFFFFu || num_slots == 0) return 256;
-    const size_t aux = std::max(sort_temp_bytes(npkts, num_slots),
-                                os_aux_bytes(npkts, sort_plan(npkts, num_slots), kOsMinRounds));
-    return 4 * align_up(npkts * 4, 256) + align_up(aux, 256) + 256;
+    return 4 * align_up(npkts * 4, 256) + align_up(sort_temp_bytes(npkts, num_slots), 256) + 256;
 }
 
 static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
@@ -1437,74 +1442,25 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     uint32_t* v_in = reinterpret_cast<uint32_t*>(base + 2 * arr);
     uint32_t* v_out = reinterpret_cast<uint32_t*>(base + 3 * arr);
     const SortPlan sp = sort_plan(npk, st->num_slots);
+    const SortAux ax = sort_aux(base + 4 * arr, npk, st->num_slots);
     // sort chunk geometry (sort_plan): one instantiation per rounds-per-wave choice
     constexpr int kR0 = INA_RS_ROUNDS_SMALL, kR1 = INA_RS_ROUNDS_MID, kR2 = kRsRounds;
-    static_assert(kR0 % 4 == 0 && kR1 % 4 == 0 && kR2 % 4 == 0, "bucket pass: 16 waves x rounds/4");
+    static_assert(kR0 % 4 == 0 && kR1 % 4 == 0 && kR2 % 4 == 0, "chunk sort: 16 waves x rounds/4");
     const int ri = sp.rounds == kR0 ? 0 : sp.rounds == kR1 ? 1 : 2;
-    auto* k_keys = desc ? (ri == 0 ? &k_switch_keys<kR0, true> : ri == 1 ? &k_switch_keys<kR1, true>
-                                                                : &k_switch_keys<kR2, true>)
-                        : (ri == 0 ? &k_switch_keys<kR0, false> : ri == 1 ? &k_switch_keys<kR1, false>
-                                                                 : &k_switch_keys<kR2, false>);
-    auto* k_hist = ri == 0 ? &k_rs_hist<kR0> : ri == 1 ? &k_rs_hist<kR1> : &k_rs_hist<kR2>;
-    auto* k_sc0 = ri == 0 ? &k_rs_scatter<false, kR0>
-                : ri == 1 ? &k_rs_scatter<false, kR1> : &k_rs_scatter<false, kR2>;
-    auto* k_sc1 = ri == 0 ? &k_rs_scatter<true, kR0>
-                : ri == 1 ? &k_rs_scatter<true, kR1> : &k_rs_scatter<true, kR2>;
-    uint32_t* hist = reinterpret_cast<uint32_t*>(base + 4 * arr);
-    uint32_t* totals = reinterpret_cast<uint32_t*>(base + 4 * arr + align_up(sp.hist_elems * 4, 256));
     const unsigned gc = (unsigned)sp.nch;
     const uint32_t nb = 1u << sp.bits;
-    const unsigned gd = (nb + kRsWaves - 1) / kRsWaves;
 
     uint32_t *kc = k_in, *vc = v_in, *kn = k_out, *vn = v_out;
     const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
                       st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
-    // keys carry the PS-ack bit for the run kernel when bit 31 is outside every digit pass
+    // keys carry the PS-ack bit for the run kernel when bit 31 is outside every digit
     const bool ack_hint = fast && sp.passes * sp.bits <= 31 && g_ack_fast.load();
     const bool small = npk <= (size_t)g_small_sort.load();
-    const bool onesweep = !small && g_sort_mode.load() == 1 && npk < ((size_t)1 << 30);
-    // bucket + local sort: two-digit keys only (the low digit is one workgroup's LDS bins)
-    const int mode = g_sort_mode.load();
-    const bool hybrid = !small && (mode == 0 || mode == 2) && sp.passes == 2;
-    uint32_t skip_bucket = 0xFFFFFFFFu;
+    // chunk + bucket sort: keys of one or two digits (the low digit is one workgroup's LDS
+    // bins) and at most kBkMaxChunks chunks (B's LDS rows); else the digit passes
+    const bool bucket = !small && g_sort_mode.load() == 0 && sp.passes <= 2 && sp.nch <= (size_t)kBkMaxChunks;
     const uint32_t* nforeign = nullptr;
-    if (onesweep) {
-        // memset(aux) + keys/histograms + one kernel per digit pass
-        const int R = os_rounds_for(npk);
-        const size_t ntiles = os_tiles(npk, R);
-        uint8_t* aux = base + 4 * arr;
-        uint32_t* ghist = reinterpret_cast<uint32_t*>(aux);
-        uint32_t* tickets = reinterpret_cast<uint32_t*>(aux + kOsHistBytes);
-        uint32_t* status = reinterpret_cast<uint32_t*>(aux + kOsHistBytes + 256);
-        if (hipMemsetAsync(aux, 0, os_aux_bytes(npk, sp, R), s) != hipSuccess)
-            return set_error(INA_EHIP, "switch sort memset%s", "");
-        const unsigned gk = (unsigned)std::min<size_t>((npk + kRsBlock * 8 - 1) / (kRsBlock * 8), 2048);
-        if (desc)
-            hipLaunchKernelGGL(k_switch_keys_os<true>, dim3(gk), dim3(kRsBlock), 0, s, pkts,
-                               reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
-                               st->switch_id, kc, actions, sp.passes, sp.bits, ghist, ack_hint ? 1 : 0);
-        else
-            hipLaunchKernelGGL(k_switch_keys_os<false>, dim3(gk), dim3(kRsBlock), 0, s, pkts,
-                               static_cast<const uint2*>(nullptr), npk, stride, st->num_slots,
-                               st->switch_id, kc, actions, sp.passes, sp.bits, ghist, ack_hint ? 1 : 0);
-        for (int pass = 0; pass < sp.passes; ++pass) {
-            const int shift = pass * sp.bits;
-            const uint32_t* gh = ghist + (size_t)pass * nb;
-            uint32_t* stp = status + (size_t)pass * ntiles * nb;
-#define INA_OS_LAUNCH(IDS, RR)                                                                        \
-            hipLaunchKernelGGL((k_rs_onesweep<IDS, RR>), dim3((unsigned)ntiles), dim3(kRsBlock), 0, s, \
-                               kc, vc, kn, vn, npk, shift, sp.bits, gh, tickets + pass, stp)
-            if (pass == 0) {
-                if (R == 4) INA_OS_LAUNCH(false, 4); else if (R == 8) INA_OS_LAUNCH(false, 8); else INA_OS_LAUNCH(false, 16);
-            } else {
-                if (R == 4) INA_OS_LAUNCH(true, 4); else if (R == 8) INA_OS_LAUNCH(true, 8); else INA_OS_LAUNCH(true, 16);
-            }
-#undef INA_OS_LAUNCH
-            if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
-            std::swap(kc, kn);
-            std::swap(vc, vn);
-        }
-    } else if (small && fast && npk <= (size_t)g_tiny_max.load()) {
+    if (small && fast && npk <= (size_t)g_tiny_max.load()) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
         uint32_t win = (uint32_t)INA_SWITCH_WIN_SMALL;
         if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
@@ -1527,63 +1483,68 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             hipLaunchKernelGGL((k_switch_sort_small<unsigned long long, 32>), dim3(1), dim3(kSmallBlock), 0,
                                s, pkts, (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
-    } else if (hybrid) {
-        // high digit (bits lb..eb-1) over the whole batch, then each bucket on its low digit.
-        // The high pass's chunks (4 waves x 64 x rounds items) run as 16 waves x rounds/4,
-        // so each wave's dependent LDS-count / rank rounds are 4x fewer
-        const int lb = end_bit_for(st->num_slots) - sp.bits;
-        constexpr int kHw = 16;
-        const dim3 hb(kHw * 64);
+    } else if (bucket) {
+        // A: keys + each chunk sorted by the high digit (bits lb..eb-1) -> (kn, vn) and the
+        // per (digit, chunk) run lengths / starts; B: each bucket gathered in chunk order and
+        // sorted on its low digit -> (kc, vc)
+        const int eb = end_bit_for(st->num_slots);
+        const int lb = eb - sp.bits;                       // low digit bits (0: one-digit keys)
         const uint2* dsc = reinterpret_cast<const uint2*>(desc);
-        if (sp.rounds == kR2) {
-            hipLaunchKernelGGL((desc ? &k_switch_keys<kR2 / 4, true, kHw> : &k_switch_keys<kR2 / 4, false, kHw>),
-                               dim3(gc), hb, 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id, kc,
-                               actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
-        } else if (sp.rounds == kR1) {
-            hipLaunchKernelGGL((desc ? &k_switch_keys<kR1 / 4, true, kHw> : &k_switch_keys<kR1 / 4, false, kHw>),
-                               dim3(gc), hb, 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id, kc,
-                               actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
-        } else {
-            hipLaunchKernelGGL((desc ? &k_switch_keys<kR0 / 4, true, kHw> : &k_switch_keys<kR0 / 4, false, kHw>),
-                               dim3(gc), hb, 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id, kc,
-                               actions, sp.bits, lb, hist, sp.nch, ack_hint ? 1 : 0);
-        }
-        hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, hist, sp.nch, nb, totals);
-        auto* k_hs = sp.rounds == kR2 ? &k_rs_scatter<false, kR2 / 4, kHw>
-                   : sp.rounds == kR1 ? &k_rs_scatter<false, kR1 / 4, kHw> : &k_rs_scatter<false, kR0 / 4, kHw>;
-        hipLaunchKernelGGL(k_hs, dim3(gc), hb, 0, s, kc, nullptr, kn, vn, npk, lb, sp.bits, hist, totals, sp.nch);
-        // a bucket of foreign packets only (a pool of a multiple of 2^lb slots): left where the
-        // high pass put them when the register-resident run kernel takes the batch (it stops
-        // before them); the generic run kernel reads every position, so then it is sorted
+        const int ah = ack_hint ? 1 : 0;
+#define INA_A_LAUNCH(RR)                                                                              \
+        hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true> : &k_sort_chunks<RR, false>), dim3(gc),   \
+                           dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id,  \
+                           actions, sp.bits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah)
+        if (ri == 2) INA_A_LAUNCH(kR2 / 4);
+        else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
+        else INA_A_LAUNCH(kR0 / 4);
+#undef INA_A_LAUNCH
+        // the bucket of foreign packets only (a pool of a multiple of 2^lb slots) is left out
+        // when the register-resident run kernel takes the batch (it stops before them); the
+        // generic run kernel reads every position, so then it is gathered like the others
+        uint32_t skip = 0xFFFFFFFFu;
         if (fast && (st->num_slots & ((1u << lb) - 1u)) == 0u) {
-            skip_bucket = st->num_slots >> lb;
-            nforeign = totals + skip_bucket;
+            skip = st->num_slots >> lb;
+            nforeign = ax.nforeign;
         }
-        hipLaunchKernelGGL((k_rs_local<kLcWaves, kLcRounds>), dim3(nb), dim3(kLcWaves * 64), 0, s, kn, vn, kc, vc, lb,
-                           totals, skip_bucket);
+        const uint32_t CH = (uint32_t)kRsWaves * 64u * (uint32_t)sp.rounds;
+        hipLaunchKernelGGL((k_sort_buckets<kLcRounds>), dim3(nb), dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist,
+                           ax.rst, (uint32_t)sp.nch, CH, lb, ax.nforeign, skip);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
+        // LSD digit passes (keys of three digits, batches beyond B's rows, or key 12 = 3):
+        // keys + pass-0 histogram, then per pass a column scan and a scatter
+        auto* k_keys = desc ? (ri == 0 ? &k_switch_keys<kR0, true> : ri == 1 ? &k_switch_keys<kR1, true>
+                                                                    : &k_switch_keys<kR2, true>)
+                            : (ri == 0 ? &k_switch_keys<kR0, false> : ri == 1 ? &k_switch_keys<kR1, false>
+                                                                     : &k_switch_keys<kR2, false>);
+        auto* k_hist = ri == 0 ? &k_rs_hist<kR0> : ri == 1 ? &k_rs_hist<kR1> : &k_rs_hist<kR2>;
+        auto* k_sc0 = ri == 0 ? &k_rs_scatter<false, kR0>
+                    : ri == 1 ? &k_rs_scatter<false, kR1> : &k_rs_scatter<false, kR2>;
+        auto* k_sc1 = ri == 0 ? &k_rs_scatter<true, kR0>
+                    : ri == 1 ? &k_rs_scatter<true, kR1> : &k_rs_scatter<true, kR2>;
+        const unsigned gd = (nb + kRsWaves - 1) / kRsWaves;
         hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
                            reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
-                           st->switch_id, k_in, actions, sp.bits, 0, hist, sp.nch, ack_hint ? 1 : 0);
+                           st->switch_id, k_in, actions, sp.bits, 0, ax.hist, sp.nch, ack_hint ? 1 : 0);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
-    }
-    // r01 digit passes: (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
-    for (int pass = 0; pass < (small || onesweep || hybrid ? 0 : sp.passes); ++pass) {
-        const int shift = pass * sp.bits;
-        if (pass > 0)
-            hipLaunchKernelGGL(k_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits, hist,
-                               sp.nch);
-        hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, hist, sp.nch, nb, totals);
-        if (pass == 0)
-            hipLaunchKernelGGL(k_sc0, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn, vn, npk, shift,
-                               sp.bits, hist, totals, sp.nch);
-        else
-            hipLaunchKernelGGL(k_sc1, dim3(gc), dim3(kRsBlock), 0, s, kc, vc, kn, vn, npk, shift,
-                               sp.bits, hist, totals, sp.nch);
-        if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
-        std::swap(kc, kn);
-        std::swap(vc, vn);
+        // (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
+        for (int pass = 0; pass < sp.passes; ++pass) {
+            const int shift = pass * sp.bits;
+            if (pass > 0)
+                hipLaunchKernelGGL(k_hist, dim3(gc), dim3(kRsBlock), 0, s, kc, npk, shift, sp.bits, ax.hist,
+                                   sp.nch);
+            hipLaunchKernelGGL(k_rs_colscan, dim3(gd), dim3(kRsBlock), 0, s, ax.hist, sp.nch, nb, ax.totals);
+            if (pass == 0)
+                hipLaunchKernelGGL(k_sc0, dim3(gc), dim3(kRsBlock), 0, s, kc, nullptr, kn, vn, npk, shift,
+                                   sp.bits, ax.hist, ax.totals, sp.nch);
+            else
+                hipLaunchKernelGGL(k_sc1, dim3(gc), dim3(kRsBlock), 0, s, kc, vc, kn, vn, npk, shift,
+                                   sp.bits, ax.hist, ax.totals, sp.nch);
+            if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
+            std::swap(kc, kn);
+            std::swap(vc, vn);
+        }
     }
     if (fast) {
         // a wave runs the segments that start in its window of `win` sorted positions: a

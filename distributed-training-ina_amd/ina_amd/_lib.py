@@ -85,6 +85,7 @@ SIGNATURES = {
     "ina_route_ipv4": [_vp, _vp, _u32, _sz, _vp, _vp, _i, _vp, _vp],
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],
     "ina_absmax_f32": [_vp, _vp, _sz, _vp, _vp],
+    "ina_absmax_multi_f32": [_vp, _i, _vp, _sz, _vp, _vp],
     "ina_scale_for": [C.c_float, _i, _i, C.POINTER(C.c_int)],
     "ina_host_reduce_scratch_bytes": [_i, _sz],
     "ina_sum_reduce_host_i32": [_vp, _i, _vp, _sz, _sz, _vp, _vp],

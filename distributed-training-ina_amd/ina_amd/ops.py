@@ -463,11 +463,29 @@ def scale_for(amax: float, W: int, bits: int = 32) -> int:
     return k.value
 
 
+def absmax_multi(xs, base: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    """Device float32 [1] = max_w,i |xs[w][i] - base[i]| over W buckets in ONE pass
+    (ina_absmax_multi_f32: each base chunk is read once for all W workers)."""
+    xs, n = _bufs(xs, torch.float32, "xs")
+    if base is not None:
+        _req(base, torch.float32, "base")
+        if base.numel() != n:
+            raise ValueError("base and xs differ in length")
+        _same_device(xs[0], base)
+    out = torch.empty(1, dtype=torch.float32, device=xs[0].device) if out is None else out
+    _fits(out, 1)
+    _req(out, torch.float32, "out")
+    arr = ptr_array([x.data_ptr() for x in xs])
+    check(load().ina_absmax_multi_f32(arr, len(xs), base.data_ptr() if base is not None else None,
+                                      n, out.data_ptr(), _stream(xs[0])), "absmax_multi")
+    return out
+
+
 def scale_for_workers(xs, base: torch.Tensor | None = None, bits: int = 32) -> int:
-    """k for W device buckets (deltas against `base` when given): one absmax kernel per
-    bucket, one host read of the maximum."""
+    """k for W device buckets (deltas against `base` when given): one absmax_multi pass over
+    all W buckets, one host read of the maximum."""
     xs = list(xs)
-    m = torch.cat([absmax(x, base) for x in xs]).max()
+    m = absmax_multi(xs, base)
     return scale_for(float(m.item()), len(xs), bits)
 
 
@@ -585,17 +603,18 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     PS combine, combine_ina_blocks the INA-semantics combine, h2d_streams the host-ingest
     pipeline's H2D copy streams (1 or 2), launch_chunks the 16-byte chunks one flat packet
     kernel launch covers (default 2^31 - 1; smaller values only split launches),
-    switch_small_sort the one-workgroup key+sort path for small switch batches (False: off,
-    True: up to the default 768 packets, an int: up to that many, at most 2048),
+    switch_small_sort the one-workgroup key+sort path for small switch batches (False or 0:
+    off; True or 1: the default threshold, 768 packets -- 1 is the C ABI's sentinel for
+    the default, not "batches of one packet"; an int 2..2048: up to that many),
     switch_window the sorted positions one wave of the switch run kernel owns (0 = auto,
     1..64), switch_ack_fast the lane-parallel path for PS acks alone in their slot's
-    segment, switch_sort the slot sort (0 auto = bucket + local where the keys have two
-    digits, 1 one-sweep passes with decoupled look-back, 2 bucket + local, 3 histogram /
-    column-scan / scatter digit passes), switch_sort_rounds the sort tile of either
-    sort (64-item rounds per wave: 0 auto, 4, 8, 16), ew_blocks the grid cap of the one-in
-    one-out elementwise kernels (default 2^24: one 16-byte chunk per thread),
+    segment, switch_sort the slot sort (0 auto = chunk + bucket sort where the keys have
+    one or two digits, 3 the LSD digit passes for every batch), switch_sort_rounds the
+    sort chunk (64-item rounds per wave: 0 auto, 4, 8, 16), ew_blocks the grid cap of the
+    one-in one-out elementwise kernels (default 2^24: one 16-byte chunk per thread),
     switch_tiny_max the largest batch the switch sorts and runs in ONE launch of one
-    workgroup (0 = off, at most 2048); unroll is the
+    workgroup (0 = off, at most 2048) -- only batches that take the small-sort path at all
+    reach it, so it is capped by switch_small_sort's threshold; unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
@@ -611,8 +630,7 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     if launch_chunks is not None:
         check(lib.ina_set_tuning(8, int(launch_chunks)), "set_tuning")
     if switch_small_sort is not None:
-        v = int(switch_small_sort) if not isinstance(switch_small_sort, bool) else int(switch_small_sort)
-        check(lib.ina_set_tuning(9, v), "set_tuning")
+        check(lib.ina_set_tuning(9, int(switch_small_sort)), "set_tuning")   # True -> 1: the default
     if switch_window is not None:
         check(lib.ina_set_tuning(10, int(switch_window)), "set_tuning")
     if switch_ack_fast is not None:

@@ -69,11 +69,12 @@ const char* ina_last_error_string(void);
  * 8 16-byte chunks per flat packet-kernel launch, 9 largest switch batch for the
  * one-workgroup sort (0 never, 1 default 768, 2..2048), 10 switch run-kernel window in sorted positions (0 = auto, 1..64),
  * 11 switch lane-parallel path for PS acks alone in their slot's segment (0/1), 12 switch
- * slot sort (0 auto = bucket + local for two-digit keys, 1 one-sweep passes with decoupled
- * look-back, 2 bucket + local, 3 histogram / column-scan / scatter digit passes),
- * 13 slot-sort tile rounds per wave (0 auto, 4, 8, 16), 14 grid cap
- * of the one-in one-out elementwise kernels (quantise, dequantise, PS apply, int16 wire),
- * 15 largest switch batch sorted and run in ONE launch of one workgroup (0 = off, <= 2048).
+ * slot sort (0 auto = chunk + bucket sort for keys of one or two digits, else the LSD digit
+ * passes; 3 the digit passes for every batch), 13 slot-sort chunk rounds per wave (0 auto,
+ * 4, 8, 16), 14 grid cap of the one-in one-out elementwise kernels (quantise, dequantise,
+ * PS apply, int16 wire), 15 largest switch batch sorted and run in ONE launch of one
+ * workgroup (0 = off, <= 2048; it applies only to batches that also take key 9's
+ * one-workgroup path, so it is capped by key 9's threshold).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 
@@ -97,6 +98,10 @@ int ina_dequantize_i16_f32(const int16_t* s, float* y, size_t n, int k, ina_stre
  * sum saturates (bits = 32, or 16 for the int16 wire); absmax 0 gives 127.  *k_out gets
  * k; INA_EINVAL for absmax negative, NaN or infinite, W < 1, or W too large for the width. */
 int ina_absmax_f32(const float* x, const float* base, size_t n, float* out_dev, ina_stream_t stream);
+/* The same over W (1..64) worker buckets in ONE pass: *out_dev = max_w,i |xs[w][i] - base[i]|
+ * (each base chunk read once for all W workers) -- what ina_scale_for takes for W workers. */
+int ina_absmax_multi_f32(const float* const* xs, int W, const float* base, size_t n, float* out_dev,
+                         ina_stream_t stream);
 int ina_scale_for(float absmax, int W, int bits, int* k_out);
 
 /* ---- the aggregator ------------------------------------------------------------

@@ -149,6 +149,7 @@ def _einval_cases():
         "ina_route_ipv4": (None, None, 0, 4, None, None, 1, None, None),
         "ina_checksum_i32": (None, 64, None, None),
         "ina_absmax_f32": (None, None, 64, None, None),
+        "ina_absmax_multi_f32": (P([None, None]), 2, None, 64, None, None),
         "ina_sum_reduce_host_i32": (P([None, None]), 2, None, 64, 0, None, None),
     }
 
@@ -190,7 +191,9 @@ def test_set_tuning_rejects_unknown_keys_and_values():
     assert lib.ina_set_tuning(10, 65) == _lib.INA_EINVAL        # switch window <= 64
     assert lib.ina_set_tuning(10, 0) == _lib.INA_OK             # 0 = automatic
     assert lib.ina_set_tuning(11, 1) == _lib.INA_OK
-    assert lib.ina_set_tuning(12, 4) == _lib.INA_EINVAL        # sort: 0 auto, 1 one-sweep, 2 bucket, 3 passes
+    assert lib.ina_set_tuning(12, 4) == _lib.INA_EINVAL        # sort: 0 auto, 3 digit passes
+    assert lib.ina_set_tuning(12, 1) == _lib.INA_EINVAL        # one-sweep: moved to tools/lab
+    assert lib.ina_set_tuning(12, 2) == _lib.INA_EINVAL
     assert lib.ina_set_tuning(12, 3) == _lib.INA_OK
     assert lib.ina_set_tuning(15, 4096) == _lib.INA_EINVAL      # tiny path: 0..2048 packets
     assert lib.ina_set_tuning(15, 512) == _lib.INA_OK

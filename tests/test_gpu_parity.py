@@ -312,6 +312,29 @@ def test_absmax_matches_numpy(n, with_base):
     assert got.view(np.uint32) == want.view(np.uint32)
 
 
+@pytest.mark.parametrize("W", [1, 3, 4, 5, 16])
+@pytest.mark.parametrize("n", [1, 6, 1023, 100_003])
+@pytest.mark.parametrize("with_base", [False, True])
+def test_absmax_multi_equals_max_of_single(W, n, with_base):
+    """ina_absmax_multi_f32 (one pass over W buckets, base read once) == the max of the W
+    single-bucket absmax values, bit for bit; NaN ignored, +-inf counted; W not a multiple
+    of the kernel's 4-worker groups, aligned and tail elements."""
+    rng = np.random.default_rng(W * 1000 + n + with_base)
+    xs = [mixed_floats(rng, n) for _ in range(W)]
+    base = (rng.standard_normal(n) * 3).astype(np.float32) if with_base else None
+    o = ops()
+    db = dev(base) if with_base else None
+    got = host(o.absmax_multi([dev(x) for x in xs], db))[0]
+    want = max(host(o.absmax(dev(x), db))[0] for x in xs)
+    assert got.view(np.uint32) == np.float32(want).view(np.uint32)
+    # an unaligned view takes the element path
+    got_u = host(o.absmax_multi([dev(x)[1:] if n > 1 else dev(x) for x in xs],
+                                (db[1:] if n > 1 else db) if with_base else None))[0]
+    want_u = max(host(o.absmax(dev(x)[1:] if n > 1 else dev(x),
+                               (db[1:] if n > 1 else db) if with_base else None))[0] for x in xs)
+    assert got_u.view(np.uint32) == np.float32(want_u).view(np.uint32)
+
+
 def test_absmax_unaligned_view_and_finite_pick():
     rng = np.random.default_rng(3)
     x = (rng.standard_normal(10_001) * 5).astype(np.float32)
@@ -572,20 +595,20 @@ def test_switch_fuzz_vs_oracle(seed):
     assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
 
 
-# slot sort variants: (sort 0 = auto / 1 = one-sweep / 2 = bucket + local / 3 = r01
-# histogram passes, descriptors, tile rounds)
-SORT_VARIANTS = [(3, True, 0), (3, False, 0), (1, False, 4), (1, True, 16), (1, False, 8),
-                 (2, True, 0), (2, False, 0), (0, True, 0)]
+# slot sort variants: (sort 0 = auto: chunk + bucket for keys of one or two digits / 3 = the
+# LSD digit passes, descriptors, chunk rounds)
+SORT_VARIANTS = [(3, True, 0), (3, False, 0), (0, False, 4), (0, True, 16), (0, False, 8),
+                 (0, True, 0), (0, False, 0), (3, True, 8)]
 
 
 @pytest.mark.parametrize("variant", SORT_VARIANTS)
 @pytest.mark.parametrize("seed", range(8))
 def test_switch_sort_paths_vs_oracle(seed, variant):
     """Batches above the one-workgroup size (> 2,048 packets) through each slot sort --
-    bucket + local (the default for 2^10..2^18-slot pools), the one-sweep passes (decoupled look-back; tiles of 1,024 / 2,048 / 4,096 items; keys
-    from the packet headers or from the batch's descriptors) and the r01 histogram /
-    column-scan / scatter passes -- bit-exact against the P4 restatement, state carried
-    across batches, pools of 1 .. 2^18 slots (1-3 digit passes)."""
+    the chunk + bucket sort (the default for pools of < 2^18 slots; chunks of 1,024 / 2,048
+    / 4,096 packets; keys from the packet headers or from the batch's descriptors) and the
+    LSD histogram / column-scan / scatter digit passes -- bit-exact against the P4
+    restatement, state carried across batches, pools of 1 .. 2^18 slots (keys of 1-3 digits)."""
     sort, use_desc, rounds = variant
     rng = np.random.default_rng(40_000 + seed)
     o = ops()
@@ -624,15 +647,15 @@ def test_switch_sort_paths_vs_oracle(seed, variant):
         o.set_tuning(switch_sort=0, switch_sort_rounds=0)
 
 
-@pytest.mark.parametrize("sort", [3, 2])
+@pytest.mark.parametrize("sort", [3, 0])
 @pytest.mark.parametrize("case", ["one_bucket", "one_slot", "two_buckets", "foreign_heavy"])
 def test_switch_skewed_buckets_vs_oracle(sort, case):
     """Slot use concentrated in one or two sort buckets (2^8 consecutive slots of a 2^17
-    pool), so a bucket holds more than one 4,096-item tile and the bucket + local sort takes
+    pool), so a bucket holds more than one 4,096-item tile and the chunk + bucket sort takes
     its multi-tile path (a counting sweep, then the tiles in order); one case puts every
     packet in ONE slot (a segment of > 4,096 packets), one is 70 % foreign packets (their
     bucket is left unsorted at the end and the run kernel stops before it).  Bit-exact against the P4
-    restatement with state carried across batches, for the bucket sort and the r01 passes."""
+    restatement with state carried across batches, for the bucket sort and the digit passes."""
     rng = np.random.default_rng({"one_bucket": 1, "one_slot": 2, "two_buckets": 3, "foreign_heavy": 4}[case])
     o = ops()
     V, num_slots, W = 32, 1 << 17, 16
@@ -664,11 +687,11 @@ def test_switch_bucket_sort_pool_edges(num_slots):
     """Pool sizes at the bucket sort's digit-split edges (2^9+1 .. 2^18-1 slots: high / low
     digits of 5..9 bits, pools that are and are not a multiple of the bucket width, i.e.
     with and without the unsorted foreign-only bucket), 30 % foreign packets and PS acks:
-    bucket + local and the r01 digit passes both bit-exact against the P4 restatement."""
+    the chunk + bucket sort and the LSD digit passes both bit-exact against the P4 restatement."""
     o = ops()
     V, W = 32, 8
     res = {}
-    for sort in (2, 3):
+    for sort in (0, 3):
         rng = np.random.default_rng(num_slots)
         o.set_tuning(switch_sort=sort)
         try:
