@@ -3,11 +3,13 @@
 // At the PS, worker gradients arrive from sockets into host memory and the aggregate
 // leaves on a socket (north star; the reference's PS receives pickled tensors,
 // worker.py:63-79 / launch.py:111-130, and sums them on the CPU, launch.py:42-52).
-// ina_sum_reduce_host_i32 moves W pinned host buckets through HBM in chunks: H2D
-// copies on one or two copy streams (workers alternate), the W-way sum-reduce on the
-// caller's stream, D2H of the aggregate on another, over a ring of kSlots device
-// slots, so the two copy directions and the reduce overlap and the run approaches
-// the PCIe link rate instead of the sum of the three phases.
+// ina_sum_reduce_host_i32: when every bucket and the output are pinned, device-mapped host
+// memory, ONE launch of the W-way reduce reads the buckets over PCIe and writes the
+// aggregate back over PCIe (zero copy); otherwise it moves the buckets through HBM in
+// chunks: H2D copies on one or two copy streams (workers alternate), the W-way sum-reduce
+// on the caller's stream, D2H of the aggregate on another, over a ring of kSlots device
+// slots, so the two copy directions and the reduce overlap and the run approaches the
+// PCIe link rate instead of the sum of the three phases.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -75,6 +77,9 @@ thread_local HostPipe t_pipe;
 // ina_set_tuning key 7: H2D copy streams; two (workers alternate) measured faster at
 // every chunk size (15.1 vs 16.0 ms at 4 Mi values: the link, ~55.6 GB/s H2D, is the bound)
 int g_h2d_streams = 2;
+// ina_set_tuning key 16: 1 (default) reduce device-mapped pinned buffers in place over PCIe,
+// 0 always the chunked copy pipeline (tests run both)
+int g_zero_copy = 1;
 
 size_t chunk_for(size_t chunk_values) {
     size_t c = chunk_values ? chunk_values : kDefaultChunk;
@@ -84,6 +89,11 @@ size_t chunk_for(size_t chunk_values) {
 }  // namespace
 
 namespace ina {
+int set_zero_copy(int v) {
+    if (v != 0 && v != 1) return INA_EINVAL;
+    g_zero_copy = v;
+    return INA_OK;
+}
 int set_h2d_streams(int v) {
     if (v != 1 && v != 2) return INA_EINVAL;
     g_h2d_streams = v;
@@ -115,6 +125,28 @@ int ina_sum_reduce_host_i32(const int32_t* const* host_bufs, int W, int32_t* hos
         return set_error(INA_EHIP, "copy stream/event creation%s", "");
     }
     hipStream_t cs = reinterpret_cast<hipStream_t>(stream);
+    // pinned (device-mapped) host buckets and output: no staging at all -- the reduce
+    // kernel's loads and stores cross PCIe themselves (GPU-initiated reads of the workers'
+    // buckets, writes of the aggregate), one launch; 55.7-56.5 GB/s against 54.2 GB/s for
+    // the chunked copy pipeline and 56.4 GB/s for plain H2D copies of the same 8 x 100 MiB
+    // (tools/lab/zerocopy_lab.py, profiles/r03/lab).  Pageable memory takes the pipeline.
+    if (g_zero_copy) {
+        const int32_t* dptr[INA_MAX_WORKERS];
+        void* dout = nullptr;
+        bool mapped = hipHostGetDevicePointer(&dout, host_out, 0) == hipSuccess;
+        for (int w = 0; w < W && mapped; ++w) {
+            void* p = nullptr;
+            mapped = hipHostGetDevicePointer(&p, const_cast<int32_t*>(host_bufs[w]), 0) == hipSuccess;
+            dptr[w] = static_cast<const int32_t*>(p);
+        }
+        if (mapped) {
+            if (int rc = ina::sum_reduce_i32_impl(dptr, W, static_cast<int32_t*>(dout), n, stream, true))
+                return rc;
+            if (hipStreamSynchronize(cs) != hipSuccess) return set_error(INA_EHIP, "zero-copy reduce sync%s", "");
+            return INA_OK;
+        }
+        (void)hipGetLastError();               // a refused query is not an error of this call
+    }
     const size_t c = chunk_for(chunk_values);
     const size_t nchunks = (n + c - 1) / c;
     int32_t* base = reinterpret_cast<int32_t*>(dev_scratch);

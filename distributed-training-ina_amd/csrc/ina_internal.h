@@ -15,6 +15,7 @@ struct PtrPack {
 
 int set_error(int code, const char* fmt, const char* detail);
 int set_h2d_streams(int v);   // ina_host.cpp
+int set_zero_copy(int v);     // ina_host.cpp
 int sum_reduce_i32_impl(const int32_t* const* bufs, int W, int32_t* out, size_t n, ina_stream_t stream,
                         bool host);   // ina_kernels.hip
 int set_small_sort(int v);    // ina_switch.hip

@@ -1567,6 +1567,7 @@ int ina_set_tuning(int key, int value) {
         case 12: return set_sort_mode(value);
         case 13: return set_os_rounds(value);
         case 15: return set_tiny_max(value);
+        case 16: return set_zero_copy(value);
         default: return INA_EINVAL;
     }
 }
@@ -1696,7 +1697,10 @@ int ina_quantize_reduce_f32_i32(const float* const* bufs, int W, int32_t* out, s
     if (W == 1) return ina_quantize_f32_i32(bufs[0], out, n, k, stream);
     int vec = al && aligned16(out);
     float sc = ldexpf(1.0f, k);
-    unsigned g = grid_for(vec ? n / 4 + 1 : n, W <= 8 ? INA_QR_U : 2, g_stream_blocks);
+    // W <= 8: one 16-byte chunk per stream per thread and a grid covering the bucket (C2,
+    // back to back: 86.2 us against 88.7 at 8192 workgroups and 87.9-96.7 at 256-2048,
+    // tools/lab/ew16_lab.py, profiles/r03/lab/ew16_lab.log); more streams stride
+    unsigned g = grid_for(vec ? n / 4 + 1 : n, W <= 8 ? INA_QR_U : 2, W <= 8 ? g_ew_blocks.load() : g_stream_blocks.load());
     hipStream_t s = hs(stream);
     switch (W) {
         case 2: hipLaunchKernelGGL(k_quant_reduce_i32<2>, dim3(g), dim3(kBlock), 0, s, pk, W, out, n, sc, vec); break;

@@ -520,7 +520,7 @@ __global__ __launch_bounds__(NW * 64) void k_rs_scatter(const uint32_t* __restri
 #endif
 constexpr int kBkWaves = INA_BK_WAVES;
 constexpr int kBkThr = kBkWaves * 64;
-constexpr int kBkMaxChunks = 4096;                  // B's LDS rows: up to 4096 x CH packets
+constexpr int kBkMaxChunks = 2048;                  // B's LDS rows: up to 2048 x CH packets
 constexpr int kLcRounds = 64 / kBkWaves > 4 ? 64 / kBkWaves : 4;   // B's tile: max(4096, 256 x waves) items
 
 // key fields of R rounds of 64 packets (all loads issued first): slot index, switch id and
@@ -626,6 +626,17 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     rs_tile_scatter<R, kBkWaves>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
 }
 
+#ifndef INA_BK_TIMING
+#define INA_BK_TIMING 0
+#endif
+#if INA_BK_TIMING
+// lab builds only: per-block wall-clock stamps of k_sort_buckets' phases (tools/lab)
+__device__ unsigned long long g_bk_t[kRsBins][6];
+#define BK_STAMP(q) do { if (threadIdx.x == 0) g_bk_t[blockIdx.x][q] = wall_clock64(); } while (0)
+#else
+#define BK_STAMP(q) do { } while (0)
+#endif
+
 // positions of bucket items i[r] (0 <= i < the bucket's size) in A's output: the run of the
 // last chunk whose bucket offset is <= i (s_dst: exclusive prefix of the run lengths over the
 // nch chunks, then the bucket's size).  A branch-free binary search with a uniform step
@@ -663,6 +674,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const uint32_t b = blockIdx.x;
+    BK_STAMP(0);
     // this bucket's run in every chunk: thread t owns chunks [t*per, t*per + per).  A chunk's
     // run start rst[b][c] is the number of its packets in lower buckets, so the rst row also
     // sums to the bucket's place in the output: no look-back over the other buckets
@@ -706,6 +718,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
     }
     if (threadIdx.x == 0) s_dst[nch] = total;
     __syncthreads();
+    BK_STAMP(1);
     const uint32_t cnt = total;
     if (b == skip) {                                  // foreign packets only: left out, counted
         if (threadIdx.x == 0) *nforeign = cnt;
@@ -771,6 +784,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
         for (int r = 0; r < R; ++r)
             if (r < rw) lds_count(base[wv], k[r] & (nb - 1), i0 + (uint32_t)r * 64u < t_end);
         __syncthreads();
+        BK_STAMP(2);
         uint32_t tc = 0;                              // this tile's count of digit d
         if (d < nb) {
 #pragma unroll
@@ -781,8 +795,10 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
             if (d < nb) gst[d] = ex;
         }
         __syncthreads();
+        BK_STAMP(3);
         rs_tile_scatter<R, kBkWaves>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
         __syncthreads();
+        BK_STAMP(4);
         if (d < nb) gst[d] += tc;
     }
 }
@@ -1414,6 +1430,12 @@ using namespace ina;
 
 extern "C" {
 
+#if INA_BK_TIMING
+int ina_lab_bk_times(unsigned long long* host_out) {   // lab builds only
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bk_t), sizeof(g_bk_t)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots) {
     if (npkts == 0 || npkts > 0x7FFFFFFFu || num_slots == 0) return 256;
     return 4 * align_up(npkts * 4, 256) + align_up(sort_temp_bytes(npkts, num_slots), 256) + 256;
@@ -1508,7 +1530,10 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             nforeign = ax.nforeign;
         }
         const uint32_t CH = (uint32_t)kRsWaves * 64u * (uint32_t)sp.rounds;
-        hipLaunchKernelGGL((k_sort_buckets<kLcRounds>), dim3(nb), dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist,
+        // buckets past the sentinel's (num_slots >> lb) are always empty: no block for them,
+        // so at 2^17 slots 257 blocks (one per CU, one generation) instead of 512
+        const unsigned gb = std::min<unsigned>(nb, (st->num_slots >> lb) + 1u);
+        hipLaunchKernelGGL((k_sort_buckets<kLcRounds>), dim3(gb), dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist,
                            ax.rst, (uint32_t)sp.nch, CH, lb, ax.nforeign, skip);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {

@@ -170,10 +170,11 @@ def sum_reduce(bufs, out: torch.Tensor | None = None) -> torch.Tensor:
 
 def sum_reduce_host(bufs, out: torch.Tensor | None = None, chunk: int = 0,
                     device: torch.device | str | None = None, scratch: torch.Tensor | None = None):
-    """PCIe-inclusive aggregation at the PS: W int32 buckets in HOST memory (pinned for
-    full link speed; what the worker sockets deliver) -> HBM -> the same W-way sum-reduce
-    -> the aggregate back in host memory (`out`, pinned CPU int32), chunked and pipelined
-    over H2D / reduce / D2H (ina_sum_reduce_host_i32).  Returns when `out` is complete."""
+    """PCIe-inclusive aggregation at the PS: W int32 buckets in HOST memory (what the worker
+    sockets deliver) -> the same W-way sum-reduce -> the aggregate back in host memory
+    (`out`, pinned CPU int32 by default).  Pinned inputs and output: one reduce launch reads
+    them across PCIe in place (zero copy); otherwise chunked and pipelined over H2D /
+    reduce / D2H (ina_sum_reduce_host_i32).  Returns when `out` is complete."""
     if isinstance(bufs, torch.Tensor):
         bufs = list(bufs.unbind(0)) if bufs.dim() > 1 else [bufs]
     bufs = list(bufs)
@@ -596,7 +597,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                launch_chunks: int | None = None, switch_small_sort: bool | int | None = None,
                switch_window: int | None = None, switch_ack_fast: bool | None = None,
                switch_sort: int | None = None, switch_sort_rounds: int | None = None,
-               ew_blocks: int | None = None, switch_tiny_max: int | None = None):
+               ew_blocks: int | None = None, switch_tiny_max: int | None = None,
+               host_zero_copy: bool | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -614,7 +616,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     one-in one-out elementwise kernels (default 2^24: one 16-byte chunk per thread),
     switch_tiny_max the largest batch the switch sorts and runs in ONE launch of one
     workgroup (0 = off, at most 2048) -- only batches that take the small-sort path at all
-    reach it, so it is capped by switch_small_sort's threshold; unroll is the
+    reach it, so it is capped by switch_small_sort's threshold; host_zero_copy lets
+    sum_reduce_host reduce pinned, device-mapped host buffers in place over PCIe (True,
+    the default) instead of through the chunked copy pipeline; unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
@@ -643,6 +647,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(14, int(ew_blocks)), "set_tuning")
     if switch_tiny_max is not None:
         check(lib.ina_set_tuning(15, int(switch_tiny_max)), "set_tuning")
+    if host_zero_copy is not None:
+        check(lib.ina_set_tuning(16, int(bool(host_zero_copy))), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

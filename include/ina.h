@@ -74,7 +74,9 @@ const char* ina_last_error_string(void);
  * 4, 8, 16), 14 grid cap of the one-in one-out elementwise kernels (quantise, dequantise,
  * PS apply, int16 wire), 15 largest switch batch sorted and run in ONE launch of one
  * workgroup (0 = off, <= 2048; it applies only to batches that also take key 9's
- * one-workgroup path, so it is capped by key 9's threshold).
+ * one-workgroup path, so it is capped by key 9's threshold), 16 host reduce on pinned
+ * device-mapped buffers in place over PCIe (1, default) or through the chunked copy
+ * pipeline (0).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 
@@ -292,14 +294,17 @@ int ina_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_
 
 /* ---- PCIe-inclusive aggregation (PS ingest) ----------------------------------------
  * The PS side of the reference receives each worker's gradients over a socket into host
- * memory and sums them on the CPU (worker.py:63-79, launch.py:111-130, 42-52).  This
- * moves W HOST buckets (pinned for full speed) through HBM in chunks of chunk_values
- * values (0 = 4 Mi; rounded up to a multiple of 64): H2D copies, the W-way sum-reduce
- * above on `stream`, D2H of the aggregate into host_out, pipelined over a ring of 3
- * device slots on internal copy streams so both copy directions overlap the reduce.
- * Bit-identical to ina_sum_reduce_i32.  dev_scratch: device memory (256-byte aligned)
- * of ina_host_reduce_scratch_bytes(W, chunk_values) bytes.  Synchronous: returns once
- * host_out holds the aggregate (the PS sends it next). */
+ * memory and sums them on the CPU (worker.py:63-79, launch.py:111-130, 42-52).  When all
+ * W HOST buckets and host_out are pinned, device-mapped memory (hipHostMalloc,
+ * hipHostRegister, torch pin_memory), ONE launch of the W-way sum-reduce on `stream`
+ * reads the buckets and writes the aggregate across PCIe directly (zero copy; tuning key
+ * 16 = 0 turns this off).  Otherwise the buckets move through HBM in chunks of
+ * chunk_values values (0 = 4 Mi; rounded up to a multiple of 64): H2D copies, the
+ * reduce, D2H of the aggregate into host_out, pipelined over a ring of 3 device slots on
+ * internal copy streams so both copy directions overlap the reduce.  Bit-identical to
+ * ina_sum_reduce_i32 either way.  dev_scratch: device memory (256-byte aligned) of
+ * ina_host_reduce_scratch_bytes(W, chunk_values) bytes (the pipeline's ring).
+ * Synchronous: returns once host_out holds the aggregate (the PS sends it next). */
 size_t ina_host_reduce_scratch_bytes(int W, size_t chunk_values);
 int ina_sum_reduce_host_i32(const int32_t* const* host_bufs, int W, int32_t* host_out, size_t n,
                             size_t chunk_values, void* dev_scratch, ina_stream_t stream);

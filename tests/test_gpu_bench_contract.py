@@ -65,6 +65,7 @@ def test_bench_json_line_contract():
         assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert c4["overflow_slots"] == c4["overflow_slots_injected"] > 0
     assert e2e["parity_spot_check"] is True and e2e["roofline"]["bound"] == "pcie_h2d"
+    assert e2e["copy_pipeline"]["parity_spot_check"] is True and e2e["copy_pipeline"]["value"] > 0
     assert 0 < e2e["roofline"]["frac"] and e2e["roofline"]["peak"] > 0
     c5 = d["sharded_c5"]
     assert c5["parity_spot_check"] is True and c5["rccl_world"] == 1 and c5["values_per_rank"] == 1 << 22

@@ -111,19 +111,46 @@ def test_sum_reduce_config3_full_size():
     assert cs == sum(orc.checksum_i32(b) for b in bufs) % 2**32 == orc.checksum_i32(want)
 
 
-# PCIe-inclusive path: host buckets -> HBM -> reduce -> host, chunked over a 3-slot ring
+# PCIe-inclusive path: pinned host buckets reduced in place over PCIe (zero copy), or host
+# buckets -> HBM -> reduce -> host, chunked over a 3-slot ring
 @pytest.mark.parametrize("W,n,chunk", [(1, 1, 0), (3, 63, 64), (8, 100_003, 4096),
                                        (8, 100_003, 0), (17, 65_537, 1000), (64, 5000, 128)])
 @pytest.mark.parametrize("pinned", [True, False])
-def test_sum_reduce_host_matches_oracle(W, n, chunk, pinned):
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_sum_reduce_host_matches_oracle(W, n, chunk, pinned, zero_copy):
     rng = np.random.default_rng(W * 31 + n + chunk)
     bufs = [rand_i32(rng, n) for _ in range(W)]
     hb = [torch.from_numpy(b) for b in bufs]
     if pinned:
         hb = [b.pin_memory() for b in hb]
-    got = ops().sum_reduce_host(hb, chunk=chunk)
+    o = ops()
+    try:
+        o.set_tuning(host_zero_copy=zero_copy)
+        got = o.sum_reduce_host(hb, chunk=chunk)
+    finally:
+        o.set_tuning(host_zero_copy=True)
     assert not got.is_cuda
     assert np.array_equal(got.numpy(), orc.sum_reduce_i32(bufs))
+
+
+def test_sum_reduce_host_zero_copy_views_and_mixed_memory():
+    """Zero copy on interior views of pinned allocations (odd offsets: the unaligned
+    kernel reads host memory), and a pageable output with pinned inputs (not device-
+    mapped: the call falls back to the copy pipeline) -- bit-exact either way, and a
+    refused mapping query leaves no HIP error behind for the next call."""
+    rng = np.random.default_rng(77)
+    W, n = 5, 40_001
+    big = [torch.from_numpy(rand_i32(rng, n + 3)).pin_memory() for _ in range(W)]
+    o = ops()
+    for off in (0, 1, 3):
+        views = [b[off:off + n] for b in big]
+        want = orc.sum_reduce_i32([v.numpy() for v in views])
+        assert np.array_equal(o.sum_reduce_host(views).numpy(), want), off
+        pageable_out = torch.empty(n, dtype=torch.int32)
+        got = o.sum_reduce_host(views, out=pageable_out)
+        assert got.data_ptr() == pageable_out.data_ptr() and np.array_equal(got.numpy(), want), off
+    assert np.array_equal(host(o.sum_reduce([dev(b.numpy()) for b in big])),
+                          orc.sum_reduce_i32([b.numpy() for b in big]))
 
 
 @pytest.mark.parametrize("h2d", [1, 2])
@@ -137,12 +164,12 @@ def test_sum_reduce_host_ring_reuse_and_copy_streams(h2d):
     o = ops()
     scratch = torch.empty(o.load().ina_host_reduce_scratch_bytes(W, 64), dtype=torch.uint8, device=DEV)
     try:
-        o.set_tuning(h2d_streams=h2d)
+        o.set_tuning(h2d_streams=h2d, host_zero_copy=False)    # the copy pipeline itself
         for _ in range(2):
             got = o.sum_reduce_host(hb, chunk=64, scratch=scratch)
             assert np.array_equal(got.numpy(), orc.sum_reduce_i32(bufs))
     finally:
-        o.set_tuning(h2d_streams=2)
+        o.set_tuning(h2d_streams=2, host_zero_copy=True)
 
 
 # --------------------------------------------------------------------------------------

@@ -20,6 +20,15 @@ for st in $STAGES; do
     test)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -25 "$OUT/pytest_gpu.log"; ok_or_fail pytest $rc ;;
+    ew16lab)
+      timeout -k 10 300 python tools/lab/ew16_lab.py > "$OUT/ew16_lab.log" 2>&1
+      rc=$?; cat "$OUT/ew16_lab.log"; [ $rc -ne 0 ] && fatal ew16lab $rc ;;
+    bkphase)
+      timeout -k 10 200 python tools/lab/bucket_phase_lab.py > "$OUT/bucket_phase_lab.log" 2>&1
+      rc=$?; cat "$OUT/bucket_phase_lab.log"; [ $rc -ne 0 ] && fatal bkphase $rc ;;
+    zerocopy)
+      timeout -k 10 200 python tools/lab/zerocopy_lab.py > "$OUT/zerocopy_lab.log" 2>&1
+      rc=$?; cat "$OUT/zerocopy_lab.log"; [ $rc -ne 0 ] && fatal zerocopy $rc ;;
     contract)
       timeout -k 10 900 python -u -m pytest tests/test_gpu_bench_contract.py -m gpu -v -rf --timeout 600 --timeout-method thread > "$OUT/contract.log" 2>&1
       rc=$?; tail -8 "$OUT/contract.log"; ok_or_fail contract $rc ;;
