@@ -7,7 +7,7 @@ These are the kernels that replace the reference's CPU / switch arithmetic:
   quantize / dequantize      float_to_int / int_to_float (absent; DataManager.py:9,
                              NGAPacket.py:5) -- build-defined, see DESIGN.md
   sum_reduce                 the switch's per-slot Processor add (processor.p4:14-24)
-  sum_reduce_host            the same from/to host memory, PCIe copies pipelined (PS ingest)
+  sum_reduce_host            the same from/to host memory across PCIe (PS ingest)
   quantize_reduce            worker quantise fused with the aggregator sum
   pack_nga / unpack_nga      DataManager._send_data (DataManager.py:111-165) and the
                              PS-side parse (NGAPacket.py:62-143), headers.p4 layout
