@@ -1,11 +1,11 @@
 #!/bin/bash
 # Copy one gpu_session.sh run (stages test bench prof pmc extra swprof [rehearse sharded
-# config1 pathprof]) into profiles/<round> and regenerate the traffic summaries, DESIGN.md's
-# kernel table and profiles/README.md.  usage: tools/refresh_profiles.sh TAG
+# config1 pathprof]) into profiles/<round> and regenerate the traffic summaries.
+# usage: tools/refresh_profiles.sh TAG
 set -eu
 TAG=$1
 S=gpurun_out/$TAG
-D=profiles/${INA_EVIDENCE_ROUND:-r02}
+D=profiles/${INA_EVIDENCE_ROUND:-r03}
 mkdir -p "$D"
 cp "$S/bench.json" "$D/bench.json"
 cp "$S/prof/run_kernel_stats.csv" "$D/kernel_stats_bench.csv"
@@ -26,4 +26,3 @@ cp "$S/bench_extra.json" "$D/bench_extra.json"
 [ -f "$S/config1.log" ] && cp "$S/config1.log" "$D/config1_loopback.log"
 [ -f "$S/pathprof/run_kernel_stats.csv" ] && cp "$S/pathprof/run_kernel_stats.csv" "$D/kernel_stats_packet_path.csv"
 echo "profiles refreshed from $TAG into $D"
-python tools/design_table.py "$TAG" && python tools/profiles_readme.py "$TAG"
