@@ -898,6 +898,11 @@ def test_switch_config3_full_size_equals_bulk_reduce(V, n, pool):
     bufs = [torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
             for _ in range(W)]
     want = o.sum_reduce(bufs)
+    # anchored to the oracle directly too: 4,099 slots' values summed on the host
+    idx = np.unique(np.concatenate([np.arange(0, n // V, 97), [n // V - 1]]))
+    cols = (idx[:, None] * V + np.arange(V)).ravel()
+    tcols = torch.from_numpy(cols).to(DEV)
+    host_want = orc.sum_reduce_i32([host(b[tcols]) for b in bufs])
     packed = [o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=pool, desc=True) for w, b in enumerate(bufs)]
     stream = torch.cat([p for p, _ in packed])
     desc = torch.cat([d for _, d in packed])
@@ -909,7 +914,9 @@ def test_switch_config3_full_size_equals_bulk_reduce(V, n, pool):
     assert done.numel() == npk and bool((done >= (W - 1) * npk).all())
     f, vals = o.unpack_nga(stream[done], V)
     order = torch.argsort(f["frag_id"].to(torch.int64))
-    assert torch.equal(vals.view(npk, V)[order].reshape(-1), want)
+    got = vals.view(npk, V)[order].reshape(-1)
+    assert torch.equal(got, want)
+    assert np.array_equal(host(got[tcols]), host_want)
 
 
 def test_switch_config3_full_size_shuffled_arrival():
@@ -923,6 +930,8 @@ def test_switch_config3_full_size_shuffled_arrival():
     bufs = [torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
             for _ in range(W)]
     want = o.sum_reduce(bufs)
+    cols = torch.arange(0, n, 9973, device=DEV)                      # oracle anchor: a strided sample
+    host_want = orc.sum_reduce_i32([host(b[cols]) for b in bufs])
     packed = [o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=pool, desc=True) for w, b in enumerate(bufs)]
     del bufs
     npk = n // V
@@ -940,7 +949,41 @@ def test_switch_config3_full_size_shuffled_arrival():
     assert torch.equal(torch.sort(done).values, torch.sort(last).values)
     f, vals = o.unpack_nga(stream[done], V)
     order = torch.argsort(f["frag_id"].to(torch.int64))
-    assert torch.equal(vals.view(npk, V)[order].reshape(-1), want)
+    got = vals.view(npk, V)[order].reshape(-1)
+    assert torch.equal(got, want)
+    assert np.array_equal(host(got[cols]), host_want)
+
+
+@pytest.mark.parametrize("extra", [0, 1])
+def test_switch_bucket_rows_limit_equals_digit_passes(extra):
+    """The chunk + bucket sort takes batches of up to 2,048 chunks (8,388,608 packets at
+    4,096-packet chunks; its bucket kernel's LDS rows), larger batches the LSD digit
+    passes.  At the limit and one packet past it, V = 4 packets of 8 workers into a 2^17-
+    slot pool (slots reused across the batch: collisions and in-batch completions): the
+    default sort and the digit passes (tuning key 12 = 3, itself oracle-tested above) give
+    identical actions, packets and registers."""
+    o = ops()
+    W, V, pool = 8, 4, 1 << 17
+    npk = 2048 * 4096 + extra
+    per = -(-npk // W)
+    g = torch.Generator(device=DEV).manual_seed(5 + extra)
+    vals = torch.randint(-(1 << 31), (1 << 31) - 1, (W, per * V), dtype=torch.int32, device=DEV, generator=g)
+    stream = torch.cat([o.pack_nga(vals[w], V, w + 1, W, 1, 1, num_slots=pool) for w in range(W)])[:npk]
+    del vals
+    res = []
+    for sort in (0, 3):
+        o.set_tuning(switch_sort=sort)
+        try:
+            sw = o.Switch(V, num_slots=pool, switch_id=1, device=DEV, write_dropped=True)
+            pk = stream.clone()
+            act = sw.process(pk)
+            torch.cuda.synchronize()
+            res.append((act, pk, sw.count, sw.frag, sw.regs))
+        finally:
+            o.set_tuning(switch_sort=0)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+    assert int((res[0][0] == orc.ACT_FWD_AGG).sum()) > 0
 
 
 @pytest.mark.parametrize("keep", [True, False])
