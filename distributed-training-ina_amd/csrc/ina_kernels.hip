@@ -12,8 +12,8 @@
 //
 // All of these are HBM-streaming kernels (no contraction -> no MFMA): 16 B per lane
 // per access (global_load_dwordx4), 256-thread workgroups, grid-stride loops over
-// a grid capped near 8 workgroups per CU, non-temporal loads/stores for data that is
-// touched exactly once.  Integer sums use uint32 arithmetic (defined wraparound).
+// a grid capped near 8 workgroups per CU, non-temporal loads and write-through (sc1)
+// stores for data that is touched exactly once (ina_device.h).  Integer sums use uint32 arithmetic (defined wraparound).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -24,6 +24,7 @@
 
 #include "ina.h"
 #include "ina_internal.h"
+#include "ina_device.h"
 
 namespace ina {
 
@@ -122,7 +123,7 @@ __device__ __forceinline__ T ld(const T* p) {
 }
 template <bool NT, typename T>
 __device__ __forceinline__ void st(T* p, T v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    if constexpr (NT) stream_store(v, p);
     else *p = v;
 }
 
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_reduce_i32_vec_dyn(PtrPack<int32
             acc += (a + b) + (c + d);
         }
         for (; w < W; ++w) acc += __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in.p[w]) + i);
-        __builtin_nontemporal_store(acc, reinterpret_cast<u32x4*>(out) + i);
+        stream_store(acc, reinterpret_cast<u32x4*>(out) + i);
     }
     size_t t = 4 * n4 + tid;
     if (t < n) {
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize_i32(const float* __restrict
             u32x4 r;
             r.x = (uint32_t)q32(v[u].x, s); r.y = (uint32_t)q32(v[u].y, s);
             r.z = (uint32_t)q32(v[u].z, s); r.w = (uint32_t)q32(v[u].w, s);
-            __builtin_nontemporal_store(r, q4 + i + u * st);
+            stream_store(r, q4 + i + u * st);
         }
     });
     const size_t stride = (size_t)gridDim.x * kBlock;
@@ -405,8 +406,8 @@ __global__ __launch_bounds__(kBlock) void k_quantize_i16_vec(const float* __rest
             oa.y = (uint32_t)(uint16_t)q16(u.z, s, sa) | ((uint32_t)q16(u.w, s, sa) << 16);
             ob.x = (uint32_t)(uint16_t)q16(v.x, s, sb) | ((uint32_t)q16(v.y, s, sb) << 16);
             ob.y = (uint32_t)(uint16_t)q16(v.z, s, sb) | ((uint32_t)q16(v.w, s, sb) << 16);
-            __builtin_nontemporal_store(oa, reinterpret_cast<u32x2*>(q + eA));
-            __builtin_nontemporal_store(ob, reinterpret_cast<u32x2*>(q + eB));
+            stream_store(oa, reinterpret_cast<u32x2*>(q + eA));
+            stream_store(ob, reinterpret_cast<u32x2*>(q + eB));
         } else {
             for (size_t j = eA; j < eA + 4 && j < n; ++j) q[j] = (int16_t)q16(x[j], s, sa);
             for (size_t j = eB; j < eB + 4 && j < n; ++j) q[j] = (int16_t)q16(x[j], s, sb);
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_quantize_i16_vec(const float* __rest
                 o.y = (uint32_t)(uint16_t)r[2] | ((uint32_t)r[3] << 16);
                 o.z = (uint32_t)(uint16_t)r[4] | ((uint32_t)r[5] << 16);
                 o.w = (uint32_t)(uint16_t)r[6] | ((uint32_t)r[7] << 16);
-                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(q + e));
+                stream_store(o, reinterpret_cast<u32x4*>(q + e));
             } else {
                 for (size_t j = e; j < n; ++j) q[j] = (int16_t)q16(x[j], s, sat);
             }
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_i32(const int32_t* __rest
             f32x4 r;
             r.x = (float)(int32_t)v[u].x * inv; r.y = (float)(int32_t)v[u].y * inv;
             r.z = (float)(int32_t)v[u].z * inv; r.w = (float)(int32_t)v[u].w * inv;
-            __builtin_nontemporal_store(r, y4 + i + u * st);
+            stream_store(r, y4 + i + u * st);
         }
     });
     const size_t stride = (size_t)gridDim.x * kBlock;
@@ -499,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void k_dequantize_i16(const int16_t* __rest
             f32x4 r;
             r.x = (float)(int16_t)(v[u].x & 0xFFFFu) * inv; r.y = (float)((int32_t)v[u].x >> 16) * inv;
             r.z = (float)(int16_t)(v[u].y & 0xFFFFu) * inv; r.w = (float)((int32_t)v[u].y >> 16) * inv;
-            __builtin_nontemporal_store(r, y4 + i + u * st);
+            stream_store(r, y4 + i + u * st);
         }
     });
     const size_t stride = (size_t)gridDim.x * kBlock;
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i32(PtrPack<float> in, 
                     acc.x += (uint32_t)q32(v[w][u].x, s); acc.y += (uint32_t)q32(v[w][u].y, s);
                     acc.z += (uint32_t)q32(v[w][u].z, s); acc.w += (uint32_t)q32(v[w][u].w, s);
                 }
-                __builtin_nontemporal_store(acc, o4 + i + u * st);
+                stream_store(acc, o4 + i + u * st);
             }
         });
     } else {
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i32(PtrPack<float> in, 
                 acc.x += (uint32_t)q32(v.x, s); acc.y += (uint32_t)q32(v.y, s);
                 acc.z += (uint32_t)q32(v.z, s); acc.w += (uint32_t)q32(v.w, s);
             }
-            __builtin_nontemporal_store(acc, o4 + i);
+            stream_store(acc, o4 + i);
         }
     }
     const size_t stride = (size_t)gridDim.x * kBlock;
@@ -592,8 +593,8 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i16(PtrPack<float> in, 
             oa.y = (uint32_t)(uint16_t)sat16(a[2], sa) | ((uint32_t)sat16(a[3], sa) << 16);
             ob.x = (uint32_t)(uint16_t)sat16(a[4], sb) | ((uint32_t)sat16(a[5], sb) << 16);
             ob.y = (uint32_t)(uint16_t)sat16(a[6], sb) | ((uint32_t)sat16(a[7], sb) << 16);
-            __builtin_nontemporal_store(oa, reinterpret_cast<u32x2*>(out + eA));
-            __builtin_nontemporal_store(ob, reinterpret_cast<u32x2*>(out + eB));
+            stream_store(oa, reinterpret_cast<u32x2*>(out + eA));
+            stream_store(ob, reinterpret_cast<u32x2*>(out + eB));
         } else {
             for (size_t j = eA; j < eA + 4 && j < n; ++j) {
                 int32_t a = 0;
@@ -633,7 +634,7 @@ __global__ __launch_bounds__(kBlock) void k_quant_reduce_i16(PtrPack<float> in, 
                 o.y = (uint32_t)(uint16_t)sat16(a[2], sat) | ((uint32_t)sat16(a[3], sat) << 16);
                 o.z = (uint32_t)(uint16_t)sat16(a[4], sat) | ((uint32_t)sat16(a[5], sat) << 16);
                 o.w = (uint32_t)(uint16_t)sat16(a[6], sat) | ((uint32_t)sat16(a[7], sat) << 16);
-                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + e));
+                stream_store(o, reinterpret_cast<u32x4*>(out + e));
             } else {
                 for (size_t j = e; j < n; ++j) {
                     int32_t a = 0;
@@ -690,7 +691,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_reduce_i16(PtrPack<int16_t> in, 
                 o.y = (uint32_t)(uint16_t)sat16(a[2], sat) | ((uint32_t)sat16(a[3], sat) << 16);
                 o.z = (uint32_t)(uint16_t)sat16(a[4], sat) | ((uint32_t)sat16(a[5], sat) << 16);
                 o.w = (uint32_t)(uint16_t)sat16(a[6], sat) | ((uint32_t)sat16(a[7], sat) << 16);
-                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + e));
+                stream_store(o, reinterpret_cast<u32x4*>(out + e));
             } else {
                 for (size_t j = e; j < n; ++j) {
                     int32_t a = 0;
@@ -999,7 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, Nga
             } else {
                 o = u32x4{0u, 0u, 0u, 0u};                   // padding chunks
             }
-            __builtin_nontemporal_store(o, ch + t);
+            stream_store(o, ch + t);
         }
     }
 }
@@ -1121,7 +1122,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_flat(const uint8_t* __res
                 o.y = __builtin_amdgcn_perm(a[u].y, a[u].x, kSelBE);
                 o.z = __builtin_amdgcn_perm(a[u].z, a[u].y, kSelBE);
                 o.w = __builtin_amdgcn_perm(a[u].w, a[u].z, kSelBE);
-                __builtin_nontemporal_store(
+                stream_store(
                     o, reinterpret_cast<u32x4*>(vals + (size_t)p * V) + (c - 1));
             }
         }

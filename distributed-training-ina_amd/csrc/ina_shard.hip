@@ -26,6 +26,7 @@
 
 #include "ina.h"
 #include "ina_internal.h"
+#include "ina_device.h"
 
 namespace ina {
 namespace {
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(kBlk) void k_quantize_i16_wire(const float* __restr
         u32x4 r;
         r.x = (uint32_t)q16w(v.x, s); r.y = (uint32_t)q16w(v.y, s);
         r.z = (uint32_t)q16w(v.z, s); r.w = (uint32_t)q16w(v.w, s);
-        __builtin_nontemporal_store(r, w4 + i);
+        stream_store(r, w4 + i);
     }
     for (size_t i = 4 * n4 + tid; i < n; i += stride) wire[i] = q16w(x[i], s);
 }
@@ -102,12 +103,12 @@ __global__ __launch_bounds__(kBlk) void k_i16_wire_finish_vec(const int32_t* __r
                 u32x2 o;
                 o.x = (uint32_t)(uint16_t)a | ((uint32_t)b << 16);
                 o.y = (uint32_t)(uint16_t)c | ((uint32_t)d << 16);
-                __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(out16 + e));
+                stream_store(o, reinterpret_cast<u32x2*>(out16 + e));
             }
             if (y) {
                 f32x4 f;
                 f.x = (float)a * inv; f.y = (float)b * inv; f.z = (float)c * inv; f.w = (float)d * inv;
-                __builtin_nontemporal_store(f, reinterpret_cast<f32x4*>(y + e));
+                stream_store(f, reinterpret_cast<f32x4*>(y + e));
             }
         } else if (e < n) {
             for (size_t j = e; j < n; ++j) {

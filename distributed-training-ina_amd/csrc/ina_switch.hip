@@ -22,6 +22,7 @@
 
 #include "ina.h"
 #include "ina_internal.h"
+#include "ina_device.h"
 
 namespace ina {
 
@@ -972,6 +973,17 @@ static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWI
 #ifndef INA_SWITCH_ACT_BATCH
 #define INA_SWITCH_ACT_BATCH 1
 #endif
+// forwarded packets and slot registers: written once per call, never read back by it
+#ifndef INA_SWITCH_STORE_SC1
+#define INA_SWITCH_STORE_SC1 0
+#endif
+__device__ __forceinline__ void sw_st(u32x4s v, u32x4s* p) {
+#if INA_SWITCH_STORE_SC1
+    stream_store(v, p);
+#else
+    *p = v;
+#endif
+}
 __device__ __forceinline__ u32x4s sw_ld(const u32x4s* p) {
 #if INA_SWITCH_NT
     return __builtin_nontemporal_load(p);
@@ -1245,14 +1257,14 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                 e.w = enc_lo(p.w, lane < L ? reg.x : e.w);
                             }
                             if (lane <= L)
-                                reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride)[lane] = e;
+                                sw_st(e, reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride) + lane);
                             if (wide && lane == 63) {        // tail chunk 64 from lane 63's values
                                 u32x4s o;
                                 o.x = enc_lo(reg.x, reg.y);
                                 o.y = enc_lo(reg.y, reg.z);
                                 o.z = enc_lo(reg.z, reg.w);
                                 o.w = enc_lo(reg.w, tw);
-                                reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride)[64] = o;
+                                sw_st(o, reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride) + 64);
                             }
                         }
                     }
@@ -1267,7 +1279,7 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
             st.count[slot] = (uint8_t)cnt;
             st.frag[slot] = frag;
         }
-        if (have_reg && vl) *reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane) = reg;
+        if (have_reg && vl) sw_st(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane));
         }
     }
 }

@@ -27,7 +27,7 @@ arrs = [(C.c_void_p * W)(*[t.data_ptr() for t in s]) for s in sets]
 flush = torch.ones(128 << 20, dtype=torch.int32, device=dev)
 st = torch.cuda.current_stream().cuda_stream
 NAMES = {0: "nt (product)", 1: "sc0 sc1", 2: "sc1 nt", 3: "sc0 sc1 nt", 4: "default", 5: "sc1"}
-K, ROUNDS, GRID = 20, 8, 512
+K, ROUNDS, GRID = int(os.environ.get("K", 20)), int(os.environ.get("ROUNDS", 8)), 512
 
 
 def launch(v, s):
