@@ -19,8 +19,12 @@ template <typename T>
 __device__ __forceinline__ void stream_store(T v, T* p) {
 #if INA_STORE_SC1
     static_assert(sizeof(T) == 16 || sizeof(T) == 8 || sizeof(T) == 4, "16, 8 or 4-byte stores");
+    // a VALU write to the data VGPRs of a store of more than 8 bytes needs a wait state
+    // after the store; the compiler's hazard recognizer does not see the store inside the
+    // asm statement, so the asm carries it (without it: wrong sums at W = 16, whose
+    // allocation rewrites a store's data registers right after it)
     if constexpr (sizeof(T) == 16)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     else if constexpr (sizeof(T) == 8)
         asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
     else
