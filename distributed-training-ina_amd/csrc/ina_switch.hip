@@ -147,8 +147,7 @@ __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const ui
                                                 size_t i0, size_t n, int shift, int bits,
                                                 uint32_t (*base)[kRsBins], const uint32_t* gst,
                                                 uint32_t* __restrict__ kout,
-                                                uint32_t* __restrict__ vout, int rw = R,
-                                                uint32_t off = 0) {   // outputs at position - off
+                                                uint32_t* __restrict__ vout, int rw = R) {
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const uint32_t nb = 1u << bits;
     constexpr int kThr = NW * 64;
@@ -176,8 +175,8 @@ __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const ui
         const uint32_t rank = (uint32_t)__builtin_popcountll(pm & below);
         const uint32_t b0 = base[wv][d];
         if (valid) {
-            kout[b0 + rank - off] = k[r];
-            vout[b0 + rank - off] = v[r];
+            kout[b0 + rank] = k[r];
+            vout[b0 + rank] = v[r];
             if (rank == 0) base[wv][d] = b0 + (uint32_t)__builtin_popcountll(pm);
         }
     }
@@ -670,14 +669,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
                                                          const uint32_t* __restrict__ rst, uint32_t nch,
                                                          uint32_t CH, int lbits, uint32_t* __restrict__ nforeign,
                                                          uint32_t skip) {
-    // the chunk rows (s_dst, s_src) are dead once the tile is gathered into registers, so
-    // the one-tile output staging (stk, stv) reuses their LDS
-    constexpr int kRows = 2 * kBkMaxChunks + 1, kStage = 2 * kBkThr * R;
-    __shared__ uint32_t lds_buf[kRows > kStage ? kRows : kStage];
-    uint32_t* const s_dst = lds_buf;
-    uint32_t* const s_src = lds_buf + kBkMaxChunks + 1;
-    uint32_t* const stk = lds_buf;
-    uint32_t* const stv = lds_buf + kBkThr * R;
+    __shared__ uint32_t s_dst[kBkMaxChunks + 1], s_src[kBkMaxChunks];
     __shared__ uint32_t base[kBkWaves][kRsBins];
     __shared__ uint32_t gst[kRsBins];                 // bucket digit counts, then output positions
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
@@ -805,19 +797,10 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
         }
         __syncthreads();
         BK_STAMP(3);
-        if (ntile == 1) {
-            // a one-tile bucket is scattered into LDS and leaves as one contiguous run: in
-            // worker-major arrival consecutive lanes' slots are W positions apart, so
-            // scattering straight to memory wrote 4-byte words 4W bytes apart
-            rs_tile_scatter<R, kBkWaves>(k, v, i0, t_end, 0, lbits, base, gst, stk, stv, rw, s0);
-            __syncthreads();
-            for (uint32_t i = threadIdx.x; i < cnt; i += kBkThr) {
-                kout[s0 + i] = stk[i];
-                vout[s0 + i] = stv[i];
-            }
-        } else {
-            rs_tile_scatter<R, kBkWaves>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
-        }
+        // (staging a one-tile bucket's output in LDS to leave as one contiguous run measured
+        // no faster: 244.5 -> 244.1 us worker-major, 228.3 -> 229.9 round-robin,
+        // profiles/r03/lab/bucket_stage_lab.log)
+        rs_tile_scatter<R, kBkWaves>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
         __syncthreads();
         BK_STAMP(4);
         if (d < nb) gst[d] += tc;
