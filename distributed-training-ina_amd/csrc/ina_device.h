@@ -4,7 +4,7 @@
 
 namespace ina {
 
-// Streaming stores of the one-pass kernels.  INA_STORE_SC1 = 1: `global_store_dwordx{2,4}
+// Streaming stores of the one-pass reduce and elementwise kernels.  INA_STORE_SC1 = 1: `global_store_dwordx{2,4}
 // ... sc1` (write-through at system scope), so a launch leaves no dirty lines for the next
 // dependent launch's boundary to drain (MI355X_MICROARCH.md: a boundary costs + B / 6 TB/s
 // when the predecessor leaves B bytes dirty).  The headline reduce, interleaved on two
@@ -32,6 +32,15 @@ __device__ __forceinline__ void stream_store(T v, T* p) {
 #else
     __builtin_nontemporal_store(v, p);
 #endif
+}
+
+// Packet kernels (pack / unpack of NGA rows) keep non-temporal stores: their rows are the
+// next launch's input (the switch, the sender), and write-through made the fused worker
+// pack 9 % slower in the packet path (54.7 -> 59.6 us per launch beside the switch,
+// profiles/r03/lab/path_store_lab.log).
+template <typename T>
+__device__ __forceinline__ void packet_store(T v, T* p) {
+    __builtin_nontemporal_store(v, p);
 }
 
 }  // namespace ina

@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, Nga
             } else {
                 o = u32x4{0u, 0u, 0u, 0u};                   // padding chunks
             }
-            stream_store(o, ch + t);
+            packet_store(o, ch + t);
         }
     }
 }
@@ -1122,7 +1122,7 @@ __global__ __launch_bounds__(kBlock) void k_unpack_nga_flat(const uint8_t* __res
                 o.y = __builtin_amdgcn_perm(a[u].y, a[u].x, kSelBE);
                 o.z = __builtin_amdgcn_perm(a[u].z, a[u].y, kSelBE);
                 o.w = __builtin_amdgcn_perm(a[u].w, a[u].z, kSelBE);
-                stream_store(
+                packet_store(
                     o, reinterpret_cast<u32x4*>(vals + (size_t)p * V) + (c - 1));
             }
         }

@@ -522,7 +522,10 @@ __global__ __launch_bounds__(NW * 64) void k_rs_scatter(const uint32_t* __restri
 constexpr int kBkWaves = INA_BK_WAVES;
 constexpr int kBkThr = kBkWaves * 64;
 constexpr int kBkMaxChunks = 2048;                  // B's LDS rows: up to 2048 x CH packets
-constexpr int kLcRounds = 64 / kBkWaves > 4 ? 64 / kBkWaves : 4;   // B's tile: max(4096, 256 x waves) items
+// B's tile: 16 waves x 64 x 4 = 4,096 items.  8,192 (one pass for the steady-state batch's
+// 9 x 512-packet buckets: 24.4 -> 18.8 us for B) cost the plain 8-worker batch 1-3 us
+// (occupancy 8 -> 7 waves/SIMD; profiles/r03/lab/bucket_tile_lab.log), so it stays 4,096
+constexpr int kLcRounds = 4;
 
 // key fields of R rounds of 64 packets (all loads issued first): slot index, switch id and
 // the PS-ack flag, from the batch's descriptors (header bytes 4..11) or the headers

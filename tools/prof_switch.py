@@ -20,6 +20,12 @@ packed = [ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots, desc=True) for w, 
 stream = torch.cat([p for p, _ in packed])
 desc = torch.cat([d for _, d in packed])     # the pack kernels' packet descriptors
 del packed
+order = os.environ.get("ORDER", "wm")           # wm: worker-major, rr: round-robin, random
+if order != "wm":
+    npw = stream.shape[0] // W
+    perm = (torch.arange(W * npw, device=dev).view(W, npw).t().reshape(-1) if order == "rr"
+            else torch.randperm(W * npw, device=dev, generator=torch.Generator(device=dev).manual_seed(9)))
+    stream, desc = stream[perm].contiguous(), desc[perm].contiguous()
 sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
 acts = torch.empty(stream.shape[0], dtype=torch.uint8, device=dev)
 use_desc = os.environ.get("DESC", "1") == "1"
