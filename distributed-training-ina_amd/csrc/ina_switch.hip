@@ -1362,7 +1362,9 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     // chunk = 4 waves x 64 x rounds items: 1,024 up to 256 Ki packets (a batch of the PS's
     // acks still spreads over more than a few dozen CUs), 2,048 up to 512 Ki, 4,096 above
     // (switch_lab, profiles/r01/lab/switch_lab_rounds.log: 102,400 packets 77.7 -> 60.9 us,
-    // 409,600 155.5 -> 146.1, 819,200 unchanged)
+    // 409,600 155.5 -> 146.1, 819,200 unchanged).  With the chunk + bucket sort, 819,200
+    // packets: 4,096-packet chunks (200 A blocks) 234.6 us worker-major, 2,048 235.8, 1,024
+    // 241.3 (profiles/r03/lab/sort_rounds_lab.log)
     p.rounds = npk <= (size_t)INA_RS_SMALL_ITEMS ? INA_RS_ROUNDS_SMALL
              : npk <= (size_t)INA_RS_MID_ITEMS   ? INA_RS_ROUNDS_MID
                                                  : kRsRounds;
