@@ -971,25 +971,37 @@ def run_reduce(args, rank, world, dev, backend):
     del sets, outs
     torch.cuda.empty_cache()
     if not args.no_c2:
-        line["c2_fused"] = measure_c2(dev, world, rank=rank)
+        run_leg(line, "c2_fused", lambda: measure_c2(dev, world, rank=rank))
     if not args.no_c4:
-        line["c4_int16"] = measure_c4(dev, world, rank=rank)
+        run_leg(line, "c4_int16", lambda: measure_c4(dev, world, rank=rank))
     if not args.no_e2e:
-        line["e2e_pcie"] = measure_e2e(dev, world, rank=rank)
+        run_leg(line, "e2e_pcie", lambda: measure_e2e(dev, world, rank=rank))
     if not args.no_c5:
-        line["sharded_c5"] = measure_c5(args, rank, world, dev)
-        torch.cuda.empty_cache()
-        line["sharded_c5"]["layout_b"] = measure_c5_layout_b(args, rank, world, dev)
+        c5 = run_leg(line, "sharded_c5", lambda: measure_c5(args, rank, world, dev))
+        run_leg(c5, "layout_b", lambda: measure_c5_layout_b(args, rank, world, dev))
         if world > 1:
-            torch.cuda.empty_cache()
-            line["sharded_c5"]["allreduce"] = measure_c5(args, rank, world, dev, collective="allreduce")
-            torch.cuda.empty_cache()
-            line["sharded_c5"]["pipelined"] = measure_c5(args, rank, world, dev, chunks=C5_CHUNKS)
+            run_leg(c5, "allreduce", lambda: measure_c5(args, rank, world, dev, collective="allreduce"))
+            run_leg(c5, "pipelined", lambda: measure_c5(args, rank, world, dev, chunks=C5_CHUNKS))
     if not args.no_switch:
-        line["switch_c3"] = measure_switch(dev, rank=rank, world=world)
+        run_leg(line, "switch_c3", lambda: measure_switch(dev, rank=rank, world=world))
     if cpu_in is not None:
-        line["cpu_baseline"] = cpu_baseline(args, *cpu_in)
+        run_leg(line, "cpu_baseline", lambda: cpu_baseline(args, *cpu_in))
     return line
+
+
+def run_leg(parent: dict, key: str, fn) -> dict:
+    """parent[key] = fn(), or {"error": ...} if the leg raises: a leg that fails the same
+    way on every rank (an RCCL or memory error at some N) is reported in the line instead of
+    taking the headline down with it.  Returns the leg's dict."""
+    try:
+        parent[key] = fn()
+    except Exception as e:          # noqa: BLE001 -- reported in the JSON line
+        parent[key] = {"error": f"{type(e).__name__}: {str(e)[:400]}"}
+    try:
+        torch.cuda.empty_cache()
+    except Exception:               # noqa: BLE001 -- a sticky device error is already reported
+        pass
+    return parent[key]
 
 
 def main():

@@ -42,3 +42,19 @@ def test_cgroup_quota_reader_is_safe():
     import bench
     q = bench.cgroup_cpus()
     assert q is None or q > 0
+
+
+def test_run_leg_reports_a_failing_leg_and_keeps_the_line():
+    sys.path.insert(0, REPO)
+    import bench
+    line = {"value": 1.0}
+    ok = bench.run_leg(line, "a", lambda: {"frac": 0.8})
+    assert ok == {"frac": 0.8} and line["a"] is ok
+
+    def boom():
+        raise RuntimeError("NCCL error: unhandled system error")
+    bad = bench.run_leg(line, "b", boom)
+    assert bad["error"].startswith("RuntimeError: NCCL error")
+    bench.run_leg(bad, "sub", lambda: {"x": 1})        # sub-legs attach to an errored parent
+    assert line["b"]["sub"] == {"x": 1} and line["value"] == 1.0
+    json.dumps(line)
