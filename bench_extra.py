@@ -53,7 +53,7 @@ def _row(name, secs, nbytes, **kw):
     return r
 
 
-DEFAULTS = {"max_blocks": 16384, "reduce_blocks": 0, "stream_blocks": 8192, "combine_blocks": 256,
+DEFAULTS = {"max_blocks": 16384, "reduce_blocks": 0, "stream_blocks": 16384, "combine_blocks": 256,
             "combine_ina_blocks": 8192, "ew_blocks": 1 << 24}
 
 
@@ -168,7 +168,7 @@ def run_extra(dev):
     stride = ops.nga_stride(V)
     npk = (n3 + V - 1) // V
     pk = torch.empty((npk, stride), dtype=torch.uint8, device=dev)
-    grids = (256, 512, 1024, 2048, 8192)
+    grids = (1024, 2048, 8192, 16384, 32768)
     _sweep(ops, rows, gsweep, "pack_nga V=256", "stream_blocks", grids,
            lambda: ops.pack_nga(o3, V, 1, 8, 1, 1, out=pk), 4 * n3 + npk * stride)
     _sweep(ops, rows, gsweep, "unpack_nga V=256", "stream_blocks", grids,

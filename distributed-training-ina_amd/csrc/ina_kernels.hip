@@ -80,8 +80,11 @@ constexpr int kEwU = INA_EW_U;
 #ifndef INA_QR_U
 #define INA_QR_U 1     // fused quantise + reduce, W <= 8: C2 91.8 -> 86.7 us (ew_lab)
 #endif
-// the other chunk_loop<4> streaming kernels
-static std::atomic<int> g_stream_blocks{8192};
+// the flat packet kernels (pack, fused quantise + pack, unpack; one 16-byte chunk per thread,
+// grid-striding) and the fused quantise + reduce for W > 8: 16,384 workgroups beat 8,192 by
+// 1-3 % on two boxes (pack 34.9 -> 33.9 us, worker pack 51.5 -> 50.8, unpack 36.6 -> 35.6;
+// a covering grid of ~26k is slower again; profiles/r03/lab/pack_grid_lab.log)
+static std::atomic<int> g_stream_blocks{16384};
 // the one-in one-out elementwise kernels (quantise, dequantise, PS apply, the int16 wire
 // kernels of ina_shard.hip): one 16-byte chunk per thread, the grid covering the whole
 // array -- no grid-stride loop.  At a 1 GiB bucket (config 5) that is 330-340 us (80 %)
@@ -905,8 +908,8 @@ __device__ __forceinline__ uint32_t nga_val(const Src& src, size_t n, size_t p, 
 // fp32) and takes value 4c -- the next chunk's first -- from the next lane (DPP
 // wave_shl:1; lane 63 loads it).  Chunk 0 is the header plus value 0's top byte.
 constexpr uint32_t kSelWire = 0x07000102u;   // perm(next, v): {v.b2, v.b1, v.b0, next.b3}
-// 16-byte chunks in flight per thread in the flat packet kernels: one (with the 8192-
-// workgroup grid striding over the rest) beat 2, 4 and 8 -- fused worker pack 57.7 -> 54.2
+// 16-byte chunks in flight per thread in the flat packet kernels: one (with an 8192-
+// workgroup grid striding over the rest, now 16,384: g_stream_blocks) beat 2, 4 and 8 -- fused worker pack 57.7 -> 54.2
 // us, pack 37.5 -> 36.5, unpack 40.4 -> 39.1 (tools/lab/apply_lab.py, lab/pack_u_lab.log)
 #ifndef INA_PACK_U
 #define INA_PACK_U 1
