@@ -281,6 +281,7 @@ static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack la
 // (DESIGN.md section 4).
 static std::atomic<int> g_sort_mode{0};
 static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: sort chunk rounds (0 auto, 4/8/16)
+static std::atomic<uint32_t> g_sort_epoch{0};   // per-call tag of the chunk sort's "unsorted" flag
 int set_sort_mode(int v) {
     if (v != 0 && v != 3) return INA_EINVAL;
     g_sort_mode = v;
@@ -589,7 +590,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                                                         uint8_t* __restrict__ actions, int hbits, int lb,
                                                         uint32_t* __restrict__ rcnt, uint32_t* __restrict__ rst,
                                                         size_t nch, uint32_t* __restrict__ kout,
-                                                        uint32_t* __restrict__ vout, int ack_hint) {
+                                                        uint32_t* __restrict__ vout, int ack_hint,
+                                                        uint32_t* __restrict__ unsorted, uint32_t epoch) {
     __shared__ uint32_t base[kBkWaves][kRsBins];     // per-wave digit counts, then bases
     __shared__ uint32_t gst[kRsBins];                 // the chunk's run starts (output positions)
     __shared__ uint32_t wtot[kBkWaves];
@@ -600,7 +602,14 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     const size_t i0 = c * (size_t)(kBkThr * R) + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t idx[R], sid[R], ack[R], k[R], v[R];
     load_key_fields<R, kDesc>(pkts, desc, npk, stride, i0, idx, sid, ack);
+    // the key before the wave's first item (the previous wave's or chunk's last): every lane
+    // loads the same entry
+    uint32_t pidx[1], psid[1], pack[1];
+    const size_t pw = i0 - (size_t)lane;                      // the wave's first position
+    load_key_fields<1, kDesc>(pkts, desc, pw > 0 ? npk : 0, stride, pw - 1, pidx, psid, pack);
     __syncthreads();
+    uint32_t prev = psid[0] == (uint32_t)(uint8_t)switch_id && switch_id >= 0 ? pidx[0] % num_slots : num_slots;
+    bool down = false;                                        // a key below its predecessor's
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const size_t p = i0 + (size_t)r * 64;
@@ -611,7 +620,15 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         v[r] = (uint32_t)p;
         if (p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
         lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
+        // predecessor: lane l-1 of this round (DPP wave_shr:1), lane 0 the previous round's
+        // lane 63 (or, in round 0, the key loaded above)
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp((int)prev, (int)key, 0x138, 0xF, 0xF, false);
+        down |= p < npk && p > 0 && pk > key;
+        prev = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
     }
+    // the batch is not in slot order: B sorts (else B only copies A's output, which is then
+    // the identity permutation).  Tagged with the call's epoch, so nothing needs clearing.
+    if (__ballot(down) && lane == 0) unsorted[0] = epoch;
     __syncthreads();
     // thread d owns digit d: the chunk's count, its chunk-local run start (block scan)
     const uint32_t d = threadIdx.x;
@@ -671,13 +688,18 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
                                                          const uint32_t* __restrict__ rcnt,
                                                          const uint32_t* __restrict__ rst, uint32_t nch,
                                                          uint32_t CH, int lbits, uint32_t* __restrict__ nforeign,
-                                                         uint32_t skip) {
+                                                         uint32_t skip, const uint32_t* __restrict__ unsorted,
+                                                         uint32_t epoch, int sorted_copy) {
     __shared__ uint32_t s_dst[kBkMaxChunks + 1], s_src[kBkMaxChunks];
     __shared__ uint32_t base[kBkWaves][kRsBins];
     __shared__ uint32_t gst[kRsBins];                 // bucket digit counts, then output positions
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const uint32_t b = blockIdx.x;
+    // keys already in slot order: A's output is the sorted order and the register-resident
+    // run kernel reads it there (sorted_copy = 0), so only the foreign bucket's size is needed
+    const bool in_order = unsorted[0] != epoch;
+    if (in_order && !sorted_copy && b != skip) return;
     BK_STAMP(0);
     // this bucket's run in every chunk: thread t owns chunks [t*per, t*per + per).  A chunk's
     // run start rst[b][c] is the number of its packets in lower buckets, so the rst row also
@@ -729,6 +751,13 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
         return;
     }
     if (cnt == 0) return;                             // block-uniform
+    if (in_order) {                                   // (the generic run kernel reads B's
+        for (uint32_t i = threadIdx.x; i < cnt; i += kBkThr) {   // output: the bucket is its
+            kout[s0 + i] = kin[s0 + i];               // own run of A's output, copied)
+            vout[s0 + i] = vin[s0 + i];
+        }
+        return;
+    }
     uint32_t top = 1;                                 // search steps: powers of two below nch
     while (top * 2 < nch) top *= 2;
     if (nch == 1) top = 0;
@@ -1315,10 +1344,18 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                           const uint32_t* __restrict__ ids,
                                                           uint8_t* __restrict__ actions,
                                                           uint32_t win, uint32_t kmask, PsFuse ps,
-                                                          const uint32_t* __restrict__ nforeign) {
+                                                          const uint32_t* __restrict__ nforeign,
+                                                          const uint32_t* __restrict__ keys_a,
+                                                          const uint32_t* __restrict__ ids_a,
+                                                          const uint32_t* __restrict__ unsorted, uint32_t epoch) {
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
+    // a batch already in slot order: the chunk sort's own output is the sorted order
+    if (unsorted && unsorted[0] != epoch) {
+        keys = keys_a;
+        ids = ids_a;
+    }
     switch_run2_body<kPs>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps,
                           switch_block_index() * (kSwBlock / 64) + wave_in_block(),
                           ((size_t)gridDim.x * kSwBlock) >> 6);
@@ -1385,6 +1422,7 @@ struct SortAux {
     uint32_t* rst;                // [2^bits][nch]
     uint32_t* totals;             // [512]
     uint32_t* nforeign;           // [1]
+    uint32_t* unsorted;           // [1]: the epoch of the last call whose keys were out of order
 };
 
 static size_t sort_hist_cap(size_t npk, uint32_t num_slots) {
@@ -1405,6 +1443,7 @@ static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
     a.rst = reinterpret_cast<uint32_t*>(aux + hist);
     a.totals = reinterpret_cast<uint32_t*>(aux + 2 * hist);
     a.nforeign = reinterpret_cast<uint32_t*>(aux + 2 * hist + align_up((size_t)kRsBins * 4, 256));
+    a.unsorted = a.nforeign + 1;
     return a;
 }
 
@@ -1502,6 +1541,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     // bins) and at most kBkMaxChunks chunks (B's LDS rows); else the digit passes
     const bool bucket = !small && g_sort_mode.load() == 0 && sp.passes <= 2 && sp.nch <= (size_t)kBkMaxChunks;
     const uint32_t* nforeign = nullptr;
+    const uint32_t* unsorted = nullptr;     // bucket sort: the run kernel may read A's output
+    uint32_t epoch = 0;
     if (small && fast && npk <= (size_t)g_tiny_max.load()) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
         uint32_t win = (uint32_t)INA_SWITCH_WIN_SMALL;
@@ -1533,10 +1574,14 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const int lb = eb - sp.bits;                       // low digit bits (0: one-digit keys)
         const uint2* dsc = reinterpret_cast<const uint2*>(desc);
         const int ah = ack_hint ? 1 : 0;
+        // never 0 (fresh scratch reads as "unsorted": the safe side); a stale epoch equal to
+        // this one (2^32 calls later) also only costs the full sort
+        epoch = g_sort_epoch.fetch_add(1u) + 1u;
+        if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
 #define INA_A_LAUNCH(RR)                                                                              \
         hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true> : &k_sort_chunks<RR, false>), dim3(gc),   \
                            dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id,  \
-                           actions, sp.bits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah)
+                           actions, sp.bits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, ax.unsorted, epoch)
         if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
         else INA_A_LAUNCH(kR0 / 4);
@@ -1554,7 +1599,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // so at 2^17 slots 257 blocks (one per CU, one generation) instead of 512
         const unsigned gb = std::min<unsigned>(nb, (st->num_slots >> lb) + 1u);
         hipLaunchKernelGGL((k_sort_buckets<kLcRounds>), dim3(gb), dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist,
-                           ax.rst, (uint32_t)sp.nch, CH, lb, ax.nforeign, skip);
+                           ax.rst, (uint32_t)sp.nch, CH, lb, ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1);
+        if (fast) unsorted = ax.unsorted;
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
         // LSD digit passes (keys of three digits, batches beyond B's rows, or key 12 = 3):
@@ -1603,7 +1649,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         auto* run = ps.on ? &k_switch_run2<true> : &k_switch_run2<false>;
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc, vc, actions,
-                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign);
+                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted, epoch);
         *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));

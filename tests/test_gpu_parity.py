@@ -741,6 +741,76 @@ def test_switch_bucket_sort_pool_edges(num_slots):
             o.set_tuning(switch_sort=0)
 
 
+def _slot_keys(stream, num_slots, switch_id=1):
+    """The sort key of every packet (slot, or num_slots for another switch's)."""
+    idx = stream[:, 6:10].copy().view(">u4").reshape(-1).astype(np.int64)
+    return np.where(stream[:, 10] == switch_id, idx % num_slots, num_slots)
+
+
+PRESORTED_CASES = ["sorted", "descent_in_round", "descent_at_round", "descent_at_wave",
+                   "descent_at_chunk", "descent_at_end", "foreign_in_middle", "equal_keys"]
+
+
+@pytest.mark.parametrize("rounds,use_desc", [(0, True), (16, False), (16, True)])
+@pytest.mark.parametrize("case", PRESORTED_CASES)
+def test_switch_presorted_batches_vs_oracle(case, rounds, use_desc):
+    """Batches already in slot order (a NIC's round-robin interleave of workers sending in
+    lockstep) take the chunk sort's fast path: A finds no key below its predecessor and B
+    only copies A's output.  One descent anywhere -- inside a 64-packet round, at a round
+    edge (lane 0 reads the previous round's lane 63), at a wave or chunk edge (the loaded
+    predecessor), at the last packet, or another switch's packets in the middle -- must take
+    the full sort.  Bit-exact against the P4 restatement, state carried across batches, with
+    collisions, acks and degree-1 slots in the stream.  rounds 0: 1,024-packet chunks, one
+    64-packet round per wave; 16: 4,096-packet chunks, four rounds per wave."""
+    rng = np.random.default_rng(1000 * PRESORTED_CASES.index(case) + rounds + use_desc)
+    o = ops()
+    V, W, num_slots = 32, 8, 1 << 17
+    o.set_tuning(switch_sort_rounds=rounds)
+    try:
+        _presorted_batches(o, rng, case, use_desc, V, W, num_slots)
+    finally:
+        o.set_tuning(switch_sort_rounds=0)
+
+
+def _presorted_batches(o, rng, case, use_desc, V, W, num_slots):
+    sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
+    sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+    for rnd in range(2):
+        stream = make_stream(rng, V, 1300, W, num_slots, collide=0.05, ack=0.1,
+                             other=0.1 if case == "foreign_in_middle" else 0.05)
+        if case == "equal_keys":                        # every packet in a handful of slots
+            stream[:, 6:10] = np.frombuffer(np.repeat(np.arange(5, dtype=">u4"),
+                                            -(-len(stream) // 5))[:len(stream)].tobytes(),
+                                            np.uint8).reshape(-1, 4)
+        keys = _slot_keys(stream, num_slots)
+        stream = stream[np.argsort(keys, kind="stable")]
+        n = len(stream)
+        assert n > 8192
+        at = {"descent_in_round": 4096 + 70 + 10, "descent_at_round": 4096 + 128,
+              "descent_at_wave": 4096 + 256, "descent_at_chunk": 4096, "descent_at_end": n - 1}.get(case)
+        if at is not None:          # the packet at `at` gets a key below its predecessor's
+            if case == "descent_at_end":                # the smallest key moves to the end
+                stream = np.concatenate([stream[1:], stream[:1]])
+            else:                                       # a large key moves to at - 1
+                stream = np.insert(np.delete(stream, n - 3, axis=0), at - 1, stream[n - 3], axis=0)
+            k2 = _slot_keys(stream, num_slots)
+            assert k2[at] < k2[at - 1] and (np.diff(k2) < 0).sum() == 1, case
+        if case == "foreign_in_middle":                 # the foreign packets sit mid-batch
+            k2 = _slot_keys(stream, num_slots)
+            foreign = stream[k2 == num_slots]
+            mine = stream[k2 != num_slots]
+            stream = np.concatenate([mine[: len(mine) // 2], foreign, mine[len(mine) // 2:]])
+        want_pk, want_act = sw_orc.run(stream, stride=o.nga_stride(V))
+        d = dev(stream)
+        act = sw_dev.process(d, desc=o.nga_descriptors(d) if use_desc else None)
+        assert np.array_equal(host(act), want_act), (case, rnd)
+        assert np.array_equal(host(d), want_pk), (case, rnd)
+    cnt, frag, regs = sw_orc.registers()
+    assert np.array_equal(host(sw_dev.count), cnt)
+    assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+    assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+
+
 @pytest.mark.parametrize("V,stride_kind", [(32, "padded"), (256, "padded"), (33, "tight"),
                                            (64, "tight"), (4, "padded")])
 def test_pack_descriptors_are_header_bytes(V, stride_kind):
