@@ -297,6 +297,26 @@ def cpu_baseline(args, bufs_host, gpu_out_sample):
 
 
 # -- config 5: sharded over RCCL --------------------------------------------------------------
+def _phase_times(phases, stream, world, passes=6):
+    """Per-phase device time (s) of a step made of `phases` (callables that enqueue work on
+    `stream`): HIP events between the phases over `passes` back-to-back passes, the median
+    over passes 2.. (the first passes start with an empty queue, so the host's launch time
+    would sit between the events; afterwards the host is ahead of the GPU), max over ranks."""
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)] for _ in range(passes)]
+    barrier(world)
+    for p in range(passes):
+        ev[p][0].record(stream)
+        for i, fn in enumerate(phases):
+            fn()
+            ev[p][i + 1].record(stream)
+    torch.cuda.synchronize()
+    out = []
+    for i in range(len(phases)):
+        t = sorted(ev[p][i].elapsed_time(ev[p][i + 1]) / 1e3 for p in range(2, passes))
+        out.append(max_over_ranks(t[len(t) // 2], world))
+    return out
+
+
 def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag", chunks=1):
     """quantise -> reduce_scatter(int32, SUM) -> decode -> all_gather of one n-value fp32
     bucket per rank (the i32 wire gathers fp32; the i16 wire gathers the saturated int16
@@ -325,24 +345,12 @@ def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag", chunks=1):
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
 
-    # per-phase breakdown (one more pass, events between the aggregator's own phases)
+    # per-phase breakdown: events between the aggregator's own phases
     phase = None
     if agg.chunks == 1:
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-        barrier(world)
-        ev[0].record(stream)
-        agg.phase_quantize(bucket)
-        ev[1].record(stream)
-        agg.phase_reduce_scatter()
-        ev[2].record(stream)
-        agg.phase_decode()
-        ev[3].record(stream)
-        agg.phase_all_gather()
-        ev[4].record(stream)
-        agg.phase_expand()
-        ev[5].record(stream)
-        torch.cuda.synchronize()
-        phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(5)]
+        phase = _phase_times([lambda: agg.phase_quantize(bucket), agg.phase_reduce_scatter,
+                              agg.phase_decode, agg.phase_all_gather, agg.phase_expand],
+                             stream, world)
 
     # parity: the aggregate at a sample of positions == decode(sum over ranks of the
     # per-rank wire of those values), the per-rank wires all-gathered.  The sample covers
@@ -493,17 +501,9 @@ def measure_c5_layout_b(args, rank, world, dev, warmup=2):
         agg(slices)
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    barrier(world)
-    ev[0].record(stream)
     m = agg.phase_reduce_decode(slices)
-    ev[1].record(stream)
-    agg.phase_all_gather()
-    ev[2].record(stream)
-    agg.phase_expand()
-    ev[3].record(stream)
-    torch.cuda.synchronize()
-    phase = [max_over_ranks(ev[i].elapsed_time(ev[i + 1]) / 1e3, world) for i in range(3)]
+    phase = _phase_times([lambda: agg.phase_reduce_decode(slices), agg.phase_all_gather,
+                          agg.phase_expand], stream, world)
     c = min(m, 1 << 16)
     ok = True
     if c:
