@@ -25,6 +25,12 @@ src = torch.cat([ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots) for w, b in
 del bufs
 if os.environ.get("ORDER", "wm") == "rr":      # a NIC's round-robin interleave of the workers
     src = src.view(W, -1, src.shape[1]).transpose(0, 1).reshape(-1, src.shape[1]).contiguous()
+elif os.environ.get("ORDER", "").startswith("wmpad"):   # worker-major, PAD foreign rows between workers
+    pad = int(os.environ["ORDER"][5:] or 3)
+    rows = src.view(W, -1, src.shape[1])
+    filler = rows[0, :pad].clone()
+    filler[:, 10] = 7                          # another switch's packets: sorted last, not run
+    src = torch.cat([torch.cat([rows[w], filler]) for w in range(W)]).contiguous()
 elif os.environ.get("ORDER") == "random":       # uniformly shuffled arrival
     src = src[torch.randperm(src.shape[0], device=dev, generator=torch.Generator(device=dev).manual_seed(9))]
 npk, stride = src.shape
