@@ -1575,6 +1575,7 @@ int ina_set_tuning(int key, int value) {
         case 13: return set_os_rounds(value);
         case 15: return set_tiny_max(value);
         case 16: return set_zero_copy(value);
+        case 17: return set_bucket_tile(value);
         default: return INA_EINVAL;
     }
 }

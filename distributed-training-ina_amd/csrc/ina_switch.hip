@@ -523,10 +523,19 @@ __global__ __launch_bounds__(NW * 64) void k_rs_scatter(const uint32_t* __restri
 constexpr int kBkWaves = INA_BK_WAVES;
 constexpr int kBkThr = kBkWaves * 64;
 constexpr int kBkMaxChunks = 2048;                  // B's LDS rows: up to 2048 x CH packets
-// B's tile: 16 waves x 64 x 4 = 4,096 items.  8,192 (one pass for the steady-state batch's
-// 9 x 512-packet buckets: 24.4 -> 18.8 us for B) cost the plain 8-worker batch 1-3 us
-// (occupancy 8 -> 7 waves/SIMD; profiles/r03/lab/bucket_tile_lab.log), so it stays 4,096
+// B's tile: 16 waves x 64 x R items.  R = 4 (4,096) by default; 8,192 (R = 8) takes the
+// steady-state batch's 9 x 512-packet buckets in one pass (24.4 -> 18.8 us for B) but costs
+// the plain 8-worker batch (3,200 per bucket) 1-3 us (profiles/r03/lab/bucket_tile_lab.log),
+// so the launch picks R = 8 only when the average bucket exceeds 7/8 of the smaller tile
 constexpr int kLcRounds = 4;
+constexpr int kLcRoundsBig = 8;
+constexpr size_t kBigTileAvg = (size_t)kBkWaves * 64 * kLcRounds * 7 / 8;   // 3,584 items
+static std::atomic<int> g_bucket_tile{0};   // ina_set_tuning key 17: 0 auto, 4 or 8 rounds
+int set_bucket_tile(int v) {
+    if (v != 0 && v != kLcRounds && v != kLcRoundsBig) return INA_EINVAL;
+    g_bucket_tile = v;
+    return INA_OK;
+}
 
 // key fields of R rounds of 64 packets (all loads issued first): slot index, switch id and
 // the PS-ack flag, from the batch's descriptors (header bytes 4..11) or the headers
@@ -1598,8 +1607,11 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // buckets past the sentinel's (num_slots >> lb) are always empty: no block for them,
         // so at 2^17 slots 257 blocks (one per CU, one generation) instead of 512
         const unsigned gb = std::min<unsigned>(nb, (st->num_slots >> lb) + 1u);
-        hipLaunchKernelGGL((k_sort_buckets<kLcRounds>), dim3(gb), dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist,
-                           ax.rst, (uint32_t)sp.nch, CH, lb, ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1);
+        const int tile = g_bucket_tile.load();
+        const bool big = tile == kLcRoundsBig || (tile == 0 && npk > (size_t)gb * kBigTileAvg);
+        hipLaunchKernelGGL((big ? &k_sort_buckets<kLcRoundsBig> : &k_sort_buckets<kLcRounds>), dim3(gb),
+                           dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
+                           ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1);
         if (fast) unsorted = ax.unsorted;
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {

@@ -598,7 +598,7 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                switch_window: int | None = None, switch_ack_fast: bool | None = None,
                switch_sort: int | None = None, switch_sort_rounds: int | None = None,
                ew_blocks: int | None = None, switch_tiny_max: int | None = None,
-               host_zero_copy: bool | None = None):
+               host_zero_copy: bool | None = None, switch_bucket_tile: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -618,7 +618,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     workgroup (0 = off, at most 2048) -- only batches that take the small-sort path at all
     reach it, so it is capped by switch_small_sort's threshold; host_zero_copy lets
     sum_reduce_host reduce pinned, device-mapped host buffers in place over PCIe (True,
-    the default) instead of through the chunked copy pipeline; unroll is the
+    the default) instead of through the chunked copy pipeline; switch_bucket_tile the slot
+    sort's bucket tile in 64-item rounds per wave (0 = auto: 8 when the average bucket
+    exceeds 3,584 packets, else 4; or 4, 8); unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
@@ -649,6 +651,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(15, int(switch_tiny_max)), "set_tuning")
     if host_zero_copy is not None:
         check(lib.ina_set_tuning(16, int(bool(host_zero_copy))), "set_tuning")
+    if switch_bucket_tile is not None:
+        check(lib.ina_set_tuning(17, int(switch_bucket_tile)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

@@ -76,7 +76,8 @@ const char* ina_last_error_string(void);
  * workgroup (0 = off, <= 2048; it applies only to batches that also take key 9's
  * one-workgroup path, so it is capped by key 9's threshold), 16 host reduce on pinned
  * device-mapped buffers in place over PCIe (1, default) or through the chunked copy
- * pipeline (0).
+ * pipeline (0), 17 the slot sort's bucket tile in 64-item rounds per wave (0 auto: 8 when
+ * the average bucket exceeds 3,584 packets, else 4; or 4, 8).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 

@@ -201,6 +201,9 @@ def test_set_tuning_rejects_unknown_keys_and_values():
     assert lib.ina_set_tuning(12, 0) == _lib.INA_OK and lib.ina_set_tuning(13, 0) == _lib.INA_OK
     assert lib.ina_set_tuning(16, 2) == _lib.INA_EINVAL        # host zero copy: 0 / 1
     assert lib.ina_set_tuning(16, 0) == _lib.INA_OK and lib.ina_set_tuning(16, 1) == _lib.INA_OK
+    assert lib.ina_set_tuning(17, 5) == _lib.INA_EINVAL        # bucket tile: 0 auto / 4 / 8
+    for v in (4, 8, 0):
+        assert lib.ina_set_tuning(17, v) == _lib.INA_OK
 
 
 def test_switch_scratch_bytes_monotonic():

@@ -624,8 +624,8 @@ def test_switch_fuzz_vs_oracle(seed):
 
 # slot sort variants: (sort 0 = auto: chunk + bucket for keys of one or two digits / 3 = the
 # LSD digit passes, descriptors, chunk rounds)
-SORT_VARIANTS = [(3, True, 0), (3, False, 0), (0, False, 4), (0, True, 16), (0, False, 8),
-                 (0, True, 0), (0, False, 0), (3, True, 8)]
+SORT_VARIANTS = [(3, True, 0, 0), (3, False, 0, 0), (0, False, 4, 0), (0, True, 16, 0), (0, False, 8, 0),
+                 (0, True, 0, 0), (0, False, 0, 0), (3, True, 8, 0), (0, True, 0, 8), (0, False, 16, 8)]
 
 
 @pytest.mark.parametrize("variant", SORT_VARIANTS)
@@ -636,7 +636,7 @@ def test_switch_sort_paths_vs_oracle(seed, variant):
     / 4,096 packets; keys from the packet headers or from the batch's descriptors) and the
     LSD histogram / column-scan / scatter digit passes -- bit-exact against the P4
     restatement, state carried across batches, pools of 1 .. 2^18 slots (keys of 1-3 digits)."""
-    sort, use_desc, rounds = variant
+    sort, use_desc, rounds, tile = variant
     rng = np.random.default_rng(40_000 + seed)
     o = ops()
     V = int(rng.choice([4, 32, 64, 256, 33]))
@@ -644,7 +644,7 @@ def test_switch_sort_paths_vs_oracle(seed, variant):
     W = int(rng.integers(1, 17))
     stride = o.nga_stride(V) if rng.random() < 0.7 else 15 + 4 * V
     wd = bool(rng.integers(0, 2))
-    o.set_tuning(switch_sort=sort, switch_sort_rounds=rounds)
+    o.set_tuning(switch_sort=sort, switch_sort_rounds=rounds, switch_bucket_tile=tile)
     try:
         sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=wd)
         sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
@@ -671,12 +671,12 @@ def test_switch_sort_paths_vs_oracle(seed, variant):
         assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
         assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
     finally:
-        o.set_tuning(switch_sort=0, switch_sort_rounds=0)
+        o.set_tuning(switch_sort=0, switch_sort_rounds=0, switch_bucket_tile=0)
 
 
-@pytest.mark.parametrize("sort", [3, 0])
+@pytest.mark.parametrize("sort,tile", [(3, 0), (0, 0), (0, 8)])
 @pytest.mark.parametrize("case", ["one_bucket", "one_slot", "two_buckets", "foreign_heavy"])
-def test_switch_skewed_buckets_vs_oracle(sort, case):
+def test_switch_skewed_buckets_vs_oracle(sort, tile, case):
     """Slot use concentrated in one or two sort buckets (2^8 consecutive slots of a 2^17
     pool), so a bucket holds more than one 4,096-item tile and the chunk + bucket sort takes
     its multi-tile path (a counting sweep, then the tiles in order); one case puts every
@@ -688,7 +688,7 @@ def test_switch_skewed_buckets_vs_oracle(sort, case):
     V, num_slots, W = 32, 1 << 17, 16
     idx_hi = {"one_bucket": 256, "one_slot": 1, "two_buckets": 512, "foreign_heavy": None}[case]
     other = 0.7 if case == "foreign_heavy" else 0.05      # packets for another switch
-    o.set_tuning(switch_sort=sort)
+    o.set_tuning(switch_sort=sort, switch_bucket_tile=tile)
     try:
         sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
         sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
@@ -706,7 +706,7 @@ def test_switch_skewed_buckets_vs_oracle(sort, case):
         assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
         assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
     finally:
-        o.set_tuning(switch_sort=0)
+        o.set_tuning(switch_sort=0, switch_bucket_tile=0)
 
 
 @pytest.mark.parametrize("num_slots", [513, 1023, 1024, 4097, 65536, (1 << 18) - 1])
