@@ -372,8 +372,17 @@ def run_extra(dev):
     t = _time(e2e, reps=5, warm=1)
     rows.append(_row("end-to-end pinned H2D(8x100MiB)+reduce+D2H", t, (W3 + 1) * n3 * 4,
                      aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2), note="one stream, phases in sequence"))
-    # the product path: chunked, H2D / reduce / D2H pipelined (ina_sum_reduce_host_i32)
+    # the product path (ina_sum_reduce_host_i32): zero copy for pinned buffers (the default),
+    # then the chunked H2D / reduce / D2H copy pipeline (zero copy off) over its knobs
     want = hout.clone()
+    hz = torch.empty(n3, dtype=torch.int32).pin_memory()
+    zscratch = torch.empty(ops.load().ina_host_reduce_scratch_bytes(W3, 0), dtype=torch.uint8, device=dev)
+    t = _time(lambda: ops.sum_reduce_host(hosts, out=hz, scratch=zscratch), reps=5, warm=1)
+    rows.append(_row("end-to-end host reduce, zero copy (pinned buckets read over PCIe in place)", t,
+                     (W3 + 1) * n3 * 4, aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2),
+                     matches=bool(torch.equal(hz, want))))
+    del hz, zscratch
+    ops.set_tuning(host_zero_copy=False)
     for h2d in (1, 2):
         for chunk in (1 << 18, 1 << 20, 1 << 22):
             ops.set_tuning(h2d_streams=h2d)
@@ -384,9 +393,10 @@ def run_extra(dev):
             def piped():
                 ops.sum_reduce_host(hosts, out=hp, chunk=chunk, scratch=scratch)
             t = _time(piped, reps=5, warm=1)
-            rows.append(_row(f"end-to-end pipelined host reduce (h2d streams {h2d}, chunk {chunk})", t,
+            rows.append(_row(f"end-to-end host reduce, copy pipeline (h2d streams {h2d}, chunk {chunk})", t,
                              (W3 + 1) * n3 * 4, aggregated_GBps=round(W3 * n3 * 4 / t / 1e9, 2),
                              matches=bool(torch.equal(hp, want))))
             del scratch
+    ops.set_tuning(host_zero_copy=True)
     ops.set_tuning(h2d_streams=2)
     return {"rows": rows, "sweep": sweep, "grid_sweeps": gsweep}
