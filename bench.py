@@ -427,7 +427,7 @@ def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag", chunks=1):
         "quantize": _phase_frac(q_bytes, phase[0]),
         "decode": _phase_frac(d_bytes, phase[2]),
         **({"expand": _phase_frac(6 * agg.plan.padded, phase[4])}
-           if args.wire == "i16" and world > 1 and collective == "rs_ag" else {}),
+           if args.wire == "i16" and world > 1 and collective != "allreduce" else {}),
     }
     return {
         "value": round(world * n * 4 * steps / elapsed / 1e9, 2), "unit": "GB/s",
@@ -437,7 +437,8 @@ def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag", chunks=1):
                      f"({args.wire} wire, k={k}) -> "
                      + ("all_reduce(int32, SUM) -> decode the whole bucket on every rank"
                         if collective == "allreduce" else
-                        "reduce_scatter(int32, SUM) -> "
+                        ("all_to_all(int32) + device sum of the slices -> " if collective == "a2a" else
+                         "reduce_scatter(int32, SUM) -> ")
                         + ("dequantise -> all_gather(fp32)" if args.wire == "i32" else
                            "saturate once -> all_gather(int16 + slot flags) -> dequantise"))),
         "values_per_rank": n, "shard_values": agg.plan.shard, "rccl_world": world,
@@ -448,7 +449,7 @@ def measure_c5(args, rank, world, dev, warmup=2, collective="rs_ag", chunks=1):
         "xgmi": ({"rs_send_bytes_per_rank": xgmi, "ag_recv_bytes_per_rank": ag,
                   "rs_busbw_GBps": round(xgmi / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None,
                   "ag_busbw_GBps": round(ag / phase[3] / 1e9, 1) if world > 1 and phase[3] > 0 else None}
-                 if collective == "rs_ag" else
+                 if collective != "allreduce" else
                  {"allreduce_bytes_per_rank": 2 * xgmi,     # nccl-tests busbw: 2(G-1)/G x S / t
                   "allreduce_busbw_GBps": round(2 * xgmi / phase[1] / 1e9, 1) if world > 1 and phase[1] > 0 else None}),
         "roofline": roofline,
@@ -863,12 +864,14 @@ def run_sharded_headline(args, rank, world, dev, backend):
     c5 = measure_c5(args, rank, world, dev)
     torch.cuda.empty_cache()
     c5_b = measure_c5_layout_b(args, rank, world, dev)
-    c5_ar = c5_pl = None
+    c5_ar = c5_pl = c5_a2a = None
     if world > 1:
         torch.cuda.empty_cache()
         c5_ar = measure_c5(args, rank, world, dev, collective="allreduce")
         torch.cuda.empty_cache()
         c5_pl = measure_c5(args, rank, world, dev, chunks=C5_CHUNKS)
+        torch.cuda.empty_cache()
+        c5_a2a = measure_c5(args, rank, world, dev, collective="a2a")
     return {
         "metric": c5["metric"], "value": c5["value"], "unit": "GB/s",
         "n_gpus": world, "steps": c5["steps"], "warmup": c5["warmup"],
@@ -883,6 +886,7 @@ def run_sharded_headline(args, rank, world, dev, backend):
         "layout_b": c5_b,
         "allreduce": c5_ar,
         "pipelined": c5_pl,
+        "a2a": c5_a2a,
     }
 
 
@@ -982,6 +986,7 @@ def run_reduce(args, rank, world, dev, backend):
         if world > 1:
             run_leg(c5, "allreduce", lambda: measure_c5(args, rank, world, dev, collective="allreduce"))
             run_leg(c5, "pipelined", lambda: measure_c5(args, rank, world, dev, chunks=C5_CHUNKS))
+            run_leg(c5, "a2a", lambda: measure_c5(args, rank, world, dev, collective="a2a"))
     if not args.no_switch:
         run_leg(line, "switch_c3", lambda: measure_switch(dev, rank=rank, world=world))
     if cpu_in is not None:

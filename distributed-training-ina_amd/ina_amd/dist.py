@@ -86,6 +86,37 @@ def reduce_scatter_sum(x_padded: torch.Tensor, plan: ShardPlan, group=None, out=
     return (out, work) if async_op else out
 
 
+def reduce_scatter_a2a(x_padded: torch.Tensor, plan: ShardPlan, group=None, out=None, recv=None):
+    """int32 [padded] -> this rank's [shard] of the element-wise sum over ranks, as ONE
+    all-to-all (rank r's slice j goes straight to rank j: on a fully connected xGMI mesh
+    every pair of GPUs has its own link, so all 7 links carry (G-1)/G x S at once instead
+    of a ring's hops) followed by the device W-way wrapping sum of the G received slices
+    (ina_sum_reduce_i32, HBM-bound) -- the same bits as the RCCL SUM (mod-2^32 adds in any
+    order).  recv: a [padded] int32 scratch (allocated when None)."""
+    if x_padded.numel() != plan.padded:
+        raise ValueError("input must be padded to plan.padded")
+    out = torch.empty(plan.shard, dtype=torch.int32, device=x_padded.device) if out is None else out
+    if plan.world == 1:
+        out.copy_(x_padded)
+        return out
+    recv = torch.empty(plan.padded, dtype=torch.int32, device=x_padded.device) if recv is None else recv
+    if x_padded.is_cuda and _host_staged(group):
+        h = torch.empty(plan.padded, dtype=torch.int32)
+        dist.all_to_all_single(h, x_padded.cpu(), group=group)
+        recv.copy_(h)
+    else:
+        dist.all_to_all_single(recv, x_padded, group=group)
+    parts = [recv[r * plan.shard:(r + 1) * plan.shard] for r in range(plan.world)]
+    if out.is_cuda:
+        ops.sum_reduce(parts, out=out)
+    else:                                       # CPU tensors (the gloo tests): the same sum
+        acc = parts[0].to(torch.int64)
+        for q in parts[1:]:
+            acc += q
+        out.copy_(((acc + (1 << 31)) % (1 << 32) - (1 << 31)).to(torch.int32))
+    return out
+
+
 def all_reduce_sum(x: torch.Tensor, group=None):
     """int32 in place -> the element-wise sum over ranks (RCCL all-reduce; host-staged
     with gloo and device tensors)."""
@@ -136,10 +167,12 @@ class ShardedAggregator:
     wire="i16": the same from the int16 saturating path; `overflow` then holds the
     per-slot flags (ceil(n / V) bytes) of the last call.
     collective="rs_ag" (default): reduce-scatter the integer wire, the owner decodes its
-    shard, all-gather.  collective="allreduce": one RCCL all-reduce of the integer wire
-    (the same (G-1)/G bytes each way per rank inside one collective) and every rank
-    decodes the whole bucket.  Both give the same bits; which one xGMI runs faster is
-    measured by bench.py at N > 1 (sharded_c5 / sharded_c5.allreduce).
+    shard, all-gather.  collective="a2a": the reduce-scatter as one all-to-all of the wire
+    slices plus the device sum of the G received slices (reduce_scatter_a2a), then the
+    same decode and all-gather.  collective="allreduce": one RCCL all-reduce of the
+    integer wire (the same (G-1)/G bytes each way per rank inside one collective) and
+    every rank decodes the whole bucket.  All give the same bits; which one xGMI runs
+    faster is measured by bench.py at N > 1 (sharded_c5 / .a2a / .allreduce).
     chunks=C > 1 (rs_ag, world > 1): the bucket is cut into C contiguous chunks, each
     reduce-scattered and all-gathered on its own (async RCCL work), so chunk c+1's
     quantise runs under chunk c's reduce-scatter and the decodes under the later
@@ -150,8 +183,8 @@ class ShardedAggregator:
                  wire: str = "i32", V: int = 256, collective: str = "rs_ag", chunks: int = 1):
         if wire not in ("i32", "i16"):
             raise ValueError("wire must be 'i32' or 'i16'")
-        if collective not in ("rs_ag", "allreduce"):
-            raise ValueError("collective must be 'rs_ag' or 'allreduce'")
+        if collective not in ("rs_ag", "a2a", "allreduce"):
+            raise ValueError("collective must be 'rs_ag', 'a2a' or 'allreduce'")
         if chunks < 1 or (chunks > 1 and collective != "rs_ag"):
             raise ValueError("chunks must be >= 1, and > 1 only with collective='rs_ag'")
         self.collective = collective
@@ -191,11 +224,14 @@ class ShardedAggregator:
             self.ovf_shard = torch.empty(self.slots_per_shard, dtype=torch.uint8, device=dev)
             self._obuf = torch.zeros(tot // V, dtype=torch.uint8, device=dev)
             self.ovf_full = self._obuf[: self.slots_per_shard * self.world]
-            if self.world > 1 and collective == "rs_ag":   # gather int16 sums, decode after
+            if self.world > 1 and collective != "allreduce":   # gather int16 sums, decode after
                 if self.chunks == 1:
                     self._shard_buf("s16", torch.int16)
                 self._s16buf = torch.empty(tot, dtype=torch.int16, device=dev)
                 self.s16_full = self._s16buf[: self.plan.padded]
+        # the all-to-all's receive buffer (world slices of one shard each)
+        self._recv = (torch.empty(self.plan.padded, dtype=torch.int32, device=dev)
+                      if collective == "a2a" and self.world > 1 else None)
         if self.chunks > 1:
             m = self.chunks * self.sc
             self.sum_c = torch.empty(m, dtype=torch.int32, device=dev)
@@ -255,6 +291,8 @@ class ShardedAggregator:
             return
         if self.collective == "allreduce":
             all_reduce_sum(self.q, self.group)
+        elif self.collective == "a2a":
+            reduce_scatter_a2a(self.q, self.plan, self.group, out=self.sum_shard, recv=self._recv)
         else:
             reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
 
@@ -280,7 +318,7 @@ class ShardedAggregator:
 
     def phase_expand(self):
         """i16 wire at world > 1: dequantise the gathered int16 sums on every rank."""
-        if self.world > 1 and self.wire == "i16" and self.collective == "rs_ag":
+        if self.world > 1 and self.wire == "i16" and self.collective != "allreduce":
             ops.dequantize(self.s16_full, self.k, out=self.full)
 
     def _quantize(self, grad: torch.Tensor):
@@ -353,7 +391,10 @@ class ShardedAggregator:
         int32 wrapped sum, or on the i16 wire the int16 saturated sum (its slot flags
         in `ovf_shard`)."""
         self._quantize(grad)
-        s = reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
+        if self.collective == "a2a":
+            s = reduce_scatter_a2a(self.q, self.plan, self.group, out=self.sum_shard, recv=self._recv)
+        else:
+            s = reduce_scatter_sum(self.q, self.plan, self.group, out=self.sum_shard)
         if self.wire == "i32":
             return s
         out16, _, _ = ops.i16_wire_finish(s, self.k, self.V, overflow=self.ovf_shard, want_y=False)

@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--layout", choices=("A", "B"), default="A")
     ap.add_argument("--workers", type=int, default=0, help="layout B: W buckets (default: world)")
-    ap.add_argument("--collective", choices=("rs_ag", "allreduce"), default="rs_ag")
+    ap.add_argument("--collective", choices=("rs_ag", "a2a", "allreduce"), default="rs_ag")
     ap.add_argument("--chunks", type=int, default=1)
     a = ap.parse_args()
     dist.init_process_group("gloo")

@@ -1,6 +1,6 @@
 """One RCCL rank (backend nccl, world size 1), launched by torch.distributed.run from
 tests/test_gpu_dist.py: the collective calls the config-5 path makes at N > 1 --
-reduce_scatter_tensor(int32, SUM), all_gather_into_tensor of fp32 values, int16 sums
+reduce_scatter_tensor(int32, SUM), all_to_all_single(int32), all_gather_into_tensor of fp32 values, int16 sums
 (the i16 wire) and uint8 slot flags, all_reduce(float64, MAX/MIN) of bench.py's max-over-ranks timing -- issued
 through RCCL on this image, with a device-kernel quantise/dequantise around them.  At
 world size 1 every collective is a copy, so results are checked exactly; what this run
@@ -51,6 +51,10 @@ def main():
     w = dist.all_gather_into_tensor(fbuf[n:], ops.dequantize(part, k), async_op=True)
     w.wait()
     assert torch.equal(fbuf[n:], y) and not fbuf[:n].any()
+    # the a2a variant's exchange: all_to_all_single of the int32 wire
+    recv = torch.empty_like(q)
+    dist.all_to_all_single(recv, q)
+    assert torch.equal(recv, q)
     t = torch.tensor([1.5], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)

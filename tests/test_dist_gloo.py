@@ -28,7 +28,8 @@ def _worker(rank, world, port, n, k, results):
     for p in (REPO, PKG_ROOT):
         if p not in sys.path:
             sys.path.insert(0, p)
-    from ina_amd.dist import ShardPlan, all_gather_shards, all_reduce_sum, reduce_scatter_sum
+    from ina_amd.dist import (ShardPlan, all_gather_shards, all_reduce_sum, reduce_scatter_a2a,
+                              reduce_scatter_sum)
     from oracle import oracle as orc
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -42,8 +43,9 @@ def _worker(rank, world, port, n, k, results):
         shard = reduce_scatter_sum(qp, plan)
         full = all_gather_shards(shard, plan)
         ar = all_reduce_sum(qp.clone())              # the collective="allreduce" variant
+        a2a = reduce_scatter_a2a(qp, plan)           # the collective="a2a" variant
         results[rank] = (shard.numpy().copy(), full[:n].numpy().copy(), plan.range_of(rank),
-                         ar[:n].numpy().copy())
+                         ar[:n].numpy().copy(), a2a.numpy().copy())
     finally:
         dist.destroy_process_group()
 
@@ -59,9 +61,10 @@ def test_sharded_integer_aggregate_gloo(world, n):
                            .astype(np.float32), k) for r in range(world)]
     want = orc.sum_reduce_i32(qs)
     for r in range(world):
-        shard, full, (lo, hi), ar = results[r]
+        shard, full, (lo, hi), ar, a2a = results[r]
         assert np.array_equal(full, want)
         assert np.array_equal(ar, want)
+        assert np.array_equal(a2a, shard)          # all-to-all + local sum == reduce-scatter
         assert np.array_equal(shard[: hi - lo], want[lo:hi])
         assert not shard[hi - lo:].any()        # padding stays zero
 

@@ -114,6 +114,9 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     ar = c5["allreduce"]                         # the one-collective variant, same bits
     assert ar["collective"] == "allreduce" and ar["parity_spot_check"] is True
     assert ar["xgmi"]["allreduce_bytes_per_rank"] == 2 * c5["shard_values"] * 4
+    a2 = c5["a2a"]                               # all-to-all + device sum, same bits
+    assert a2["collective"] == "a2a" and a2["parity_spot_check"] is True
+    assert a2["roofline"]["bytes_per_rank"] == c5["roofline"]["bytes_per_rank"]
     pl = c5["pipelined"]                         # chunked, async RCCL work, same bits
     assert pl["chunks"] > 1 and pl["parity_spot_check"] is True
     # every variant carries an xGMI roofline with the per-rank bytes it moved
@@ -121,7 +124,7 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert c5["layout_b"]["roofline"]["bytes_per_rank"] == c5["shard_values"] * 4
     assert ar["roofline"]["bytes_per_rank"] == 2 * c5["shard_values"] * 4
     assert pl["roofline"]["bytes_per_rank"] == pl["xgmi"]["rs_send_bytes_per_rank"] + pl["xgmi"]["ag_recv_bytes_per_rank"]
-    for r in (c5["roofline"], c5["layout_b"]["roofline"], ar["roofline"], pl["roofline"]):
+    for r in (c5["roofline"], c5["layout_b"]["roofline"], ar["roofline"], pl["roofline"], a2["roofline"]):
         assert r["bound"] == "xgmi" and r["achieved"] > 0 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert set(c5["roofline"]["hbm_phases"]) == {"quantize", "decode"}
     sw = d["switch_c3"]                          # every rank switched its own bucket
@@ -135,3 +138,4 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert d["xgmi"]["ag_recv_bytes_per_rank"] == 2 * shard + shard // 256
     assert d["xgmi"]["rs_send_bytes_per_rank"] == 4 * shard
     assert d["allreduce"]["parity_spot_check"] is True and d["pipelined"]["parity_spot_check"] is True
+    assert d["a2a"]["parity_spot_check"] is True

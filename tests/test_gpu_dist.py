@@ -41,11 +41,12 @@ def _run_ranks(tmp_path, world, n, wire, k, V=256, layout="A", workers=0, collec
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,n,coll", [(2, 1_000_003, "rs_ag"), (3, 70_001, "rs_ag"), (2, 1, "rs_ag"),
-                                          (8, 400_001, "rs_ag"), (3, 70_001, "allreduce"),
+                                          (8, 400_001, "rs_ag"), (3, 70_001, "allreduce"), (3, 70_001, "a2a"), (8, 400_001, "a2a"),
                                           (3, 70_001, "chunks3"), (2, 1, "chunks2"), (8, 400_001, "chunks4")])
 def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n, coll):
-    """Layout A, int32 wire: reduce-scatter + all-gather, the all-reduce variant, and the
-    pipelined chunks (chunksC: C async reduce-scatters / all-gathers)."""
+    """Layout A, int32 wire: reduce-scatter + all-gather, the all-reduce variant, the
+    all-to-all + device-sum reduce-scatter (a2a), and the pipelined chunks (chunksC: C
+    async reduce-scatters / all-gathers)."""
     from oracle import oracle as orc
     k = 20
     chunks = int(coll[6:]) if coll.startswith("chunks") else 1
@@ -66,7 +67,7 @@ def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n, coll):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,n,V,coll", [(2, 1_000_003, 256, "rs_ag"), (3, 50_000, 32, "rs_ag"),
                                             (2, 300, 100, "rs_ag"), (8, 200_000, 32, "rs_ag"),
-                                            (3, 50_000, 32, "allreduce"), (3, 50_000, 32, "chunks4"),
+                                            (3, 50_000, 32, "allreduce"), (3, 50_000, 32, "chunks4"), (4, 60_000, 32, "a2a"),
                                             (2, 300_001, 100, "chunks3")])
 def test_sharded_i16_two_ranks_device_kernels(tmp_path, world, n, V, coll):
     from oracle import oracle as orc
