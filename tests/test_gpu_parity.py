@@ -772,6 +772,16 @@ def test_switch_presorted_batches_vs_oracle(case, rounds, use_desc):
         o.set_tuning(switch_sort_rounds=0)
 
 
+@pytest.mark.parametrize("case", ["sorted", "descent_at_chunk", "foreign_in_middle"])
+def test_switch_presorted_batches_generic_run_kernel(case):
+    """The in-order fast path when the generic (LDS-staged) run kernel takes the batch (V =
+    33: not a multiple of 4): the bucket pass then copies the chunk pass's output into the
+    arrays that kernel reads."""
+    rng = np.random.default_rng(77 + PRESORTED_CASES.index(case))
+    o = ops()
+    _presorted_batches(o, rng, case, False, 33, 8, 1 << 17)
+
+
 def _presorted_batches(o, rng, case, use_desc, V, W, num_slots):
     sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
     sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
