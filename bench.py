@@ -78,6 +78,7 @@ PCIE_SPEC_GBS = 63.0         # PCIe Gen5 x16, MI355X_MICROARCH.md (host link)
 # the task's MI355X notes).  A single ring uses one link each way (153 GB/s).
 XGMI_LINKS, XGMI_LINK_GBS = 7, 153.0
 XGMI_PEAK_GBS = XGMI_LINKS * XGMI_LINK_GBS
+_ACT_FWD_AGG, _ACT_FWD_ACK = 1, 3      # ina.h action codes: completed slot forwarded, PS ack
 
 
 def parse(argv=None):
@@ -774,6 +775,82 @@ def measure_e2e(dev, world=1, reps=5, warm=1, rank=0):
     return res
 
 
+# -- the whole INA packet path, steady state (SURVEY 8f-1 + 8f-2) ---------------------------
+def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
+    """One step of the INA data path on one GPU, as a PS co-located with the switch runs it
+    in steady state: 8 workers quantise their deltas (p_w - p_global, k=16) straight into
+    NGA-256 packets (DataManager.py:37 + 111-165, fused), the PS's acks of the previous
+    step ride in the same switch batch in front of the packets (fragcheck.p4:26-31), the
+    switch aggregates every slot (ngaa.p4:120-196) and each completed slot's sum goes from
+    the switch's registers straight into the PS update p_global + (1/(W+1)) * sum * 2^-k
+    (launch.py:46-50) and its ack row (ina_switch_process_apply).  Config-3 sizes: 8 x
+    26,214,400 fp32, 102,400 slots.  HIP events around `steps` back-to-back steps; the
+    roofline is the path's algorithmic bytes (packs, switch + PS, acks) over the step time.
+    Parity: every worker packet completes its slot once, every ack frees one, and the
+    update at a strided sample equals a numpy restatement bit for bit."""
+    from ina_amd import ops
+    W, n, V, k, slots = W_WORKERS, N_VALUES, V_SLOT, 16, 1 << 17
+    npk = n // V
+    g = torch.Generator(device=dev)
+    g.manual_seed(6000 + rank)
+    xs = [torch.randn(n, device=dev, generator=g) * 1e-2 for _ in range(W)]
+    glob = torch.randn(n, device=dev, generator=g) * 1e-2
+    upd = torch.empty_like(glob)
+    stride = ops.nga_stride(V)
+    big = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=dev)   # [acks | workers]
+    ack_rows, rows_w = big[:npk], big[npk:].view(W, npk, stride)
+    desc = torch.empty((W + 1) * npk, dtype=torch.int64, device=dev)
+    desc_ack, desc_w = desc[:npk], desc[npk:].view(W, npk)
+    acts = torch.empty((W + 1) * npk, dtype=torch.uint8, device=dev)
+    sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
+    ws = 1.0 / (W + 1)
+
+    def step(_r=0):
+        for w in range(W):
+            ops.quantize_pack_nga(xs[w], k, V, w + 1, W, 1, 1, base=glob, num_slots=slots,
+                                  out=rows_w[w], desc=desc_w[w])
+        ops.nga_descriptors(ack_rows, out=desc_ack)
+        sw.process_apply(big, 1, glob, k, ws, out=upd, acks=ack_rows, keep_forwarded=False,
+                         actions=acts, desc=desc)
+    step()                                     # the first step's ack rows are another switch's
+    s = torch.cuda.current_stream(dev)
+    barrier(world)
+    avg = max_over_ranks(_time_rotating(step, 1, steps, warm, s), world)
+    ok = bool(int((acts[npk:] == _ACT_FWD_AGG).sum()) == npk) and bool((acts[:npk] == _ACT_FWD_ACK).all())
+    idx = _sample_idx(n)
+    ti = torch.from_numpy(idx).to(dev)
+    gl = glob[ti].cpu().numpy()
+    acc = np.zeros(idx.size, np.int64)
+    for x in xs:
+        acc += _np_q32(x[ti].cpu().numpy() - gl, k)
+    acc = ((acc + (1 << 31)) % (1 << 32) - (1 << 31)).astype(np.int32)
+    want = gl + (acc.astype(np.float32) * np.float32(2.0 ** -k)) * np.float32(ws)
+    ok = all_ranks_true(ok and bool(np.array_equal(upd[ti].cpu().numpy().view(np.uint32),
+                                                   want.astype(np.float32).view(np.uint32))), world)
+    rb, npk_all = stride, W * npk
+    path = (W * (8 * n + npk * rb)                        # fused worker quantise + pack
+            + npk * (16 + 8)                              # ack descriptors
+            + npk_all * rb + npk * (4 * V + 5) + npk_all  # switch: packets, registers, actions
+            + npk * rb + 8 * n + 16 * npk)                # PS fused: acks in, local + update, ack rows
+    res = {"workload": ("INA packet path, steady state, PS fused into the switch pass: 8 workers x "
+                        f"{n} fp32 -> quantise(p_w - p_global) + NGA-256 pack -> one switch batch of "
+                        f"{npk} PS acks + {npk_all} worker packets -> completed slots applied to "
+                        "p_global (launch.py:46-50) + ack rows"),
+           "value": round(W * n * 4 / avg / 1e9, 2), "unit": "GB/s (worker fp32 bytes aggregated)",
+           "ms_per_step": round(avg * 1e3, 3), "steps": steps, "warmup": warm,
+           "launches_per_step": W + 1 + 3,
+           "roofline": {"bound": "hbm", "achieved": round(path / avg / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(path / avg / 1e9 / HBM_PEAK_GBS, 4),
+                        "path_bytes_per_step": int(path),
+                        "measures": "the step's algorithmic bytes (all its kernels) / the step time"},
+           "parity_spot_check": ok,
+           "parity_sample": (f"every worker packet completes its slot, every ack frees one; the update at "
+                             f"{idx.size} positions vs numpy quantise + wrapping sum + launch.py update")}
+    del xs, glob, upd, big, desc, acts, sw
+    torch.cuda.empty_cache()
+    return res
+
+
 # -- the packet-stream switch on config 3 (SURVEY 8f-1) ----------------------------------------
 def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
     """ina_switch_process over config 3 as NGA-256 packets: 8 workers x 102,400 packets
@@ -989,6 +1066,7 @@ def run_reduce(args, rank, world, dev, backend):
             run_leg(c5, "a2a", lambda: measure_c5(args, rank, world, dev, collective="a2a"))
     if not args.no_switch:
         run_leg(line, "switch_c3", lambda: measure_switch(dev, rank=rank, world=world))
+        run_leg(line, "packet_path", lambda: measure_packet_path(dev, rank=rank, world=world))
     if cpu_in is not None:
         run_leg(line, "cpu_baseline", lambda: cpu_baseline(args, *cpu_in))
     return line

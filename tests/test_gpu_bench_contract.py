@@ -80,6 +80,11 @@ def test_bench_json_line_contract():
     for order in ("worker_major", "round_robin"):
         assert sw[order]["ok"] is True and sw[order]["slots_completed"] == 102_400
         assert 0 < sw[order]["frac"] < 1
+    pp = d["packet_path"]                        # the whole INA step, PS fused, steady state
+    assert pp["parity_spot_check"] is True and pp["value"] > 0 and pp["ms_per_step"] > 0
+    assert pp["roofline"]["bound"] == "hbm" and 0 < pp["roofline"]["frac"] < 1
+    assert abs(pp["roofline"]["frac"] - pp["roofline"]["achieved"] / pp["roofline"]["peak"]) < 1e-3
+    assert not any(isinstance(v, dict) and "error" in v for v in d.values())   # no leg raised
 
 
 @pytest.mark.gpu
@@ -129,6 +134,7 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert set(c5["roofline"]["hbm_phases"]) == {"quantize", "decode"}
     sw = d["switch_c3"]                          # every rank switched its own bucket
     assert sw["ranks"] == 2 and sw["worker_major"]["ok"] is True and sw["round_robin"]["ok"] is True
+    assert d["packet_path"]["parity_spot_check"] is True
     assert sw["worker_major"]["aggregate_GBps"] > 0
     d = _line(_run("--gpus", "2", "--mode", "sharded", "--wire", "i16", "--c5-values", "1000003",
                    "--c5-steps", "2", env={"INA_BENCH_BACKEND": "gloo"}, timeout=400))
