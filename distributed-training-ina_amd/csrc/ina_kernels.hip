@@ -1247,9 +1247,9 @@ __global__ __launch_bounds__(kBlock) void k_apply_completed_nga(
                     r.y = __fadd_rn(l[b].y, __fmul_rn(__fmul_rn((float)(int32_t)v[1], inv), ws));
                     r.z = __fadd_rn(l[b].z, __fmul_rn(__fmul_rn((float)(int32_t)v[2], inv), ws));
                     r.w = __fadd_rn(l[b].w, __fmul_rn(__fmul_rn((float)(int32_t)v[3], inv), ws));
-                    // a bulk output: written through like the other kernels' (58.0 -> 57.0 us
-                    // cold, nt 56.5; profiles/r03/lab/apply_store_lab.log)
-                    stream_store(r, reinterpret_cast<f32x4*>(out + e));
+                    // nt, like the fused switch pass's PS output (cold: default 58.0 us,
+                    // write-through 57.0, nt 56.5; profiles/r03/lab/apply_store_lab.log)
+                    __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(out + e));
                 } else {
                     for (int t = 0; t < 4 && e + t < n; ++t)
                         out[e + t] = __fadd_rn(local[e + t], __fmul_rn(__fmul_rn((float)(int32_t)v[t], inv), ws));
