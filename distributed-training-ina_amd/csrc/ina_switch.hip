@@ -1017,13 +1017,15 @@ static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWI
 #ifndef INA_SWITCH_ACT_BATCH
 #define INA_SWITCH_ACT_BATCH 1
 #endif
-// forwarded packets and slot registers: written once per call, never read back by it
+// forwarded packets: written once per call, never read back by it (lab knobs: sc1, nt)
 #ifndef INA_SWITCH_STORE_SC1
 #define INA_SWITCH_STORE_SC1 0
 #endif
 __device__ __forceinline__ void sw_st(u32x4s v, u32x4s* p) {
 #if INA_SWITCH_STORE_SC1
     stream_store(v, p);
+#elif INA_SWITCH_FWD_NT
+    __builtin_nontemporal_store(v, p);
 #else
     *p = v;
 #endif
@@ -1326,7 +1328,12 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
             st.count[slot] = (uint8_t)cnt;
             st.frag[slot] = frag;
         }
-        if (have_reg && vl) sw_st(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane));
+        // the slot registers are written once per call and read back only by a later batch
+        // (and then rarely: the first packet of a fresh segment overwrites them), so they
+        // are stored nt and do not displace the packet lines the gather shares in L2:
+        // bench.py's switch leg 228.4 -> 213.9 us worker-major, 217.2 -> 195.1 round-robin
+        // (tools/lab/psout_ab.sh, profiles/r03/lab/switch_reg_nt_lab.log)
+        if (have_reg && vl) __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane));
         }
     }
 }
