@@ -883,7 +883,11 @@ struct SrcQ32 {
     __device__ __forceinline__ u32x4 four(size_t e) const {
         f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + e));
         if (base) {
-            f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base + e));
+            // the base (p_global) is shared: every worker's pack and the PS update read the
+            // same vector, so it is loaded with the default policy and stays in the
+            // Infinity Cache between them (nt: the steady-state 8-worker step 0.690 ->
+            // 0.661 ms; one cold pack unchanged; profiles/r03/lab/qpack_base_lab.log)
+            f32x4 b = *reinterpret_cast<const f32x4*>(base + e);
             a.x = __fsub_rn(a.x, b.x); a.y = __fsub_rn(a.y, b.y);
             a.z = __fsub_rn(a.z, b.z); a.w = __fsub_rn(a.w, b.w);
         }
