@@ -1012,6 +1012,115 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, Nga
     }
 }
 
+// Several workers' fused quantise + pack in ONE launch (a GPU hosting a group of the
+// job's workers; the packet path's W simulated workers): the flat chunk stream of
+// k_pack_nga_flat<SrcQ32>, with every thread producing the same chunk of up to kQpGroup
+// workers' packets.  The shared base chunk (p_global) is loaded once for all of them and
+// the workers' loads are all in flight together; each worker's output stream stays
+// coalesced.  Bytes = the per-worker kernel's, worker by worker.
+constexpr int kQpGroup = 8;
+// store policy of the one-launch worker pack (lab knob): 0 nt like the other packet
+// kernels, 1 write-through (stream_store), 2 the default policy
+#ifndef INA_QPM_STORE
+#define INA_QPM_STORE 0
+#endif
+__device__ __forceinline__ void qpm_store(u32x4 v, u32x4* p) {
+#if INA_QPM_STORE == 1
+    stream_store(v, p);
+#elif INA_QPM_STORE == 2
+    *p = v;
+#else
+    packet_store(v, p);
+#endif
+}
+struct QPackGroup {
+    const float* x[kQpGroup];
+    uint8_t* pkts[kQpGroup];
+    u32x2* desc[kQpGroup];          // all null or all set
+    uint32_t bitmap[kQpGroup], seq0[kQpGroup], fcs[kQpGroup];   // fcs: count | flags<<8 | sw<<16
+};
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_qpack_nga_multi(QPackGroup a, const float* __restrict__ base,
+                                                            size_t n, float s, uint32_t num_slots,
+                                                            uint32_t V, uint32_t C, uint32_t L,
+                                                            uint32_t nch) {
+    const uint32_t gs = gridDim.x * kBlock;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
+    if (a.desc[0]) {                                   // descriptors: thread per packet, coalesced
+        const uint32_t np = nch / C;
+        for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < np; p += gs) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const uint32_t seq = a.seq0[g] + p;
+                const uint32_t bi = bswap(seq % num_slots), bf = bswap(seq);
+                const uint32_t f = a.fcs[g];
+                a.desc[g][p] = u32x2{(f & 0xFFFFu) | (bi << 16),
+                                     (bi >> 16) | (((f >> 16) & 0xFFu) << 16) | (bf << 24)};
+            }
+        }
+    }
+    for (uint32_t t0 = wave0; t0 < nch; t0 += gs) {
+        const uint32_t t = t0 + (uint32_t)lane;
+        const uint32_t p = t / C, c = t - p * C;
+        const bool body = t < nch && c >= 1 && c <= L;
+        const size_t e0 = (size_t)p * V + 4 * (size_t)(c - 1);
+        const bool full = body && e0 + 4 <= n;
+        u32x4 v[G];
+        uint32_t nx0[G];
+        f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (full && base) b = *reinterpret_cast<const f32x4*>(base + e0);   // default policy: shared
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            v[g] = u32x4{0u, 0u, 0u, 0u};
+            if (full) {
+                f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.x[g] + e0));
+                if (base) {
+                    x.x = __fsub_rn(x.x, b.x); x.y = __fsub_rn(x.y, b.y);
+                    x.z = __fsub_rn(x.z, b.z); x.w = __fsub_rn(x.w, b.w);
+                }
+                v[g] = u32x4{(uint32_t)q32(x.x, s), (uint32_t)q32(x.y, s), (uint32_t)q32(x.z, s),
+                             (uint32_t)q32(x.w, s)};
+            } else if (body) {                         // last packet of the bucket: zero tail
+                const SrcQ32 src{a.x[g], base, s};
+                v[g].x = e0 < n ? src.one(e0) : 0u;
+                v[g].y = e0 + 1 < n ? src.one(e0 + 1) : 0u;
+                v[g].z = e0 + 2 < n ? src.one(e0 + 2) : 0u;
+            }
+            nx0[g] = 0u;
+            if (lane == 63 && t < nch && c < L) {      // the next chunk's first value
+                const size_t e = (size_t)p * V + 4 * (size_t)c;
+                nx0[g] = e < n ? SrcQ32{a.x[g], base, s}.one(e) : 0u;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)nx0[g], (int)v[g].x, 0x130,
+                                                                      0xF, 0xF, false);
+            if (t >= nch) continue;
+            u32x4 o;
+            if (c == 0) {
+                const uint32_t seq = a.seq0[g] + p;
+                const uint32_t bi = bswap(seq % num_slots), bf = bswap(seq);
+                const uint32_t f = a.fcs[g];
+                o.x = bswap(a.bitmap[g]);
+                o.y = (f & 0xFFFFu) | (bi << 16);
+                o.z = (bi >> 16) | (((f >> 16) & 0xFFu) << 16) | (bf << 24);
+                o.w = (bf >> 8) | (nx & 0xFF000000u);
+            } else if (c <= L) {
+                o.x = __builtin_amdgcn_perm(v[g].y, v[g].x, kSelWire);
+                o.y = __builtin_amdgcn_perm(v[g].z, v[g].y, kSelWire);
+                o.z = __builtin_amdgcn_perm(v[g].w, v[g].z, kSelWire);
+                o.w = __builtin_amdgcn_perm(nx, v[g].w, kSelWire);
+            } else {
+                o = u32x4{0u, 0u, 0u, 0u};
+            }
+            qpm_store(o, reinterpret_cast<u32x4*>(a.pkts[g]) + t);
+        }
+    }
+}
+
 // generic path: any stride / alignment, thread per output byte
 template <typename Src>
 __global__ __launch_bounds__(kBlock) void k_pack_nga_bytes(Src src, size_t n,
@@ -1832,6 +1941,69 @@ int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
                           const ina_nga_params_t* prm, uint8_t* pkts, size_t pstride,
                           ina_stream_t stream) {
     return ina_quantize_pack_nga_desc(x, base, n, k, prm, pkts, pstride, nullptr, stream);
+}
+
+int ina_quantize_pack_nga_multi(const float* const* x, int W, const float* base, size_t n, int k,
+                                const ina_nga_params_t* prm, uint8_t* const* pkts, size_t pstride,
+                                ina_nga_desc_t* const* desc, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (!x || !prm || !pkts || W < 1 || W > INA_MAX_WORKERS)
+        return set_error(INA_EINVAL, "x, prm, pkts non-null and W in [1, %s]", "64");
+    const int V = prm[0].V;
+    if (V <= 0 || prm[0].num_slots == 0) return set_error(INA_EINVAL, "bad nga params%s", "");
+    if (pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V)
+        return set_error(INA_EINVAL, "stride < 15 + 4V%s", "");
+    bool flat = pstride % 16 == 0 && V % 4 == 0 && (!base || aligned16(base));
+    for (int w = 0; w < W; ++w) {
+        if (prm[w].V != V || prm[w].num_slots != prm[0].num_slots)
+            return set_error(INA_EINVAL, "every worker needs the same V and num_slots%s", "");
+        if ((n && !x[w]) || !pkts[w]) return set_error(INA_EINVAL, "null worker buffer%s", "");
+        if (desc && (!desc[w] || ((uintptr_t)desc[w] & 7u)))
+            return set_error(INA_EINVAL, "descriptors must be non-null and 8-byte aligned%s", "");
+        flat &= aligned16(x[w]) && aligned16(pkts[w]);
+    }
+    const size_t npk = (n + (size_t)V - 1) / (size_t)V;
+    if (npk == 0) return INA_OK;
+    hipStream_t s = hs(stream);
+    if (!flat) {     // generic layouts: the per-worker byte path, worker by worker
+        for (int w = 0; w < W; ++w)
+            if (int rc = ina_quantize_pack_nga_desc(x[w], base, n, k, &prm[w], pkts[w], pstride,
+                                                    desc ? desc[w] : nullptr, stream))
+                return rc;
+        return INA_OK;
+    }
+    const float sc = ldexpf(1.0f, k);
+    const size_t C = pstride / 16;
+    const size_t per = std::max<size_t>(1, (size_t)g_launch_chunks.load() / C);
+    for (int w0 = 0; w0 < W; w0 += kQpGroup) {
+        const int G = std::min(kQpGroup, W - w0);
+        for (size_t p0 = 0; p0 < npk; p0 += per) {     // 32-bit chunk indices: packet ranges
+            const size_t np = npk - p0 < per ? npk - p0 : per;
+            const size_t v0 = p0 * (size_t)V;
+            QPackGroup a{};
+            for (int g = 0; g < G; ++g) {
+                const ina_nga_params_t& q = prm[w0 + g];
+                a.x[g] = x[w0 + g] + v0;
+                a.pkts[g] = pkts[w0 + g] + p0 * pstride;
+                a.desc[g] = desc ? reinterpret_cast<u32x2*>(desc[w0 + g] + p0) : nullptr;
+                a.bitmap[g] = q.bitmap;
+                a.seq0[g] = q.seq0 + (uint32_t)p0;
+                a.fcs[g] = (uint32_t)q.count | ((uint32_t)q.flags << 8) | ((uint32_t)q.switch_id << 16);
+            }
+            const dim3 grid(grid_for(np * C, 1, g_stream_blocks)), blk(kBlock);
+            const float* bp = base ? base + v0 : nullptr;
+            const size_t nn = n - v0;
+            const uint32_t ns = prm[0].num_slots, VV = (uint32_t)V, CC = (uint32_t)C, L = (uint32_t)(V / 4),
+                           nch = (uint32_t)(np * C);
+            switch (G) {
+#define INA_QPM(g_) case g_: hipLaunchKernelGGL(k_qpack_nga_multi<g_>, grid, blk, 0, s, a, bp, nn, sc, ns, \
+                                                VV, CC, L, nch); break;
+                INA_QPM(1) INA_QPM(2) INA_QPM(3) INA_QPM(4) INA_QPM(5) INA_QPM(6) INA_QPM(7) INA_QPM(8)
+#undef INA_QPM
+            }
+        }
+    }
+    return check_launch("quantize_pack_nga_multi");
 }
 
 int ina_nga_descriptors(const uint8_t* pkts, size_t npk, size_t pstride, ina_nga_desc_t* desc,

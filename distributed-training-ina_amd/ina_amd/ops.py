@@ -347,6 +347,51 @@ def quantize_pack_nga(x: torch.Tensor, k: int, V: int, bitmap: int, count: int, 
     return (out, d) if d is not None else out
 
 
+def quantize_pack_nga_multi(xs, k: int, V: int, bitmaps, count: int, switch_id: int, seq0,
+                            base: torch.Tensor | None = None, flags: int = 0,
+                            num_slots: int = NUM_REGISTER, stride: int | None = None,
+                            outs=None, descs=None):
+    """W workers' quantize_pack_nga in ONE launch (ina_quantize_pack_nga_multi): worker w's
+    packets of quantize(xs[w] - base, k) with header word bitmaps[w] and sequence start
+    seq0 (an int for all workers or one per worker); the shared base is read once for
+    every 8 workers.  Same bytes as W quantize_pack_nga calls.  outs / descs: W tensors
+    each (descs=True allocates them); returns outs, or (outs, descs)."""
+    xs, n = _bufs(xs, torch.float32, "xs")
+    W, dev = len(xs), xs[0].device
+    if base is not None:
+        _req(base, torch.float32, "base")
+        if base.numel() != n:
+            raise ValueError("base and xs differ in length")
+        _same_device(xs[0], base)
+    bitmaps = list(bitmaps)
+    seqs = [int(seq0)] * W if isinstance(seq0, int) else list(seq0)
+    if len(bitmaps) != W or len(seqs) != W:
+        raise ValueError("one bitmap and one seq0 per worker")
+    stride = stride or nga_stride(V)
+    npk = (n + V - 1) // V
+    if outs is None:
+        outs = [torch.empty((npk, stride), dtype=torch.uint8, device=dev) for _ in range(W)]
+    outs = list(outs)
+    if len(outs) != W:
+        raise ValueError("one output per worker")
+    for o in outs:
+        _fits(o, npk * stride)
+        _req(o, torch.uint8, "outs")
+        _same_device(xs[0], o)
+    ds = None
+    if descs is not None and descs is not False:
+        ds = [_desc_arg(True if descs is True else descs[w], npk, dev) for w in range(W)]
+    prm = (_lib.NgaParams * W)(*[_lib.NgaParams(bitmaps[w] & 0xFFFFFFFF, count & 0xFF, flags & 0xFF,
+                                                switch_id & 0xFF, 0, seqs[w] & 0xFFFFFFFF, num_slots, V)
+                                 for w in range(W)])
+    check(load().ina_quantize_pack_nga_multi(
+        ptr_array([x.data_ptr() for x in xs]), W, base.data_ptr() if base is not None else None, n, k,
+        prm, ptr_array([o.data_ptr() for o in outs]), stride,
+        ptr_array([d.data_ptr() for d in ds]) if ds is not None else None, _stream(xs[0])),
+        "quantize_pack_nga_multi")
+    return (outs, ds) if ds is not None else outs
+
+
 def unpack_nga(pkts: torch.Tensor, V: int, stride: int | None = None, with_values: bool = True):
     """Returns (fields dict of device tensors, int32 values [npkts*V] or None)."""
     _req(pkts, torch.uint8, "pkts")

@@ -211,6 +211,15 @@ int ina_quantize_pack_nga_desc(const float* x, const float* base, size_t n, int 
                                ina_nga_desc_t* desc, ina_stream_t stream);
 int ina_nga_descriptors(const uint8_t* pkts, size_t npkts, size_t stride, ina_nga_desc_t* desc,
                         ina_stream_t stream);
+/* W workers' fused quantise + pack in one launch (a GPU hosting a group of the job's
+ * workers): worker w's x[w] - base (base shared, may be NULL) into pkts[w] with header
+ * prm[w] and descriptors desc[w] (desc itself may be NULL) -- exactly the bytes of W calls
+ * of ina_quantize_pack_nga_desc (DataManager.py:37 + 111-165 per worker), with the base
+ * read once for every 8 workers.  Every prm[w] has the same V and num_slots; W <= 64;
+ * x, pkts and desc are host arrays of W device pointers. */
+int ina_quantize_pack_nga_multi(const float* const* x, int W, const float* base, size_t n, int k,
+                                const ina_nga_params_t* prm, uint8_t* const* pkts, size_t stride,
+                                ina_nga_desc_t* const* desc, ina_stream_t stream);
 /* PS-side parse (NGAPacket.py:62-143 / get_data_from_nic, utils.py:61-64), following
  * headers.p4: payload at byte 15, big-endian.  vals gets npkts*V int32 (may be NULL). */
 int ina_unpack_nga(const uint8_t* pkts, size_t npkts, int V, size_t stride,

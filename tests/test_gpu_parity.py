@@ -1204,6 +1204,54 @@ def test_quantize_pack_fused_matches_oracle(V, with_base, padded):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("V,W,with_base,padded", [
+    (256, 8, True, True), (256, 8, False, True), (32, 3, True, True), (256, 13, True, True),
+    (256, 1, True, True), (4, 5, True, True), (100, 2, True, True), (256, 17, True, True),
+    (32, 4, True, False), (256, 2, False, False)])
+def test_quantize_pack_multi_matches_oracle(V, W, with_base, padded):
+    """W workers' quantise + pack in one launch (groups of 8, per-worker bitmaps and
+    sequence starts, descriptors) == the oracle's quantize then pack worker by worker;
+    unpadded strides and V % 4 != 0 take the per-worker byte path, same bytes."""
+    o = ops()
+    rng = np.random.default_rng(1000 * V + W + 2 * with_base + padded)
+    n = 61 * V + 7                                  # ragged last packet
+    xs = [mixed_floats(rng, n) for _ in range(W)]
+    base = (rng.standard_normal(n) * 0.1).astype(np.float32) if with_base else None
+    stride = o.nga_stride(V) if padded else 15 + 4 * V
+    seqs = [int(s) for s in rng.integers(0, 2**32 - 100, W)]
+    seqs[0] = 2**32 - 30                            # sequence numbers wrap inside the bucket
+    outs, descs = o.quantize_pack_nga_multi([dev(x) for x in xs], 16, V, [w + 1 for w in range(W)],
+                                            W, 1, seqs, base=dev(base) if with_base else None,
+                                            num_slots=1000, stride=stride, descs=True)
+    for w, x in enumerate(xs):
+        d = (x - base).astype(np.float32) if with_base else x
+        want = orc.pack_nga(orc.quantize_i32(d, 16), V, w + 1, W, 1, seqs[w], stride=stride,
+                            num_slots=1000)
+        got = host(outs[w])
+        assert np.array_equal(got, want), w
+        dw = host(descs[w]).view(np.uint8).reshape(-1, 8)
+        assert np.array_equal(dw, want.reshape(-1, stride)[:, 4:12]), w
+
+
+def test_quantize_pack_multi_split_launches():
+    """Packet ranges (a small launch_chunks forces them) carry every worker's sequence."""
+    o = ops()
+    rng = np.random.default_rng(7)
+    V, W, n = 256, 9, 256 * 23 + 100
+    xs = [mixed_floats(rng, n) for _ in range(W)]
+    base = (rng.standard_normal(n) * 0.1).astype(np.float32)
+    try:
+        o.set_tuning(launch_chunks=65 * 5)
+        outs = o.quantize_pack_nga_multi([dev(x) for x in xs], 12, V, [7] * W, 8, 2,
+                                         [100 * w for w in range(W)], base=dev(base))
+    finally:
+        o.set_tuning(launch_chunks=2**31 - 1)
+    for w, x in enumerate(xs):
+        want = orc.pack_nga(orc.quantize_i32((x - base).astype(np.float32), 12), V, 7, 8, 2,
+                            100 * w, stride=o.nga_stride(V))
+        assert np.array_equal(host(outs[w]), want), w
+
+
 @pytest.mark.parametrize("V,W", [(256, 8), (32, 3), (128, 4), (100, 5), (4, 2)])
 def test_switch_then_fused_apply_matches_oracle(V, W):
     """PS side: device switch over W worker streams, then one fused kernel places,

@@ -20,6 +20,14 @@ for st in $STAGES; do
     test)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -25 "$OUT/pytest_gpu.log"; ok_or_fail pytest $rc ;;
+    lab:*)
+      nm=${st#lab:}
+      timeout -k 10 300 python tools/lab/$nm.py > "$OUT/$nm.log" 2>&1
+      rc=$?; cat "$OUT/$nm.log"; [ $rc -ne 0 ] && fatal "$st" $rc ;;
+    ptest:*)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread \
+        -k "${st#ptest:}" > "$OUT/ptest.log" 2>&1
+      rc=$?; tail -8 "$OUT/ptest.log"; ok_or_fail "$st" $rc ;;
     ew16lab)
       timeout -k 10 300 python tools/lab/ew16_lab.py > "$OUT/ew16_lab.log" 2>&1
       rc=$?; cat "$OUT/ew16_lab.log"; [ $rc -ne 0 ] && fatal ew16lab $rc ;;
