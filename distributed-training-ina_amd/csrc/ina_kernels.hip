@@ -1121,6 +1121,87 @@ __global__ __launch_bounds__(kBlock) void k_qpack_nga_multi(QPackGroup a, const 
     }
 }
 
+// NGA-256 (64 value chunks per packet): a wave per packet.  Lane l holds values 4l..4l+3
+// (one aligned 1 KiB load per worker) and writes value chunk l + 1; the next chunk's first
+// value comes from lane l + 1 (DPP wave_shl:1), lane 63's is value 256 = the zero past the
+// packet, so no lane loads anything twice or alone; lane 0 also writes the header chunk.
+// (one launch, 8 workers, config 3: 343 -> 329 us, the steady packet-path step 587 -> 563 us;
+// write-through or default-policy stores are slower in both layouts, qpack_multi_lab.log)
+#ifndef INA_QPM_PPW
+#define INA_QPM_PPW 1
+#endif
+#ifndef INA_QPM_PPW_BLOCKS
+#define INA_QPM_PPW_BLOCKS (1 << 20)      // a covering grid (a wave per packet)
+#endif
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_qpack_nga_multi_v256(QPackGroup a, const float* __restrict__ base,
+                                                                 size_t n, float s, uint32_t num_slots,
+                                                                 uint32_t stride, uint32_t np) {
+    const uint32_t gs = gridDim.x * kBlock;
+    const int lane = threadIdx.x & 63;
+    if (a.desc[0]) {
+        for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < np; p += gs) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const uint32_t seq = a.seq0[g] + p;
+                const uint32_t bi = bswap(seq % num_slots), bf = bswap(seq);
+                const uint32_t f = a.fcs[g];
+                a.desc[g][p] = u32x2{(f & 0xFFFFu) | (bi << 16),
+                                     (bi >> 16) | (((f >> 16) & 0xFFu) << 16) | (bf << 24)};
+            }
+        }
+    }
+    const uint32_t nwaves = gs >> 6, pad = stride / 16 - 65;
+    for (uint32_t p = (blockIdx.x * kBlock + threadIdx.x) >> 6; p < np; p += nwaves) {
+        const size_t e0 = (size_t)p * 256 + 4 * (size_t)lane;
+        const bool full = e0 + 4 <= n;
+        u32x4 v[G];
+        f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (full && base) b = *reinterpret_cast<const f32x4*>(base + e0);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            v[g] = u32x4{0u, 0u, 0u, 0u};
+            if (full) {
+                f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.x[g] + e0));
+                if (base) {
+                    x.x = __fsub_rn(x.x, b.x); x.y = __fsub_rn(x.y, b.y);
+                    x.z = __fsub_rn(x.z, b.z); x.w = __fsub_rn(x.w, b.w);
+                }
+                v[g] = u32x4{(uint32_t)q32(x.x, s), (uint32_t)q32(x.y, s), (uint32_t)q32(x.z, s),
+                             (uint32_t)q32(x.w, s)};
+            } else {
+                const SrcQ32 src{a.x[g], base, s};
+                v[g].x = e0 < n ? src.one(e0) : 0u;
+                v[g].y = e0 + 1 < n ? src.one(e0 + 1) : 0u;
+                v[g].z = e0 + 2 < n ? src.one(e0 + 2) : 0u;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[g].x, 0x130, 0xF, 0xF, false);
+            u32x4* row = reinterpret_cast<u32x4*>(a.pkts[g] + (size_t)p * stride);
+            u32x4 o;
+            o.x = __builtin_amdgcn_perm(v[g].y, v[g].x, kSelWire);
+            o.y = __builtin_amdgcn_perm(v[g].z, v[g].y, kSelWire);
+            o.z = __builtin_amdgcn_perm(v[g].w, v[g].z, kSelWire);
+            o.w = __builtin_amdgcn_perm(nx, v[g].w, kSelWire);
+            qpm_store(o, row + 1 + lane);
+            if (lane == 0) {
+                const uint32_t seq = a.seq0[g] + p;
+                const uint32_t bi = bswap(seq % num_slots), bf = bswap(seq);
+                const uint32_t f = a.fcs[g];
+                u32x4 h;
+                h.x = bswap(a.bitmap[g]);
+                h.y = (f & 0xFFFFu) | (bi << 16);
+                h.z = (bi >> 16) | (((f >> 16) & 0xFFu) << 16) | (bf << 24);
+                h.w = (bf >> 8) | (v[g].x & 0xFF000000u);
+                qpm_store(h, row);
+            }
+            if ((uint32_t)lane < pad) qpm_store(u32x4{0u, 0u, 0u, 0u}, row + 65 + lane);
+        }
+    }
+}
+
 // generic path: any stride / alignment, thread per output byte
 template <typename Src>
 __global__ __launch_bounds__(kBlock) void k_pack_nga_bytes(Src src, size_t n,
@@ -1990,9 +2071,20 @@ int ina_quantize_pack_nga_multi(const float* const* x, int W, const float* base,
                 a.seq0[g] = q.seq0 + (uint32_t)p0;
                 a.fcs[g] = (uint32_t)q.count | ((uint32_t)q.flags << 8) | ((uint32_t)q.switch_id << 16);
             }
-            const dim3 grid(grid_for(np * C, 1, g_stream_blocks)), blk(kBlock);
+            const dim3 blk(kBlock);
             const float* bp = base ? base + v0 : nullptr;
             const size_t nn = n - v0;
+            if (INA_QPM_PPW && V == 256 && C <= 65 + 64) {          // a wave per packet
+                const dim3 grid(grid_for(np * 64, 1, INA_QPM_PPW_BLOCKS));
+                switch (G) {
+#define INA_QPM(g_) case g_: hipLaunchKernelGGL(k_qpack_nga_multi_v256<g_>, grid, blk, 0, s, a, bp, nn, sc, \
+                                                prm[0].num_slots, (uint32_t)pstride, (uint32_t)np); break;
+                    INA_QPM(1) INA_QPM(2) INA_QPM(3) INA_QPM(4) INA_QPM(5) INA_QPM(6) INA_QPM(7) INA_QPM(8)
+#undef INA_QPM
+                }
+                continue;
+            }
+            const dim3 grid(grid_for(np * C, 1, g_stream_blocks));
             const uint32_t ns = prm[0].num_slots, VV = (uint32_t)V, CC = (uint32_t)C, L = (uint32_t)(V / 4),
                            nch = (uint32_t)(np * C);
             switch (G) {

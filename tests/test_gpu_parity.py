@@ -1207,17 +1207,18 @@ def test_quantize_pack_fused_matches_oracle(V, with_base, padded):
 @pytest.mark.parametrize("V,W,with_base,padded", [
     (256, 8, True, True), (256, 8, False, True), (32, 3, True, True), (256, 13, True, True),
     (256, 1, True, True), (4, 5, True, True), (100, 2, True, True), (256, 17, True, True),
-    (32, 4, True, False), (256, 2, False, False)])
+    (32, 4, True, False), (256, 2, False, False), (256, 3, True, "wide"), (256, 9, True, "wide")])
 def test_quantize_pack_multi_matches_oracle(V, W, with_base, padded):
     """W workers' quantise + pack in one launch (groups of 8, per-worker bitmaps and
     sequence starts, descriptors) == the oracle's quantize then pack worker by worker;
-    unpadded strides and V % 4 != 0 take the per-worker byte path, same bytes."""
+    V = 256 takes the wave-per-packet kernel (wide strides: zeroed padding chunks), other
+    V the flat chunk stream, unpadded strides the per-worker byte path; same bytes."""
     o = ops()
-    rng = np.random.default_rng(1000 * V + W + 2 * with_base + padded)
+    rng = np.random.default_rng(1000 * V + W + 2 * with_base + (padded is True))
     n = 61 * V + 7                                  # ragged last packet
     xs = [mixed_floats(rng, n) for _ in range(W)]
     base = (rng.standard_normal(n) * 0.1).astype(np.float32) if with_base else None
-    stride = o.nga_stride(V) if padded else 15 + 4 * V
+    stride = {True: o.nga_stride(V), False: 15 + 4 * V, "wide": o.nga_stride(V) + 48}[padded]
     seqs = [int(s) for s in rng.integers(0, 2**32 - 100, W)]
     seqs[0] = 2**32 - 30                            # sequence numbers wrap inside the bucket
     outs, descs = o.quantize_pack_nga_multi([dev(x) for x in xs], 16, V, [w + 1 for w in range(W)],

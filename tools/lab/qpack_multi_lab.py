@@ -86,18 +86,17 @@ for gb in (4096, 8192, 16384, 32768, 65536):
     print(f"grid {gb:6d}: one launch {t1:7.1f} us ({b1 / t1 / 8e6:.3f})")
 ops.set_tuning(stream_blocks=16384)
 
-# store-policy variants of the one launch (tools/lab/libina_qpm{0,1,2}.so: nt, write-through,
-# default), each called through its own library, alone and inside the step, alternated
+# variants of the one launch (tools/lab/libina_qpm_<layout>_<store>.so: flat chunk stream or a
+# wave per packet; nt, write-through or default-policy stores), each called through its own library, alone and inside the step, alternated
 import ctypes as C  # noqa: E402
 from ina_amd import _lib  # noqa: E402
 here = os.path.dirname(os.path.abspath(__file__))
 libs = {}
-for v, nm in ((0, "nt"), (1, "sc1"), (2, "default")):
-    path = os.path.join(here, f"libina_qpm{v}.so")
-    if os.path.exists(path):
-        lib = C.CDLL(path)
+for f in sorted(os.listdir(here)):          # libina_qpm_<layout>_<store>[_<grid>].so
+    if f.startswith("libina_qpm_") and f.endswith(".so"):
+        lib = C.CDLL(os.path.join(here, f))
         lib.ina_quantize_pack_nga_multi.argtypes = _lib.SIGNATURES["ina_quantize_pack_nga_multi"]
-        libs[nm] = lib
+        libs[f[len("libina_qpm_"):-3]] = lib
 prm = (_lib.NgaParams * W)(*[_lib.NgaParams(w + 1, W, 0, 1, 0, 1, slots, V) for w in range(W)])
 xa = _lib.ptr_array([x.data_ptr() for x in xs])
 oa = _lib.ptr_array([o.data_ptr() for o in outs])
@@ -119,4 +118,4 @@ for r in range(3):
     for nm, lib in libs.items():
         t1 = timed(via(lib))
         st = timed(lambda: step(via(lib)), reps=10, warm=3)
-        print(f"round {r}: {nm:8s} one launch {t1:7.1f} us ({b1 / t1 / 8e6:.3f})   steady step {st:7.1f} us")
+        print(f"round {r}: {nm:12s} one launch {t1:7.1f} us ({b1 / t1 / 8e6:.3f})   steady step {st:7.1f} us")
