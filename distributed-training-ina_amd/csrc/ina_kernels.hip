@@ -1133,8 +1133,15 @@ __global__ __launch_bounds__(kBlock) void k_qpack_nga_multi(QPackGroup a, const 
 #ifndef INA_QPM_PPW_BLOCKS
 #define INA_QPM_PPW_BLOCKS (1 << 20)      // a covering grid (a wave per packet)
 #endif
+#ifndef INA_QPM_WPE
+#define INA_QPM_WPE 0       // lab knob: amdgpu_waves_per_eu minimum (0: the compiler's choice)
+#endif
 template <int G>
-__global__ __launch_bounds__(kBlock) void k_qpack_nga_multi_v256(QPackGroup a, const float* __restrict__ base,
+__global__ __launch_bounds__(kBlock)
+#if INA_QPM_WPE
+__attribute__((amdgpu_waves_per_eu(INA_QPM_WPE, 8)))
+#endif
+void k_qpack_nga_multi_v256(QPackGroup a, const float* __restrict__ base,
                                                                  size_t n, float s, uint32_t num_slots,
                                                                  uint32_t stride, uint32_t np) {
     const uint32_t gs = gridDim.x * kBlock;
