@@ -321,6 +321,26 @@ def run_extra(dev):
                      acks_and_slots_ok=ok,
                      note="ina_switch_process_apply(keep_forwarded=0): bytes = the steady-state row's "
                           "minus the PS's re-read of completed packets and their write-back"))
+    # the same with the 8 worker packs as ONE launch (ina_quantize_pack_nga_multi: the
+    # shared base is read once for the 8 workers) -- bench.py's packet_path leg
+    outs_w2, descs_w2 = list(rows_w2.unbind(0)), list(desc_w2.unbind(0))
+
+    def ina_step_fused_multi():
+        ops.quantize_pack_nga_multi(xs, 16, V, [w + 1 for w in range(Ws)], Ws, 1, 1, base=glob_p,
+                                    num_slots=1 << 17, outs=outs_w2, descs=descs_w2)
+        ops.nga_descriptors(ack_rows, out=desc_ack)
+        sw3.process_apply(big, 1, glob_p, 16, 1.0 / (Ws + 1), out=upd, acks=ack_rows,
+                          keep_forwarded=False, actions=acts2, desc=desc_big)
+    ina_step_fused_multi()
+    t = _time(ina_step_fused_multi, reps=5, warm=1)
+    ina_step_fused_multi()
+    torch.cuda.synchronize()
+    ok = bool((acts2[npk:] == 1).sum() == npk) and bool((acts2[:npk] == 3).all())
+    rows.append(_row("INA packet path step, steady state, PS fused, the 8 worker packs in one launch",
+                     t, fused_bytes - (Ws - 1) * n3 * 4, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
+                     acks_and_slots_ok=ok,
+                     note="ina_quantize_pack_nga_multi + ina_switch_process_apply; bytes = the row above "
+                          "with the shared base read once"))
     # the same step recorded once as a hipGraph and replayed: the step's 15 launches (8
     # worker packs, the descriptor pass, the switch's 5 sort/run launches, ...) leave the
     # CPU and the launch queue

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <atomic>
 #include <cstdio>
@@ -1121,6 +1122,27 @@ __global__ __launch_bounds__(kBlock) void k_qpack_nga_multi(QPackGroup a, const 
     }
 }
 
+// Descriptors from the header parameters alone (no packet read): what the pack kernels
+// write beside each packet, for up to kQpGroup workers of npk packets each -- so a switch's
+// slot sort can start before the payload exists.
+struct DescGroup {
+    u32x2* desc[kQpGroup];
+    uint32_t seq0[kQpGroup], fcs[kQpGroup];
+};
+__global__ __launch_bounds__(kBlock) void k_nga_make_desc(DescGroup a, int G, uint32_t num_slots,
+                                                          uint32_t np) {
+    const uint32_t gs = gridDim.x * kBlock;
+    for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < np; p += gs) {
+        for (int g = 0; g < G; ++g) {
+            const uint32_t seq = a.seq0[g] + p;
+            const uint32_t bi = bswap(seq % num_slots), bf = bswap(seq);
+            const uint32_t f = a.fcs[g];
+            a.desc[g][p] = u32x2{(f & 0xFFFFu) | (bi << 16),
+                                 (bi >> 16) | (((f >> 16) & 0xFFu) << 16) | (bf << 24)};
+        }
+    }
+}
+
 // NGA-256 (64 value chunks per packet): a wave per packet.  Lane l holds values 4l..4l+3
 // (one aligned 1 KiB load per worker) and writes value chunk l + 1; the next chunk's first
 // value comes from lane l + 1 (DPP wave_shl:1), lane 63's is value 256 = the zero past the
@@ -1206,6 +1228,64 @@ void k_qpack_nga_multi_v256(QPackGroup a, const float* __restrict__ base,
             }
             if ((uint32_t)lane < pad) qpm_store(u32x4{0u, 0u, 0u, 0u}, row + 65 + lane);
         }
+    }
+}
+
+// One worker's NGA-256 packets, a wave per packet (the layout of k_qpack_nga_multi_v256):
+// fp32 quantised on the fly (int32 words and the per-packet overflow flag are supported; the
+// int32 pack is faster on the flat stream, see pack_nga_launch).
+#ifndef INA_PACK_PPW
+#define INA_PACK_PPW 1
+#endif
+template <typename Src>
+__global__ __launch_bounds__(kBlock) void k_pack_nga_v256(Src src, size_t n, NgaHdr h,
+                                                          const uint8_t* __restrict__ ovf,
+                                                          uint8_t* __restrict__ pkts, uint32_t stride,
+                                                          uint32_t np, u32x2* __restrict__ desc) {
+    const uint32_t gs = gridDim.x * kBlock;
+    const int lane = threadIdx.x & 63;
+    const uint32_t count = h.flags_count_sw & 0xFFu, sw = (h.flags_count_sw >> 16) & 0xFFu;
+    if (desc) {
+        for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < np; p += gs) {
+            const uint32_t seq = h.seq0 + p;
+            const uint32_t bi = bswap(seq % h.num_slots), bf = bswap(seq);
+            uint32_t flags = (h.flags_count_sw >> 8) & 0xFFu;
+            if (ovf && ovf[p]) flags |= INA_FLAG_OVERFLOW;
+            desc[p] = u32x2{count | (flags << 8) | (bi << 16), (bi >> 16) | (sw << 16) | (bf << 24)};
+        }
+    }
+    const uint32_t nwaves = gs >> 6, pad = stride / 16 - 65;
+    for (uint32_t p = (blockIdx.x * kBlock + threadIdx.x) >> 6; p < np; p += nwaves) {
+        const size_t e0 = (size_t)p * 256 + 4 * (size_t)lane;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (e0 + 4 <= n) {
+            v = src.four(e0);
+        } else {
+            v.x = e0 < n ? src.one(e0) : 0u;
+            v.y = e0 + 1 < n ? src.one(e0 + 1) : 0u;
+            v.z = e0 + 2 < n ? src.one(e0 + 2) : 0u;
+        }
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x130, 0xF, 0xF, false);
+        u32x4* row = reinterpret_cast<u32x4*>(pkts + (size_t)p * stride);
+        u32x4 o;
+        o.x = __builtin_amdgcn_perm(v.y, v.x, kSelWire);
+        o.y = __builtin_amdgcn_perm(v.z, v.y, kSelWire);
+        o.z = __builtin_amdgcn_perm(v.w, v.z, kSelWire);
+        o.w = __builtin_amdgcn_perm(nx, v.w, kSelWire);
+        packet_store(o, row + 1 + lane);
+        if (lane == 0) {
+            const uint32_t seq = h.seq0 + p;
+            const uint32_t bi = bswap(seq % h.num_slots), bf = bswap(seq);
+            uint32_t flags = (h.flags_count_sw >> 8) & 0xFFu;
+            if (ovf && ovf[p]) flags |= INA_FLAG_OVERFLOW;
+            u32x4 hd;
+            hd.x = bswap(h.bitmap);
+            hd.y = count | (flags << 8) | (bi << 16);
+            hd.z = (bi >> 16) | (sw << 16) | (bf << 24);
+            hd.w = (bf >> 8) | (v.x & 0xFF000000u);
+            packet_store(hd, row);
+        }
+        if ((uint32_t)lane < pad) packet_store(u32x4{0u, 0u, 0u, 0u}, row + 65 + lane);
     }
 }
 
@@ -1736,6 +1816,17 @@ static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina
             const size_t v0 = p0 * (size_t)V;
             NgaHdr hp = h;
             hp.seq0 = h.seq0 + (uint32_t)p0;
+            // a wave per packet for the fused worker pack (cold, one launch: 53.2 -> 48.9 us);
+            // the int32 pack stays on the flat stream (36.5 -> 39.1 us with a wave per
+            // packet: one 16-byte load per lane leaves too little in flight),
+            // profiles/r03/lab/pack_ppw_lab.log
+            if (INA_PACK_PPW && std::is_same_v<Src, SrcQ32> && V == 256 && C <= 65 + 64) {
+                hipLaunchKernelGGL((k_pack_nga_v256<Src>), dim3(grid_for(np * 64, 1, 1 << 20)), dim3(kBlock), 0, s,
+                                   src.shifted(v0), n - v0, hp, ovf ? ovf + p0 : nullptr, pkts + p0 * pstride,
+                                   (uint32_t)pstride, (uint32_t)np,
+                                   desc ? reinterpret_cast<u32x2*>(desc + p0) : nullptr);
+                continue;
+            }
             hipLaunchKernelGGL((k_pack_nga_flat<Src, INA_PACK_U>), dim3(grid_for(np * C, INA_PACK_U, g_stream_blocks)),
                                dim3(kBlock), 0, s, src.shifted(v0), n - v0, hp, ovf ? ovf + p0 : nullptr,
                                pkts + p0 * pstride, (uint32_t)C, (uint32_t)(V / 4), (uint32_t)(np * C),
@@ -2029,6 +2120,33 @@ int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
                           const ina_nga_params_t* prm, uint8_t* pkts, size_t pstride,
                           ina_stream_t stream) {
     return ina_quantize_pack_nga_desc(x, base, n, k, prm, pkts, pstride, nullptr, stream);
+}
+
+int ina_nga_make_descriptors(const ina_nga_params_t* prm, int W, size_t npk, ina_nga_desc_t* const* desc,
+                             ina_stream_t stream) {
+    if (!prm || !desc || W < 1 || W > INA_MAX_WORKERS)
+        return set_error(INA_EINVAL, "prm, desc non-null and W in [1, %s]", "64");
+    if (npk > 0xFFFFFFFFu) return set_error(INA_EINVAL, "too many packets%s", "");
+    for (int w = 0; w < W; ++w) {
+        if (prm[w].num_slots == 0 || prm[w].num_slots != prm[0].num_slots)
+            return set_error(INA_EINVAL, "every worker needs the same non-zero num_slots%s", "");
+        if (!desc[w] || ((uintptr_t)desc[w] & 7u))
+            return set_error(INA_EINVAL, "descriptors must be non-null and 8-byte aligned%s", "");
+    }
+    if (npk == 0) return INA_OK;
+    for (int w0 = 0; w0 < W; w0 += kQpGroup) {
+        const int G = std::min(kQpGroup, W - w0);
+        DescGroup a{};
+        for (int g = 0; g < G; ++g) {
+            const ina_nga_params_t& q = prm[w0 + g];
+            a.desc[g] = reinterpret_cast<u32x2*>(desc[w0 + g]);
+            a.seq0[g] = q.seq0;
+            a.fcs[g] = (uint32_t)q.count | ((uint32_t)q.flags << 8) | ((uint32_t)q.switch_id << 16);
+        }
+        hipLaunchKernelGGL(k_nga_make_desc, dim3(grid_for(npk, 1)), dim3(kBlock), 0, hs(stream), a, G,
+                           prm[0].num_slots, (uint32_t)npk);
+    }
+    return check_launch("nga_make_descriptors");
 }
 
 int ina_quantize_pack_nga_multi(const float* const* x, int W, const float* base, size_t n, int k,

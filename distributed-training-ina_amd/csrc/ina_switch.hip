@@ -638,6 +638,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     // the batch is not in slot order: B sorts (else B only copies A's output, which is then
     // the identity permutation).  Tagged with the call's epoch, so nothing needs clearing.
     if (__ballot(down) && lane == 0) unsorted[0] = epoch;
+    if (c == 0 && threadIdx.x == 0) unsorted[1] = epoch;     // this call's epoch, for the run kernel
     __syncthreads();
     // thread d owns digit d: the chunk's count, its chunk-local run start (block scan)
     const uint32_t d = threadIdx.x;
@@ -1366,12 +1367,14 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                           const uint32_t* __restrict__ nforeign,
                                                           const uint32_t* __restrict__ keys_a,
                                                           const uint32_t* __restrict__ ids_a,
-                                                          const uint32_t* __restrict__ unsorted, uint32_t epoch) {
+                                                          const uint32_t* __restrict__ unsorted) {
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
     // a batch already in slot order: the chunk sort's own output is the sorted order
-    if (unsorted && unsorted[0] != epoch) {
+    // (unsorted[1]: the epoch of the sort that filled the scratch, written by its chunk pass,
+    // so a run queued apart from its sort needs no host-side state)
+    if (unsorted && unsorted[0] != unsorted[1]) {
         keys = keys_a;
         ids = ids_a;
     }
@@ -1441,7 +1444,8 @@ struct SortAux {
     uint32_t* rst;                // [2^bits][nch]
     uint32_t* totals;             // [512]
     uint32_t* nforeign;           // [1]
-    uint32_t* unsorted;           // [1]: the epoch of the last call whose keys were out of order
+    uint32_t* unsorted;           // [2]: the epoch of the last call whose keys were out of order,
+                                  // the epoch of the last chunk pass
 };
 
 static size_t sort_hist_cap(size_t npk, uint32_t num_slots) {
@@ -1519,10 +1523,17 @@ size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots) {
     return 4 * align_up(npkts * 4, 256) + align_up(sort_temp_bytes(npkts, num_slots), 256) + 256;
 }
 
+// phase: 0 sort + run; 1 the slot sort alone (descriptor batches: it reads only the
+// descriptors, so it may run before or beside the kernels that fill the payload); 2 the run
+// alone over a scratch a phase-1 call filled for the same batch (paths whose sort reads the
+// packets -- the one-workgroup small-batch paths -- sort in phase 2 instead)
 static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
                                const uint64_t* desc, uint8_t* actions, void* scratch,
-                               ina_stream_t stream, const PsFuse& ps, bool* fused_out) {
+                               ina_stream_t stream, const PsFuse& ps, bool* fused_out, int phase = 0) {
     *fused_out = false;
+    if (phase == 1 && !desc && npk)
+        return set_error(INA_EINVAL, "the separate slot sort needs the batch's descriptors%s", "");
+    const bool do_sort = phase != 2, do_run = phase != 1;
     if (!st || st->V <= 0 || st->V > kMaxV || st->num_slots == 0)
         return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
     if (stride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)st->V)
@@ -1564,6 +1575,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     uint32_t epoch = 0;
     if (small && fast && npk <= (size_t)g_tiny_max.load()) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
+        if (!do_run) return INA_OK;
         uint32_t win = (uint32_t)INA_SWITCH_WIN_SMALL;
         if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
         const bool narrow = (uint64_t)st->num_slots + 1 <= (1u << 20);
@@ -1578,6 +1590,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         *fused_out = ps.on != 0;
         return INA_OK;
     } else if (small) {
+        if (!do_run) return INA_OK;                         // this sort reads the packets
         if ((uint64_t)st->num_slots + 1 <= (1u << 20))
             hipLaunchKernelGGL((k_switch_sort_small<uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, pkts,
                                (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
@@ -1595,6 +1608,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const int ah = ack_hint ? 1 : 0;
         // never 0 (fresh scratch reads as "unsorted": the safe side); a stale epoch equal to
         // this one (2^32 calls later) also only costs the full sort
+        if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
 #define INA_A_LAUNCH(RR)                                                                              \
@@ -1605,6 +1619,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
         else INA_A_LAUNCH(kR0 / 4);
 #undef INA_A_LAUNCH
+        }
         // the bucket of foreign packets only (a pool of a multiple of 2^lb slots) is left out
         // when the register-resident run kernel takes the batch (it stops before them); the
         // generic run kernel reads every position, so then it is gathered like the others
@@ -1619,9 +1634,10 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const unsigned gb = std::min<unsigned>(nb, (st->num_slots >> lb) + 1u);
         const int tile = g_bucket_tile.load();
         const bool big = tile == kLcRoundsBig || (tile == 0 && npk > (size_t)gb * kBigTileAvg);
-        hipLaunchKernelGGL((big ? &k_sort_buckets<kLcRoundsBig> : &k_sort_buckets<kLcRounds>), dim3(gb),
-                           dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
-                           ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1);
+        if (do_sort)
+            hipLaunchKernelGGL((big ? &k_sort_buckets<kLcRoundsBig> : &k_sort_buckets<kLcRounds>), dim3(gb),
+                               dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
+                               ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1);
         if (fast) unsorted = ax.unsorted;
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
@@ -1637,6 +1653,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         auto* k_sc1 = ri == 0 ? &k_rs_scatter<true, kR0>
                     : ri == 1 ? &k_rs_scatter<true, kR1> : &k_rs_scatter<true, kR2>;
         const unsigned gd = (nb + kRsWaves - 1) / kRsWaves;
+        if (do_sort) {
         hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
                            reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
                            st->switch_id, k_in, actions, sp.bits, 0, ax.hist, sp.nch, ack_hint ? 1 : 0);
@@ -1658,7 +1675,14 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             std::swap(kc, kn);
             std::swap(vc, vn);
         }
+        } else {
+            for (int pass = 0; pass < sp.passes; ++pass) {    // where the passes left the keys
+                std::swap(kc, kn);
+                std::swap(vc, vn);
+            }
+        }
     }
+    if (!do_run) return INA_OK;
     if (fast) {
         // a wave runs the segments that start in its window of `win` sorted positions: a
         // segment is a chain of dependent round trips, so small windows (more waves) win
@@ -1671,7 +1695,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         auto* run = ps.on ? &k_switch_run2<true> : &k_switch_run2<false>;
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc, vc, actions,
-                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted, epoch);
+                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted);
         *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
@@ -1703,11 +1727,50 @@ int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t
                                          weight_step, out, n, acks, ack_stride, keep_forwarded, stream);
 }
 
+static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                             const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                             uint32_t seq0, const float* local, int k, double weight_step,
+                             float* out, size_t n, uint8_t* acks, size_t ack_stride,
+                             int keep_forwarded, ina_stream_t stream, int phase);
+
 int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
                                   const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
                                   uint32_t seq0, const float* local, int k, double weight_step,
                                   float* out, size_t n, uint8_t* acks, size_t ack_stride,
                                   int keep_forwarded, ina_stream_t stream) {
+    return switch_apply_impl(st, pkts, npk, stride, desc, actions, scratch, seq0, local, k, weight_step,
+                             out, n, acks, ack_stride, keep_forwarded, stream, 0);
+}
+
+int ina_switch_sort_desc(const ina_switch_state_t* st, const uint8_t* pkts, size_t npk, size_t stride,
+                         const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                         ina_stream_t stream) {
+    PsFuse off{};
+    bool fused = false;
+    return switch_process_impl(st, const_cast<uint8_t*>(pkts), npk, stride, desc, actions, scratch, stream,
+                               off, &fused, 1);
+}
+
+int ina_switch_run_sorted(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                          uint8_t* actions, void* scratch, ina_stream_t stream) {
+    PsFuse off{};
+    bool fused = false;
+    return switch_process_impl(st, pkts, npk, stride, nullptr, actions, scratch, stream, off, &fused, 2);
+}
+
+int ina_switch_run_sorted_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                                uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
+                                double weight_step, float* out, size_t n, uint8_t* acks,
+                                size_t ack_stride, int keep_forwarded, ina_stream_t stream) {
+    return switch_apply_impl(st, pkts, npk, stride, nullptr, actions, scratch, seq0, local, k, weight_step,
+                             out, n, acks, ack_stride, keep_forwarded, stream, 2);
+}
+
+static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                             const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                             uint32_t seq0, const float* local, int k, double weight_step,
+                             float* out, size_t n, uint8_t* acks, size_t ack_stride,
+                             int keep_forwarded, ina_stream_t stream, int phase) {
     if (k < -126 || k > 127) return set_error(INA_EINVAL, "k out of range [-126,127]%s", "");
     if (npk == 0) return INA_OK;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
@@ -1727,7 +1790,8 @@ int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, s
               nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,
               keep_forwarded ? 1 : 0};
     bool fused = false;
-    if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused)) return rc;
+    if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused, phase))
+        return rc;
     if (fused) return INA_OK;
     // layouts the register-resident run kernel does not take: the two steps one by one
     return ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,

@@ -73,6 +73,11 @@ SIGNATURES = {
     "ina_quantize_pack_nga_desc": [_vp, _vp, _sz, _i, C.POINTER(NgaParams), _vp, _sz, _vp, _vp],
     "ina_nga_descriptors": [_vp, _sz, _sz, _vp, _vp],
     "ina_quantize_pack_nga_multi": [_vp, _i, _vp, _sz, _i, _vp, _vp, _sz, _vp, _vp],
+    "ina_nga_make_descriptors": [_vp, _i, _sz, _vp, _vp],
+    "ina_switch_sort_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _vp],
+    "ina_switch_run_sorted": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
+    "ina_switch_run_sorted_apply": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i, _d,
+                                    _vp, _sz, _vp, _sz, _i, _vp],
     "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
     "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],

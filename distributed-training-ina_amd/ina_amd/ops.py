@@ -392,6 +392,30 @@ def quantize_pack_nga_multi(xs, k: int, V: int, bitmaps, count: int, switch_id: 
     return (outs, ds) if ds is not None else outs
 
 
+def make_descriptors(n_packets: int, bitmaps_or_W, count: int, switch_id: int, seq0,
+                     flags: int = 0, num_slots: int = NUM_REGISTER, outs=None,
+                     device: str | torch.device = "cuda", stream: torch.cuda.Stream | None = None):
+    """Packet descriptors from the header fields alone (ina_nga_make_descriptors): W
+    workers x n_packets int64 entries, what pack_nga(desc=True) writes beside each packet
+    (no overflow bits) -- a switch's sort() can take them before the payload exists.
+    seq0: one int for every worker or one per worker.  Returns the W tensors."""
+    W = bitmaps_or_W if isinstance(bitmaps_or_W, int) else len(list(bitmaps_or_W))
+    seqs = [int(seq0)] * W if isinstance(seq0, int) else list(seq0)
+    if len(seqs) != W or not 1 <= W <= _lib.MAX_WORKERS:
+        raise ValueError("one seq0 per worker, 1..64 workers")
+    if outs is None:
+        outs = [torch.empty(n_packets, dtype=torch.int64, device=device) for _ in range(W)]
+    outs = [_desc_arg(o, n_packets, outs[0].device) for o in outs]
+    if len(outs) != W:
+        raise ValueError("one output per worker")
+    prm = (_lib.NgaParams * W)(*[_lib.NgaParams(0, count & 0xFF, flags & 0xFF, switch_id & 0xFF, 0,
+                                                seqs[w] & 0xFFFFFFFF, num_slots, 1) for w in range(W)])
+    st = stream.cuda_stream if stream is not None else _stream(outs[0])
+    check(load().ina_nga_make_descriptors(prm, W, n_packets, ptr_array([o.data_ptr() for o in outs]), st),
+          "nga_make_descriptors")
+    return outs
+
+
 def unpack_nga(pkts: torch.Tensor, V: int, stride: int | None = None, with_values: bool = True):
     """Returns (fields dict of device tensors, int32 values [npkts*V] or None)."""
     _req(pkts, torch.uint8, "pkts")
@@ -574,6 +598,67 @@ class Switch:
                                              actions.data_ptr(), self._scratch.data_ptr(),
                                              _stream(pkts)), "switch_process")
         return actions
+
+    def _scratch_for(self, npk, dev):
+        need = load().ina_switch_scratch_bytes(npk, self.num_slots)
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=dev)
+        return self._scratch
+
+    def sort(self, pkts: torch.Tensor, desc: torch.Tensor, actions: torch.Tensor | None = None,
+             stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+        """The slot sort of process(pkts, desc=desc) alone (ina_switch_sort_desc): it reads
+        only the descriptors, so it may be queued before -- or on `stream`, beside -- the
+        kernels still filling pkts' payload; run() / run_apply() finish the batch over the
+        same scratch (order them after it; the scratch is this switch's, one batch at a time).
+        Returns the actions tensor to hand to run()."""
+        _req(pkts, torch.uint8, "pkts")
+        npk, stride = pkts.shape
+        d = _desc_arg(desc, npk, pkts.device)
+        if d is None:
+            raise ValueError("sort() needs the batch's descriptors")
+        actions = torch.empty(npk, dtype=torch.uint8, device=pkts.device) if actions is None else actions
+        _req(actions, torch.uint8, "actions")
+        _fits(actions, npk, "actions")
+        _same_device(pkts, actions)
+        scratch = self._scratch_for(npk, pkts.device)
+        st = stream.cuda_stream if stream is not None else _stream(pkts)
+        check(load().ina_switch_sort_desc(C.byref(self._state), pkts.data_ptr(), npk, stride, d.data_ptr(),
+                                          actions.data_ptr(), scratch.data_ptr(), st), "switch_sort")
+        return actions
+
+    def run(self, pkts: torch.Tensor, actions: torch.Tensor) -> torch.Tensor:
+        """Second phase of process(): the batch sort() sorted, run over its scratch."""
+        _req(pkts, torch.uint8, "pkts")
+        _req(actions, torch.uint8, "actions")
+        npk, stride = pkts.shape
+        _fits(actions, npk, "actions")
+        _same_device(pkts, actions)
+        scratch = self._scratch_for(npk, pkts.device)
+        check(load().ina_switch_run_sorted(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                           actions.data_ptr(), scratch.data_ptr(), _stream(pkts)),
+              "switch_run_sorted")
+        return actions
+
+    def run_apply(self, pkts: torch.Tensor, actions: torch.Tensor, seq0: int, local: torch.Tensor,
+                  k: int, weight_step: float, out: torch.Tensor | None = None,
+                  acks: torch.Tensor | None = None, keep_forwarded: bool = True):
+        """Second phase of process_apply() after sort().  Returns (actions, out)."""
+        _req(pkts, torch.uint8, "pkts")
+        _req(local, torch.float32, "local")
+        npk, stride = pkts.shape
+        _req(actions, torch.uint8, "actions")
+        out = torch.empty_like(local) if out is None else out
+        _fits(out, local.numel())
+        _check_apply(pkts, actions, self.V, local, out, acks)
+        ack_ptr, ack_stride = (acks.data_ptr(), acks.shape[1]) if acks is not None else (None, 0)
+        scratch = self._scratch_for(npk, pkts.device)
+        check(load().ina_switch_run_sorted_apply(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                                 actions.data_ptr(), scratch.data_ptr(), seq0 & 0xFFFFFFFF,
+                                                 local.data_ptr(), k, weight_step, out.data_ptr(),
+                                                 local.numel(), ack_ptr, ack_stride, int(keep_forwarded),
+                                                 _stream(pkts)), "switch_run_sorted_apply")
+        return actions, out
 
     def process_apply(self, pkts: torch.Tensor, seq0: int, local: torch.Tensor, k: int,
                       weight_step: float, out: torch.Tensor | None = None,

@@ -211,6 +211,12 @@ int ina_quantize_pack_nga_desc(const float* x, const float* base, size_t n, int 
                                ina_nga_desc_t* desc, ina_stream_t stream);
 int ina_nga_descriptors(const uint8_t* pkts, size_t npkts, size_t stride, ina_nga_desc_t* desc,
                         ina_stream_t stream);
+/* Descriptors from the header parameters alone (nothing read): W workers x npkts packets,
+ * desc[w][p] = what the pack entry points write for packet p of worker w (prm[w]'s count,
+ * flags, switch_id, sequence; the overflow bit is not known without the values).  desc is a
+ * host array of W device pointers; every prm[w] has the same num_slots. */
+int ina_nga_make_descriptors(const ina_nga_params_t* prm, int W, size_t npkts,
+                             ina_nga_desc_t* const* desc, ina_stream_t stream);
 /* W workers' fused quantise + pack in one launch (a GPU hosting a group of the job's
  * workers): worker w's x[w] - base (base shared, may be NULL) into pkts[w] with header
  * prm[w] and descriptors desc[w] (desc itself may be NULL) -- exactly the bytes of W calls
@@ -284,6 +290,23 @@ int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, s
                                   void* scratch, uint32_t seq0, const float* local, int k,
                                   double weight_step, float* out, size_t n, uint8_t* acks,
                                   size_t ack_stride, int keep_forwarded, ina_stream_t stream);
+/* The same calls in two phases.  With descriptors the slot sort reads nothing but them, so
+ * it can be queued as soon as they exist -- before, or on another stream beside, the
+ * kernels that still fill the packets' payload (descriptors from the header parameters
+ * alone: ina_nga_make_descriptors).  ina_switch_sort_desc queues the sort into `scratch`
+ * (pkts is not read, but must be the batch's final address); ina_switch_run_sorted[_apply]
+ * then runs the batch over that scratch -- the caller orders the two (same stream or an
+ * event) and changes no ina_set_tuning switch key between them.  Same actions, registers,
+ * packets and update as ina_switch_process[_apply]_desc.  (Batches the small-batch paths
+ * take, which sort from the headers, are sorted inside the run call.) */
+int ina_switch_sort_desc(const ina_switch_state_t* st, const uint8_t* pkts, size_t npkts, size_t stride,
+                         const ina_nga_desc_t* desc, uint8_t* actions, void* scratch, ina_stream_t stream);
+int ina_switch_run_sorted(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
+                          uint8_t* actions, void* scratch, ina_stream_t stream);
+int ina_switch_run_sorted_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
+                                uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
+                                double weight_step, float* out, size_t n, uint8_t* acks,
+                                size_t ack_stride, int keep_forwarded, ina_stream_t stream);
 
 /* ---- ipRoute (ngaa.p4:39-61, entries as bfrt/setup.py:85-95 installs them) -------
  * Every packet the ingress does not drop (actions FWD_AGG, FWD_COLLISION, FWD_ACK,

@@ -144,6 +144,11 @@ def _einval_cases():
         "ina_pack_nga_desc": (None, 64, ctypes.byref(prm), None, None, 144, None, None),
         "ina_quantize_pack_nga_desc": (None, None, 64, 16, ctypes.byref(prm), None, 144, None, None),
         "ina_nga_descriptors": (None, 2, 144, None, None),
+        "ina_nga_make_descriptors": ((_lib.NgaParams * 2)(prm, prm), 2, 64, P([None, None]), None),
+        "ina_switch_sort_desc": (ctypes.byref(st), None, 2, 144, None, None, None, None),
+        "ina_switch_run_sorted": (ctypes.byref(st), None, 2, 144, None, None, None),
+        "ina_switch_run_sorted_apply": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
+                                        None, 64, None, 144, 1, None),
         "ina_quantize_pack_nga_multi": (P([None, None]), 2, None, 64, 16,
                                         (_lib.NgaParams * 2)(prm, prm), P([None, None]), 144, None, None),
         "ina_switch_process_apply": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,

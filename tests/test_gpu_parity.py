@@ -1115,6 +1115,100 @@ def test_switch_process_apply_equals_two_steps(V, W, per, tail, keep):
     assert np.array_equal(c0, c1) and np.array_equal(f0, f1) and np.array_equal(r0, r1)
 
 
+@pytest.mark.parametrize("sort_mode", [0, 3])
+@pytest.mark.parametrize("V,W,per,order", [(256, 8, 700, "worker"), (256, 8, 700, "round_robin"),
+                                           (32, 4, 3000, "shuffled"), (256, 3, 30, "worker"),
+                                           (32, 4, 150, "worker"), (64, 16, 200, "shuffled")])
+def test_switch_two_phase_equals_one_call(V, W, per, order, sort_mode):
+    """ina_switch_sort_desc queued on a side stream from descriptors made from the header
+    fields alone (ina_nga_make_descriptors + the ack rows' descriptors), BEFORE the packets'
+    payload is packed on the main stream, then ina_switch_run_sorted_apply after both ==
+    ina_switch_process_apply_desc on the packed batch: same actions, PS update (bit for bit),
+    ack rows and switch state over two steady-state steps.  Covers the bucket sort, the
+    digit passes (sort_mode 3), presorted batches and the one-workgroup small-batch paths
+    (<= 768 and <= 128 packets, which sort inside the run call)."""
+    rng = np.random.default_rng(V * W + per)
+    o = ops()
+    n = V * per - 5
+    npk = -(-n // V)
+    stride = o.nga_stride(V)
+    slots = 1 << 13
+    xs = [dev((rng.standard_normal(n) * 1e-2).astype(np.float32)) for _ in range(W)]
+    glob0 = rng.standard_normal(n).astype(np.float32) * 1e-2
+    perm = None
+    if order == "round_robin":
+        perm = torch.arange(W * npk, device=DEV).view(W, npk).t().reshape(-1)
+    elif order == "shuffled":
+        perm = torch.randperm(W * npk, device=DEV)
+    res = {}
+    side = torch.cuda.Stream(DEV)
+    try:
+        o.set_tuning(switch_sort=sort_mode)
+        for two in (False, True):
+            glob = dev(glob0.copy())
+            upd = torch.empty_like(glob)
+            big = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=DEV)
+            acks, rows = big[:npk], big[npk:]
+            desc = torch.zeros((W + 1) * npk, dtype=torch.int64, device=DEV)
+            acts = torch.empty((W + 1) * npk, dtype=torch.uint8, device=DEV)
+            wrows = torch.empty((W, npk, stride), dtype=torch.uint8, device=DEV)
+            wdesc = torch.empty((W, npk), dtype=torch.int64, device=DEV)
+            sw = o.Switch(V, num_slots=slots, switch_id=1, device=DEV)
+            steps = []
+            for step in range(2):
+                if two:
+                    side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(side):
+                        o.make_descriptors(npk, W, W, 1, 1, num_slots=slots, outs=list(wdesc.unbind(0)),
+                                           device=DEV)
+                        o.nga_descriptors(acks, out=desc[:npk])
+                        desc[npk:] = wdesc.reshape(-1) if perm is None else wdesc.reshape(-1)[perm]
+                        sw.sort(big, desc, actions=acts)
+                    o.quantize_pack_nga_multi(xs, 16, V, list(range(1, W + 1)), W, 1, 1, base=glob,
+                                              num_slots=slots, outs=list(wrows.unbind(0)))
+                    rows.view(W * npk, stride)[:] = wrows.view(W * npk, stride) if perm is None \
+                        else wrows.view(W * npk, stride)[perm]
+                    torch.cuda.current_stream().wait_stream(side)
+                    sw.run_apply(big, acts, 1, glob, 16, 1.0 / (W + 1), out=upd, acks=acks,
+                                 keep_forwarded=False)
+                else:
+                    o.quantize_pack_nga_multi(xs, 16, V, list(range(1, W + 1)), W, 1, 1, base=glob,
+                                              num_slots=slots, outs=list(wrows.unbind(0)),
+                                              descs=list(wdesc.unbind(0)))
+                    rows.view(W * npk, stride)[:] = wrows.view(W * npk, stride) if perm is None \
+                        else wrows.view(W * npk, stride)[perm]
+                    o.nga_descriptors(acks, out=desc[:npk])
+                    desc[npk:] = wdesc.reshape(-1) if perm is None else wdesc.reshape(-1)[perm]
+                    sw.process_apply(big, 1, glob, 16, 1.0 / (W + 1), out=upd, acks=acks,
+                                     keep_forwarded=False, actions=acts, desc=desc)
+                steps.append((host(acts).copy(), host(upd).view(np.uint32).copy(), host(acks).copy()))
+                glob.copy_(upd)
+            res[two] = (steps, host(sw.count), host(sw.frag), host(sw.regs))
+    finally:
+        o.set_tuning(switch_sort=0)
+    (s0, c0, f0, r0), (s1, c1, f1, r1) = res[False], res[True]
+    for (a0, u0, k0), (a1, u1, k1) in zip(s0, s1):
+        assert np.array_equal(a0, a1)
+        assert np.array_equal(u0, u1)
+        assert np.array_equal(k0, k1)
+    assert int((s1[1][0] == orc.ACT_FWD_AGG).sum()) == npk        # every slot completed
+    assert np.array_equal(c0, c1) and np.array_equal(f0, f1) and np.array_equal(r0, r1)
+
+
+def test_make_descriptors_equal_pack_descriptors():
+    """Descriptors from the header fields alone == the ones the pack kernel writes."""
+    o = ops()
+    rng = np.random.default_rng(3)
+    V, W, n = 256, 11, 256 * 40 + 9
+    xs = [dev(mixed_floats(rng, n)) for _ in range(W)]
+    seqs = [int(s) for s in rng.integers(0, 2**32 - 64, W)]
+    _, d_pack = o.quantize_pack_nga_multi(xs, 16, V, list(range(W)), 5, 2, seqs, num_slots=777,
+                                          flags=0x10, descs=True)
+    d_made = o.make_descriptors(-(-n // V), W, 5, 2, seqs, flags=0x10, num_slots=777, device=DEV)
+    for a, b in zip(d_pack, d_made):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("V,W,per", [(32, 4, 300), (256, 8, 70)])
 def test_process_apply_packets_outside_the_bucket_are_forwarded(V, W, per):
     """keep_forwarded=False consumes only the completed packets the PS takes (frag_id -

@@ -26,7 +26,7 @@ for st in $STAGES; do
       rc=$?; cat "$OUT/$nm.log"; [ $rc -ne 0 ] && fatal "$st" $rc ;;
     ptest:*)
       timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread \
-        -k "${st#ptest:}" > "$OUT/ptest.log" 2>&1
+        -k "${PTEST_K:-${st#ptest:}}" > "$OUT/ptest.log" 2>&1
       rc=$?; tail -8 "$OUT/ptest.log"; ok_or_fail "$st" $rc ;;
     ew16lab)
       timeout -k 10 300 python tools/lab/ew16_lab.py > "$OUT/ew16_lab.log" 2>&1

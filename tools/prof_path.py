@@ -1,5 +1,5 @@
 """Profile target: the one-GPU INA packet path in steady state with the PS step fused into
-the switch pass (8 x fused worker quantise+pack, one ina_switch_process_apply over
+the switch pass (the 8 workers' fused quantise+packs in one launch, one ina_switch_process_apply over
 [last step's acks | 8 x 102,400 NGA-256 packets]); run under rocprofv3 --kernel-trace
 --stats for the per-kernel breakdown of bench_extra's last packet-path row."""
 import os
@@ -26,9 +26,8 @@ desc_ack, desc_w = desc[:npk], desc[npk:].view(W, npk)
 out = torch.empty_like(params)
 sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
 for step in range(int(os.environ.get("STEPS", 6))):
-    for w in range(W):
-        ops.quantize_pack_nga(xs[w], 16, V, w + 1, W, 1, 1, base=params, num_slots=slots, out=rows[w],
-                              desc=desc_w[w])
+    ops.quantize_pack_nga_multi(xs, 16, V, [w + 1 for w in range(W)], W, 1, 1, base=params,
+                                num_slots=slots, outs=list(rows.unbind(0)), descs=list(desc_w.unbind(0)))
     ops.nga_descriptors(acks, out=desc_ack)
     sw.process_apply(batch, 1, params, 16, 1.0 / (W + 1), out=out, acks=acks, keep_forwarded=False,
                      actions=acts, desc=desc)
