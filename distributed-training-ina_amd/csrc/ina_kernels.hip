@@ -1020,20 +1020,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_nga_flat(Src src, size_t n, Nga
 // the workers' loads are all in flight together; each worker's output stream stays
 // coalesced.  Bytes = the per-worker kernel's, worker by worker.
 constexpr int kQpGroup = 8;
-// store policy of the one-launch worker pack (lab knob): 0 nt like the other packet
-// kernels, 1 write-through (stream_store), 2 the default policy
-#ifndef INA_QPM_STORE
-#define INA_QPM_STORE 0
-#endif
-__device__ __forceinline__ void qpm_store(u32x4 v, u32x4* p) {
-#if INA_QPM_STORE == 1
-    stream_store(v, p);
-#elif INA_QPM_STORE == 2
-    *p = v;
-#else
-    packet_store(v, p);
-#endif
-}
+// stores: nt like the other packet kernels (write-through and default-policy stores were
+// slower in both layouts, profiles/r03/lab/qpack_multi_lab.log)
+__device__ __forceinline__ void qpm_store(u32x4 v, u32x4* p) { packet_store(v, p); }
 struct QPackGroup {
     const float* x[kQpGroup];
     uint8_t* pkts[kQpGroup];
@@ -1155,15 +1144,10 @@ __global__ __launch_bounds__(kBlock) void k_nga_make_desc(DescGroup a, int G, ui
 #ifndef INA_QPM_PPW_BLOCKS
 #define INA_QPM_PPW_BLOCKS (1 << 20)      // a covering grid (a wave per packet)
 #endif
-#ifndef INA_QPM_WPE
-#define INA_QPM_WPE 0       // lab knob: amdgpu_waves_per_eu minimum (0: the compiler's choice)
-#endif
+// (amdgpu_waves_per_eu 6 / 7 -- 74 / 71 VGPRs against 87 -- gained nothing,
+// profiles/r03/lab/qpack_occupancy_lab.log)
 template <int G>
-__global__ __launch_bounds__(kBlock)
-#if INA_QPM_WPE
-__attribute__((amdgpu_waves_per_eu(INA_QPM_WPE, 8)))
-#endif
-void k_qpack_nga_multi_v256(QPackGroup a, const float* __restrict__ base,
+__global__ __launch_bounds__(kBlock) void k_qpack_nga_multi_v256(QPackGroup a, const float* __restrict__ base,
                                                                  size_t n, float s, uint32_t num_slots,
                                                                  uint32_t stride, uint32_t np) {
     const uint32_t gs = gridDim.x * kBlock;
