@@ -2143,6 +2143,8 @@ int ina_quantize_pack_nga_multi(const float* const* x, int W, const float* base,
     if (V <= 0 || prm[0].num_slots == 0) return set_error(INA_EINVAL, "bad nga params%s", "");
     if (pstride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)V)
         return set_error(INA_EINVAL, "stride < 15 + 4V%s", "");
+    const size_t npk = (n + (size_t)V - 1) / (size_t)V;
+    if (npk == 0) return INA_OK;                       // empty buckets: nothing to write
     bool flat = pstride % 16 == 0 && V % 4 == 0 && (!base || aligned16(base));
     for (int w = 0; w < W; ++w) {
         if (prm[w].V != V || prm[w].num_slots != prm[0].num_slots)
@@ -2152,8 +2154,6 @@ int ina_quantize_pack_nga_multi(const float* const* x, int W, const float* base,
             return set_error(INA_EINVAL, "descriptors must be non-null and 8-byte aligned%s", "");
         flat &= aligned16(x[w]) && aligned16(pkts[w]);
     }
-    const size_t npk = (n + (size_t)V - 1) / (size_t)V;
-    if (npk == 0) return INA_OK;
     hipStream_t s = hs(stream);
     if (!flat) {     // generic layouts: the per-worker byte path, worker by worker
         for (int w = 0; w < W; ++w)

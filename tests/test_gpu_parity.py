@@ -1328,6 +1328,21 @@ def test_quantize_pack_multi_matches_oracle(V, W, with_base, padded):
         assert np.array_equal(dw, want.reshape(-1, stride)[:, 4:12]), w
 
 
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257])
+def test_quantize_pack_multi_tiny_buckets(n):
+    """Empty and sub-packet buckets at the 64-worker maximum: zero packets, or one ragged
+    packet per worker, byte-equal to the oracle."""
+    o = ops()
+    rng = np.random.default_rng(n + 1)
+    V, W = 256, 64
+    xs = [mixed_floats(rng, n) for _ in range(W)]
+    outs = o.quantize_pack_nga_multi([dev(x) for x in xs], 16, V, list(range(W)), W, 3, 77)
+    for w, x in enumerate(xs):
+        got = host(outs[w])
+        want = orc.pack_nga(orc.quantize_i32(x, 16), V, w, W, 3, 77, stride=o.nga_stride(V))
+        assert got.size == want.size and np.array_equal(got.reshape(-1), want.reshape(-1)), w
+
+
 def test_quantize_pack_multi_split_launches():
     """Packet ranges (a small launch_chunks forces them) carry every worker's sequence."""
     o = ops()
