@@ -392,14 +392,14 @@ def quantize_pack_nga_multi(xs, k: int, V: int, bitmaps, count: int, switch_id: 
     return (outs, ds) if ds is not None else outs
 
 
-def make_descriptors(n_packets: int, bitmaps_or_W, count: int, switch_id: int, seq0,
+def make_descriptors(n_packets: int, W: int, count: int, switch_id: int, seq0,
                      flags: int = 0, num_slots: int = NUM_REGISTER, outs=None,
                      device: str | torch.device = "cuda", stream: torch.cuda.Stream | None = None):
     """Packet descriptors from the header fields alone (ina_nga_make_descriptors): W
     workers x n_packets int64 entries, what pack_nga(desc=True) writes beside each packet
     (no overflow bits) -- a switch's sort() can take them before the payload exists.
     seq0: one int for every worker or one per worker.  Returns the W tensors."""
-    W = bitmaps_or_W if isinstance(bitmaps_or_W, int) else len(list(bitmaps_or_W))
+    W = int(W)
     seqs = [int(seq0)] * W if isinstance(seq0, int) else list(seq0)
     if len(seqs) != W or not 1 <= W <= _lib.MAX_WORKERS:
         raise ValueError("one seq0 per worker, 1..64 workers")
@@ -575,6 +575,7 @@ class Switch:
                                        self.count.data_ptr(), self.frag.data_ptr(),
                                        self.regs.data_ptr())
         self._scratch = None
+        self._sorted = None        # (batch, scratch) of a sort() awaiting its run()
 
     def process(self, pkts: torch.Tensor, actions: torch.Tensor | None = None,
                 desc: torch.Tensor | None = None) -> torch.Tensor:
@@ -593,6 +594,7 @@ class Switch:
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
+        self._sorted = None                       # the scratch is reused below
         check(load().ina_switch_process_desc(C.byref(self._state), pkts.data_ptr(), npk, stride,
                                              d.data_ptr() if d is not None else None,
                                              actions.data_ptr(), self._scratch.data_ptr(),
@@ -623,9 +625,23 @@ class Switch:
         _same_device(pkts, actions)
         scratch = self._scratch_for(npk, pkts.device)
         st = stream.cuda_stream if stream is not None else _stream(pkts)
+        if stream is not None:
+            scratch.record_stream(stream)        # in use there until run() joins it
         check(load().ina_switch_sort_desc(C.byref(self._state), pkts.data_ptr(), npk, stride, d.data_ptr(),
                                           actions.data_ptr(), scratch.data_ptr(), st), "switch_sort")
+        self._sorted = (pkts.data_ptr(), npk, stride, actions.data_ptr(), scratch.data_ptr())
         return actions
+
+    def _take_sorted(self, pkts, actions):
+        # the run reads the sort's scratch as it stands: a run without its own sort (or for
+        # another batch) would read stale packet ids, so the pairing is enforced here
+        npk, stride = pkts.shape
+        want = (pkts.data_ptr(), npk, stride, actions.data_ptr(),
+                self._scratch.data_ptr() if self._scratch is not None else None)
+        if self._sorted != want:
+            raise ValueError("run() / run_apply() must follow sort() of the same batch and actions")
+        self._sorted = None
+        return self._scratch
 
     def run(self, pkts: torch.Tensor, actions: torch.Tensor) -> torch.Tensor:
         """Second phase of process(): the batch sort() sorted, run over its scratch."""
@@ -634,7 +650,7 @@ class Switch:
         npk, stride = pkts.shape
         _fits(actions, npk, "actions")
         _same_device(pkts, actions)
-        scratch = self._scratch_for(npk, pkts.device)
+        scratch = self._take_sorted(pkts, actions)
         check(load().ina_switch_run_sorted(C.byref(self._state), pkts.data_ptr(), npk, stride,
                                            actions.data_ptr(), scratch.data_ptr(), _stream(pkts)),
               "switch_run_sorted")
@@ -652,7 +668,7 @@ class Switch:
         _fits(out, local.numel())
         _check_apply(pkts, actions, self.V, local, out, acks)
         ack_ptr, ack_stride = (acks.data_ptr(), acks.shape[1]) if acks is not None else (None, 0)
-        scratch = self._scratch_for(npk, pkts.device)
+        scratch = self._take_sorted(pkts, actions)
         check(load().ina_switch_run_sorted_apply(C.byref(self._state), pkts.data_ptr(), npk, stride,
                                                  actions.data_ptr(), scratch.data_ptr(), seq0 & 0xFFFFFFFF,
                                                  local.data_ptr(), k, weight_step, out.data_ptr(),
@@ -683,6 +699,7 @@ class Switch:
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
+        self._sorted = None
         check(load().ina_switch_process_apply_desc(C.byref(self._state), pkts.data_ptr(), npk, stride,
                                               d.data_ptr() if d is not None else None,
                                               actions.data_ptr(), self._scratch.data_ptr(),

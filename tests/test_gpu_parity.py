@@ -1195,6 +1195,30 @@ def test_switch_two_phase_equals_one_call(V, W, per, order, sort_mode):
     assert np.array_equal(c0, c1) and np.array_equal(f0, f1) and np.array_equal(r0, r1)
 
 
+def test_switch_run_requires_its_sort():
+    """run() reads the scratch its sort() left: without that sort, for another batch, or
+    after a one-call process() reused the scratch, it refuses before any launch."""
+    o = ops()
+    V, W, n = 32, 4, 32 * 3000
+    pk = [o.pack_nga(dev(rand_i32(np.random.default_rng(w), n, full=False)), V, w + 1, W, 1, 1,
+                     num_slots=4096, desc=True) for w in range(W)]
+    batch = torch.cat([p for p, _ in pk])
+    desc = torch.cat([d for _, d in pk])
+    sw = o.Switch(V, num_slots=4096, switch_id=1, device=DEV)
+    acts = torch.empty(batch.shape[0], dtype=torch.uint8, device=DEV)
+    with pytest.raises(ValueError):
+        sw.run(batch, acts)
+    sw.sort(batch, desc, actions=acts)
+    with pytest.raises(ValueError):
+        sw.run(batch[:-1], acts)
+    sw.process(batch[:10].clone())
+    with pytest.raises(ValueError):
+        sw.run(batch, acts)
+    sw.sort(batch, desc, actions=acts)
+    sw.run(batch, acts)
+    assert int((acts == orc.ACT_FWD_AGG).sum()) == n // V
+
+
 def test_make_descriptors_equal_pack_descriptors():
     """Descriptors from the header fields alone == the ones the pack kernel writes."""
     o = ops()
