@@ -296,7 +296,9 @@ int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, s
  * alone: ina_nga_make_descriptors).  ina_switch_sort_desc queues the sort into `scratch`
  * (pkts is not read, but must be the batch's final address); ina_switch_run_sorted[_apply]
  * then runs the batch over that scratch -- the caller orders the two (same stream or an
- * event) and changes no ina_set_tuning switch key between them.  Same actions, registers,
+ * event) and changes no ina_set_tuning switch key between them.  A run over a scratch that
+ * no sort of this same batch (state, pkts, npkts, stride, actions) filled is undefined: it
+ * reads that sort's packet ids.  Same actions, registers,
  * packets and update as ina_switch_process[_apply]_desc.  (Batches the small-batch paths
  * take, which sort from the headers, are sorted inside the run call.) */
 int ina_switch_sort_desc(const ina_switch_state_t* st, const uint8_t* pkts, size_t npkts, size_t stride,
