@@ -109,6 +109,26 @@ int main() {
         prm.bitmap = 1u << w; prm.num_slots = slots;
         CK(ina_pack_nga(d_q[w], n, &prm, nullptr, d_stream + (size_t)w * npk * stride, stride, s));
     }
+    // the same packets from the fp32 gradients, every worker quantised and packed in ONE
+    // launch (ina_quantize_pack_nga_multi): byte-identical to quantise, then pack
+    {
+        uint8_t* d_stream2;
+        HK(hipMalloc(&d_stream2, (size_t)W * npk * stride));
+        std::vector<ina_nga_params_t> prms(W, prm);
+        std::vector<uint8_t*> outs(W);
+        for (int w = 0; w < W; ++w) {
+            prms[w].bitmap = 1u << w;
+            outs[w] = d_stream2 + (size_t)w * npk * stride;
+        }
+        CK(ina_quantize_pack_nga_multi((const float* const*)d_g, W, nullptr, n, k, prms.data(), outs.data(),
+                                       stride, nullptr, s));
+        HK(hipStreamSynchronize(s));
+        std::vector<uint8_t> a((size_t)W * npk * stride), b(a.size());
+        HK(hipMemcpy(a.data(), d_stream, a.size(), hipMemcpyDeviceToHost));
+        HK(hipMemcpy(b.data(), d_stream2, b.size(), hipMemcpyDeviceToHost));
+        if (a != b) ++bad;
+        HK(hipFree(d_stream2));
+    }
     uint8_t *d_count, *d_act;
     uint32_t *d_frag, *d_regs;
     float *d_zero, *d_out;
@@ -139,6 +159,6 @@ int main() {
     // the error path: a bad argument returns a code, sets a message, never exits
     const int rc = ina_sum_reduce_i32((const int32_t* const*)d_q, 0, d_sum, n, s);
     if (rc != INA_EINVAL || std::strlen(ina_last_error_string()) == 0) ++bad;
-    std::printf("capi_check: %zu values x %d workers (bulk reduce, NGA-256 pack/unpack, switch + fused PS step), %zu mismatches\n", n, W, bad);
+    std::printf("capi_check: %zu values x %d workers (bulk reduce, NGA-256 pack/unpack, one-launch worker packs, switch + fused PS step), %zu mismatches\n", n, W, bad);
     return bad ? 1 : 0;
 }
