@@ -806,18 +806,37 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
     ws = 1.0 / (W + 1)
 
     outs_w, descs_w = list(rows_w.unbind(0)), list(desc_w.unbind(0))
+    bms = [w + 1 for w in range(W)]
 
-    def step(_r=0):
+    def pack():
         # the 8 workers' quantise + packs as ONE launch (p_global read once for all of them)
-        ops.quantize_pack_nga_multi(xs, k, V, [w + 1 for w in range(W)], W, 1, 1, base=glob,
-                                    num_slots=slots, outs=outs_w, descs=descs_w)
+        ops.quantize_pack_nga_multi(xs, k, V, bms, W, 1, 1, base=glob, num_slots=slots,
+                                    outs=outs_w, descs=descs_w)
+
+    def switch():
         ops.nga_descriptors(ack_rows, out=desc_ack)
         sw.process_apply(big, 1, glob, k, ws, out=upd, acks=ack_rows, keep_forwarded=False,
                          actions=acts, desc=desc)
+
+    def step(_r=0):
+        pack()
+        switch()
     step()                                     # the first step's ack rows are another switch's
     s = torch.cuda.current_stream(dev)
     barrier(world)
     avg = max_over_ranks(_time_rotating(step, 1, steps, warm, s), world)
+    # phase split (after the timed region): events between the packs and the switch pass of
+    # each step, medians over `steps` steps
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in ev:
+        e[0].record(s)
+        pack()
+        e[1].record(s)
+        switch()
+        e[2].record(s)
+    torch.cuda.synchronize()
+    t_pack = statistics.median(e[0].elapsed_time(e[1]) for e in ev) / 1e3
+    t_sw = statistics.median(e[1].elapsed_time(e[2]) for e in ev) / 1e3
     ok = bool(int((acts[npk:] == _ACT_FWD_AGG).sum()) == npk) and bool((acts[:npk] == _ACT_FWD_ACK).all())
     idx = _sample_idx(n)
     ti = torch.from_numpy(idx).to(dev)
@@ -830,11 +849,12 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
     ok = all_ranks_true(ok and bool(np.array_equal(upd[ti].cpu().numpy().view(np.uint32),
                                                    want.astype(np.float32).view(np.uint32))), world)
     rb, npk_all = stride, W * npk
-    path = (W * (4 * n + npk * rb) + 4 * n                # fused worker quantise + packs (one launch,
-                                                          # p_global read once for all 8 workers)
-            + npk * (16 + 8)                              # ack descriptors
+    b_pack = W * (4 * n + npk * rb) + 4 * n + W * npk * 8  # fused worker quantise + packs (one
+                                                          # launch, p_global read once) + descriptors
+    b_sw = (npk * (16 + 8)                                # ack descriptors
             + npk_all * rb + npk * (4 * V + 5) + npk_all  # switch: packets, registers, actions
             + npk * rb + 8 * n + 16 * npk)                # PS fused: acks in, local + update, ack rows
+    path = b_pack + b_sw
     res = {"workload": ("INA packet path, steady state, PS fused into the switch pass: 8 workers x "
                         f"{n} fp32 -> quantise(p_w - p_global) + NGA-256 pack -> one switch batch of "
                         f"{npk} PS acks + {npk_all} worker packets -> completed slots applied to "
@@ -846,6 +866,14 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
                         "unit": "GB/s", "frac": round(path / avg / 1e9 / HBM_PEAK_GBS, 4),
                         "path_bytes_per_step": int(path),
                         "measures": "the step's algorithmic bytes (all its kernels) / the step time"},
+           "phases": {"worker_packs": {"kernel": "ina::k_qpack_nga_multi_v256<8> (one launch)",
+                                       "us": round(t_pack * 1e6, 1), "bytes": int(b_pack),
+                                       "frac": round(b_pack / t_pack / 1e9 / HBM_PEAK_GBS, 4)},
+                      "switch_and_ps": {"kernels": "k_nga_desc (ack rows), k_sort_chunks, k_sort_buckets, "
+                                                   "k_switch_run2<true>",
+                                        "us": round(t_sw * 1e6, 1), "bytes": int(b_sw),
+                                        "frac": round(b_sw / t_sw / 1e9 / HBM_PEAK_GBS, 4)},
+                      "measures": "HIP events between the two phases of each step, medians"},
            "parity_spot_check": ok,
            "parity_sample": (f"every worker packet completes its slot, every ack frees one; the update at "
                              f"{idx.size} positions vs numpy quantise + wrapping sum + launch.py update")}
