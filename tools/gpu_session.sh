@@ -4,6 +4,7 @@
 # abort or timeout (only an ordinary pytest failure, rc 1, lets it continue).
 # usage: tools/gpu_session.sh TAG [stages...]   stages: smoke test bench prof pmc extra swprof
 #        contract config1 rehearse rehearse8 sharded swlab pathprof
+#        lab:<name> (tools/lab/<name>.py)   ptest:<expr> (GPU tests -k <expr>, or -k "$PTEST_K")
 set -u
 TAG=${1:-r02}; shift || true
 STAGES=${*:-"smoke test bench prof pmc extra"}
