@@ -64,6 +64,18 @@ def step_c():
     sw.run_apply(big, acts, 1, glob, k, ws, out=upd, acks=ack_rows, keep_forwarded=False)
 
 
+def step_d():
+    # only the ack rows' descriptor gather beside the packs (a small kernel that fits in the
+    # VGPRs the pack kernel leaves free), the sort + run after both
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        ops.nga_descriptors(ack_rows, out=desc_ack)
+    ops.quantize_pack_nga_multi(xs, k, V, bm, W, 1, 1, base=glob, num_slots=slots, outs=outs, descs=descs)
+    main.wait_stream(side)
+    sw.process_apply(big, 1, glob, k, ws, out=upd, acks=ack_rows, keep_forwarded=False,
+                     actions=acts, desc=desc)
+
+
 def timed(fn, reps=10, warm=3):
     for _ in range(warm):
         fn()
@@ -77,7 +89,7 @@ def timed(fn, reps=10, warm=3):
 
 
 ref = None
-for nm, fn in (("a", step_a), ("b", step_b), ("c", step_c)):
+for nm, fn in (("a", step_a), ("b", step_b), ("c", step_c), ("d", step_d)):
     fn()
     fn()
     torch.cuda.synchronize()
@@ -86,6 +98,6 @@ for nm, fn in (("a", step_a), ("b", step_b), ("c", step_c)):
         ref = got
     print(f"{nm}: update and actions equal to (a): {bool(torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]))}")
 for r in range(4):
-    ta, tb, tc = timed(step_a), timed(step_b), timed(step_c)
+    ta, tb, tc, td = timed(step_a), timed(step_b), timed(step_c), timed(step_d)
     print(f"round {r}: (a) one call {ta:7.1f} us   (b) sort first, one stream {tb:7.1f} us   "
-          f"(c) sort on a second stream {tc:7.1f} us")
+          f"(c) sort on a second stream {tc:7.1f} us   (d) ack descriptors beside the packs {td:7.1f} us")
