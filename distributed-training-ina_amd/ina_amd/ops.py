@@ -380,6 +380,8 @@ def quantize_pack_nga_multi(xs, k: int, V: int, bitmaps, count: int, switch_id: 
         _same_device(xs[0], o)
     ds = None
     if descs is not None and descs is not False:
+        if descs is not True and (len(descs) != W or any(d is None for d in descs)):
+            raise ValueError("descs: True, or one int64 tensor per worker")
         ds = [_desc_arg(True if descs is True else descs[w], npk, dev) for w in range(W)]
     prm = (_lib.NgaParams * W)(*[_lib.NgaParams(bitmaps[w] & 0xFFFFFFFF, count & 0xFF, flags & 0xFF,
                                                 switch_id & 0xFF, 0, seqs[w] & 0xFFFFFFFF, num_slots, V)
