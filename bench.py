@@ -199,14 +199,32 @@ def make_inputs(W, n, seed_base, dev):
     return bufs
 
 
-def load_traffic(path, W, n):
+HEADLINE_KERNEL = "ina::k_sum_reduce_i32_vec<8,4,true>"
+
+
+def _kernel_symbol(name: str) -> str:
+    """'void ina::k<8, 4, true>(args...)' -> 'ina::k<8,4,true>' (comparable form)."""
+    name = name.split("(")[0].strip()
+    if name.startswith("void "):
+        name = name[5:]
+    return "".join(name.split())
+
+
+def load_traffic(path, W, n, kernel=HEADLINE_KERNEL):
+    """Per-launch HBM bytes from the committed PMC file (tools/pmc_traffic.py: two rocprofv3
+    --pmc passes, FETCH_SIZE doubled per the gfx950 half-count, WRITE_SIZE) and where they
+    came from: (bytes, source).  The bytes are null unless the file measured THIS kernel
+    symbol at this size -- a file from another kernel build must not be quoted."""
     try:
         t = json.load(open(path))
-        if t.get("workers") == W and t.get("values") == n:
-            return t.get("hbm_bytes_per_launch")
-    except Exception:
-        pass
-    return None
+    except Exception as e:                # noqa: BLE001 -- no file: traffic unmeasured
+        return None, {"file": os.path.relpath(path, REPO), "error": type(e).__name__}
+    ok = (t.get("workers") == W and t.get("values") == n
+          and _kernel_symbol(t.get("kernel", "")) == _kernel_symbol(kernel))
+    src = {"file": os.path.relpath(path, REPO), "session": t.get("session"),
+           "kernel": t.get("kernel"), "matches_kernel_and_size": ok,
+           "measured": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/pmc_traffic.py)"}
+    return (t.get("hbm_bytes_per_launch") if ok else None), src
 
 
 # -- CPU baseline ----------------------------------------------------------------------------
@@ -814,14 +832,16 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
                                     outs=outs_w, descs=descs_w)
 
     def switch():
-        ops.nga_descriptors(ack_rows, out=desc_ack)
+        # the fused run kernel writes each ack row's descriptor beside it (ack_desc), so the
+        # next step's batch -- these acks in front of the packets -- needs no gather pass
         sw.process_apply(big, 1, glob, k, ws, out=upd, acks=ack_rows, keep_forwarded=False,
-                         actions=acts, desc=desc)
+                         actions=acts, desc=desc, ack_desc=desc_ack)
 
     def step(_r=0):
         pack()
         switch()
-    step()                                     # the first step's ack rows are another switch's
+    ops.nga_descriptors(ack_rows, out=desc_ack)    # the first step's ack rows are another switch's
+    step()
     s = torch.cuda.current_stream(dev)
     barrier(world)
     avg = max_over_ranks(_time_rotating(step, 1, steps, warm, s), world)
@@ -851,7 +871,7 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
     rb, npk_all = stride, W * npk
     b_pack = W * (4 * n + npk * rb) + 4 * n + W * npk * 8  # fused worker quantise + packs (one
                                                           # launch, p_global read once) + descriptors
-    b_sw = (npk * (16 + 8)                                # ack descriptors
+    b_sw = (npk * 8                                       # ack descriptors (run kernel)
             + npk_all * rb + npk * (4 * V + 5) + npk_all  # switch: packets, registers, actions
             + npk * rb + 8 * n + 16 * npk)                # PS fused: acks in, local + update, ack rows
     path = b_pack + b_sw
@@ -861,7 +881,8 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
                         "p_global (launch.py:46-50) + ack rows"),
            "value": round(W * n * 4 / avg / 1e9, 2), "unit": "GB/s (worker fp32 bytes aggregated)",
            "ms_per_step": round(avg * 1e3, 3), "steps": steps, "warmup": warm,
-           "launches_per_step": 1 + 1 + 3,
+           "launches_per_step": 1 + 3,
+           "switch_batch_path": sw.batch_path((W + 1) * npk),
            "roofline": {"bound": "hbm", "achieved": round(path / avg / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(path / avg / 1e9 / HBM_PEAK_GBS, 4),
                         "path_bytes_per_step": int(path),
@@ -869,8 +890,9 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
            "phases": {"worker_packs": {"kernel": "ina::k_qpack_nga_multi_v256<8> (one launch)",
                                        "us": round(t_pack * 1e6, 1), "bytes": int(b_pack),
                                        "frac": round(b_pack / t_pack / 1e9 / HBM_PEAK_GBS, 4)},
-                      "switch_and_ps": {"kernels": "k_nga_desc (ack rows), k_sort_chunks, k_sort_buckets, "
-                                                   "k_switch_run2<true>",
+                      "switch_and_ps": {"kernels": "k_sort_chunks, k_sort_buckets (finds 9 dense runs: "
+                                                   "no sort), k_switch_run2<true> (writes the ack "
+                                                   "rows and their descriptors)",
                                         "us": round(t_sw * 1e6, 1), "bytes": int(b_sw),
                                         "frac": round(b_sw / t_sw / 1e9 / HBM_PEAK_GBS, 4)},
                       "measures": "HIP events between the two phases of each step, medians"},
@@ -914,10 +936,19 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
     res = {"workload": "C3 as NGA-256 packets: 8 workers x 102,400 packets (819,200), 2^17-slot "
                        "pool, keys from descriptors; ina_switch_process incl. its slot sort",
            "algorithmic_bytes": algo, "ranks": world}
+    # worker_major: 8 dense runs of consecutive slots (no sort: the run table); round_robin:
+    # already in slot order (no sort); worker_major_sorted: the same worker-major batch with
+    # the run table off (tuning key 18 = 0: the chunk + bucket sort); shuffled: a random
+    # arrival order (the sort, unavoidably)
+    gperm = torch.Generator(device=dev)
+    gperm.manual_seed(77 + rank)
     order = {"worker_major": None,
-             "round_robin": torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1)}
+             "round_robin": torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1),
+             "worker_major_sorted": None,
+             "shuffled": torch.randperm(npk_all, device=dev, generator=gperm)}
     for name, perm in order.items():
         st, ds = (stream, desc) if perm is None else (stream[perm], desc[perm])
+        ops.set_tuning(switch_runs=name != "worker_major_sorted")
         for _ in range(warm):
             sw.process(st, acts, desc=ds)
         barrier(world)
@@ -946,7 +977,9 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
         done = int((acts == 1).sum())
         res[name] = {"us": round(us, 2), "achieved_GBps": round(algo / us / 1e3, 1),
                      "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
-                     "ok": all_ranks_true(done == npk, world), "us_event_pair_per_call": round(us_pair, 2)}
+                     "ok": all_ranks_true(done == npk, world), "us_event_pair_per_call": round(us_pair, 2),
+                     "batch_path": sw.batch_path(npk_all)}
+        ops.set_tuning(switch_runs=True)
         if world > 1:
             res[name]["aggregate_GBps"] = round(world * algo / us / 1e3, 1)
         del st, ds
@@ -1026,20 +1059,22 @@ def run_reduce(args, rank, world, dev, backend):
     avg_launch_s = max_over_ranks(my_avg_s, world)
     best_avg_s = reduce_over_ranks(my_avg_s, world, "min")
 
-    # spot check of the measured output (first slots) against a numpy wrapping sum
-    check_n = min(n, 1 << 16)
+    # spot check of the measured output against a numpy wrapping sum: every 997th value over
+    # the whole bucket plus its first and last 4 Ki values
     last = (args.steps - 1) % ROTATE
-    want = np.zeros(check_n, np.uint32)
+    idx = _sample_idx(n)
+    ti = torch.from_numpy(idx).to(dev)
+    want = np.zeros(idx.size, np.uint32)
     for b in sets[last]:
-        want += b[:check_n].cpu().numpy().view(np.uint32)
+        want += b[ti].cpu().numpy().view(np.uint32)
     parity = all_ranks_true(
-        bool(np.array_equal(outs[last][:check_n].cpu().numpy().view(np.uint32), want)), world)
+        bool(np.array_equal(outs[last][ti].cpu().numpy().view(np.uint32), want)), world)
 
     worker_bytes = W * n * 4
     algo_bytes = (W + 1) * n * 4
     value = worker_bytes * args.steps * world / elapsed / 1e9
     achieved = algo_bytes / avg_launch_s / 1e9
-    traffic = load_traffic(args.traffic_file, W, n)
+    traffic, traffic_source = load_traffic(args.traffic_file, W, n)
     slots = (n + V_SLOT - 1) // V_SLOT
     line = {
         "metric": METRIC,
@@ -1067,12 +1102,15 @@ def run_reduce(args, rank, world, dev, backend):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "ina::k_sum_reduce_i32_vec<8,4,true> (512 x 256 threads)",
+                     "traffic_source": traffic_source,
+                     "kernel": f"{HEADLINE_KERNEL} (512 x 256 threads)",
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "avg_launch_us": round(avg_launch_s * 1e6, 2),
                      "per_rank_frac_min": round(algo_bytes / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4),
                      "per_rank_frac_max": round(algo_bytes / best_avg_s / 1e9 / HBM_PEAK_GBS, 4)},
         "parity_spot_check": parity,
+        "parity_sample": (f"{idx.size} values (every 997th over the whole bucket, the first and last "
+                          f"4 Ki) vs numpy wrapping int32 sum"),
     }
     cpu_in = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

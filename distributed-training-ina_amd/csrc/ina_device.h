@@ -4,31 +4,56 @@
 
 namespace ina {
 
-// Streaming stores of the one-pass reduce and elementwise kernels.  INA_STORE_SC1 = 1: `global_store_dwordx{2,4}
-// ... sc1` (write-through at system scope), so a launch leaves no dirty lines for the next
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+// Streaming stores of the one-pass reduce and elementwise kernels.  INA_STORE_SC1 = 1: stores with
+// the sc1 cache-policy bit (write-through at system scope), so a launch leaves no dirty lines for the next
 // dependent launch's boundary to drain (MI355X_MICROARCH.md: a boundary costs + B / 6 TB/s
 // when the predecessor leaves B bytes dirty).  The headline reduce, interleaved on two
 // boxes (tools/lab/store_policy_lab.py, profiles/r03/lab/store_policy_lab*.log): back to
 // back 151.7 -> 150.9 and 149.2 -> 147.1 us, single launches 157.2 -> 153.1 and
 // 152.7 -> 148.5 us against nt stores; default-policy stores 155.8-156.4.
 // INA_STORE_SC1 = 0: the non-temporal (nt) stores of rounds 1-2.
+//
+// The sc1 store is a compiler builtin (`__builtin_amdgcn_raw_buffer_store_b*`, aux bit 4 =
+// SC1 on gfx950), never inline asm: the compiler then owns the store's wait states and
+// hazards (round 3's asm store needed a hand-placed s_nop -- a VALU overwrite of the data
+// VGPRs of a >8-byte store -- and gave wrong W = 16 sums without it).  A buffer store needs
+// a wave-uniform base: the wave's first active lane's address (readfirstlane) is the
+// resource base and every lane stores at its byte distance from it.
+// CONTRACT: at every call site a lane's address is >= the first active lane's (lanes
+// store at wave_base + lane * sizeof(T), or at rising packet / slot positions), so the
+// distance is small and positive.  Every caller in csrc/ keeps it (a lane below the first
+// one would fall outside the resource and its store would be dropped -- which the parity
+// tests of every kernel would see).  A per-store check with an ordinary-store fallback
+// measured 4-7 % slower on the streaming kernels and 2.3x on the int16 reduce (the branch
+// split the unrolled loop and doubled its registers; profiles/r04/lab/store_builtin_lab.log).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "stream_store's SC1 cache-policy bit (aux bit 4) is the gfx942 / gfx950 encoding"
+#endif
 #ifndef INA_STORE_SC1
 #define INA_STORE_SC1 1
 #endif
+// buffer resource word 3 for a raw (stride 0, untyped) gfx9 buffer: 32-bit data format
+constexpr int kRawBufferWord3 = 0x00020000;
+constexpr int kAuxSC1 = 16;
 template <typename T>
 __device__ __forceinline__ void stream_store(T v, T* p) {
 #if INA_STORE_SC1
     static_assert(sizeof(T) == 16 || sizeof(T) == 8 || sizeof(T) == 4, "16, 8 or 4-byte stores");
-    // a VALU write to the data VGPRs of a store of more than 8 bytes needs a wait state
-    // after the store; the compiler's hazard recognizer does not see the store inside the
-    // asm statement, so the asm carries it (without it: wrong sums at W = 16, whose
-    // allocation rewrites a store's data registers right after it)
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint64_t a0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                        (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t d = (uint32_t)(a - a0);
+    __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)a0, 0, 0x7FFFFFFF, kRawBufferWord3);
     if constexpr (sizeof(T) == 16)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, (int)d, 0, kAuxSC1);
     else if constexpr (sizeof(T) == 8)
-        asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)d, 0, kAuxSC1);
     else
-        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)d, 0, kAuxSC1);
 #else
     __builtin_nontemporal_store(v, p);
 #endif

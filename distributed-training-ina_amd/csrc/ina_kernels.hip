@@ -1852,6 +1852,7 @@ int ina_set_tuning(int key, int value) {
         case 15: return set_tiny_max(value);
         case 16: return set_zero_copy(value);
         case 17: return set_bucket_tile(value);
+        case 18: return set_runs(value);
         default: return INA_EINVAL;
     }
 }

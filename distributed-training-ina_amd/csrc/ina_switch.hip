@@ -282,6 +282,11 @@ static std::atomic<int> g_ack_fast{1};     // ina_set_tuning key 11: lone-ack la
 static std::atomic<int> g_sort_mode{0};
 static std::atomic<int> g_os_rounds{0};    // ina_set_tuning key 13: sort chunk rounds (0 auto, 4/8/16)
 static std::atomic<uint32_t> g_sort_epoch{0};   // per-call tag of the chunk sort's "unsorted" flag
+static std::atomic<int> g_runs{1};         // ina_set_tuning key 18: dense-run batches skip the sort (0: off)
+int set_runs(int v) {
+    g_runs = v ? 1 : 0;
+    return INA_OK;
+}
 int set_sort_mode(int v) {
     if (v != 0 && v != 3) return INA_EINVAL;
     g_sort_mode = v;
@@ -592,6 +597,26 @@ __device__ __forceinline__ uint32_t block_digit_scan(uint32_t x, uint32_t* wtot,
     return pre + inc - x;
 }
 
+// ---- structured batches: dense ascending runs --------------------------------------------
+// A batch made of a few runs of consecutive slots -- each worker's packets for slots s, s+1,
+// ... (worker-major arrival), the PS's acks for the previous step in front of them -- needs
+// no sort: slot s's segment is, in arrival order, the one packet each run holds for s, at
+// run_start + (s - run_first_slot).  A "break" is a packet that does not continue its
+// predecessor's run (first packet, slot != predecessor's + 1, a change of the PS-ack flag,
+// a foreign packet).  The chunk pass records each chunk's breaks (count + up to kRunsMax
+// (position, key) entries); when the whole batch has at most kRunsMax of them the bucket
+// pass builds the run table instead of sorting and the run kernel walks slots
+// (switch_runs_body).  Slots are independent (ngaa.p4:87-168) and a slot's packets stay in
+// arrival order (ngaa.p4:120-196), so the results are those of the sorted run.
+constexpr int kRunsMax = 64;   // one run per lane of the run kernel's waves
+// control block in the sort scratch (32-bit words): [0] foreign-bucket size, [1..3] epochs
+// (descent found, chunk pass, run table valid), then the run table: R, start[kRunsMax + 1]
+// (start[R] = npk), key[kRunsMax] (slot | ack bit of each run's first packet)
+constexpr int kCtlForeign = 0, kCtlEpochs = 1, kCtlRuns = 4;
+constexpr int kRunsStart = 1, kRunsKey = 2 + kRunsMax;
+constexpr int kCtlWords = kCtlRuns + kRunsKey + kRunsMax;
+static_assert(kCtlWords * 4 <= 1024, "control block fits its 1 KiB");
+
 template <int R, bool kDesc>
 __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restrict__ pkts,
                                                         const uint2* __restrict__ desc, size_t npk,
@@ -600,10 +625,13 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                                                         uint32_t* __restrict__ rcnt, uint32_t* __restrict__ rst,
                                                         size_t nch, uint32_t* __restrict__ kout,
                                                         uint32_t* __restrict__ vout, int ack_hint,
-                                                        uint32_t* __restrict__ unsorted, uint32_t epoch) {
+                                                        uint32_t* __restrict__ unsorted, uint32_t epoch,
+                                                        uint32_t* __restrict__ brk_cnt,
+                                                        uint2* __restrict__ brk_ent) {
     __shared__ uint32_t base[kBkWaves][kRsBins];     // per-wave digit counts, then bases
     __shared__ uint32_t gst[kRsBins];                 // the chunk's run starts (output positions)
     __shared__ uint32_t wtot[kBkWaves];
+    __shared__ uint32_t wbrk[kBkWaves];               // per-wave break counts
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
     const uint32_t nb = 1u << hbits;
@@ -617,8 +645,11 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     const size_t pw = i0 - (size_t)lane;                      // the wave's first position
     load_key_fields<1, kDesc>(pkts, desc, pw > 0 ? npk : 0, stride, pw - 1, pidx, psid, pack);
     __syncthreads();
-    uint32_t prev = psid[0] == (uint32_t)(uint8_t)switch_id && switch_id >= 0 ? pidx[0] % num_slots : num_slots;
+    const bool pmine = psid[0] == (uint32_t)(uint8_t)switch_id && switch_id >= 0;
+    uint32_t prev = pmine ? pidx[0] % num_slots : num_slots;
+    uint32_t prevf = prev | ((ack_hint && pmine && pack[0]) ? kAckBit : 0u);   // with the ack bit
     bool down = false;                                        // a key below its predecessor's
+    unsigned long long bm[R];                                 // breaks of the dense runs
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const size_t p = i0 + (size_t)r * 64;
@@ -634,12 +665,40 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp((int)prev, (int)key, 0x138, 0xF, 0xF, false);
         down |= p < npk && p > 0 && pk > key;
         prev = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
+        const uint32_t pkf = (uint32_t)__builtin_amdgcn_update_dpp((int)prevf, (int)k[r], 0x138, 0xF, 0xF, false);
+        bm[r] = __ballot(p < npk && (p == 0 || !mine || (pkf & ~kAckBit) + 1u != key ||
+                                     ((pkf ^ k[r]) & kAckBit) != 0u));
+        prevf = (uint32_t)__builtin_amdgcn_readlane((int)k[r], 63);
     }
     // the batch is not in slot order: B sorts (else B only copies A's output, which is then
     // the identity permutation).  Tagged with the call's epoch, so nothing needs clearing.
     if (__ballot(down) && lane == 0) unsorted[0] = epoch;
     if (c == 0 && threadIdx.x == 0) unsorted[1] = epoch;     // this call's epoch, for the run kernel
+    uint32_t nbw = 0;                                         // this wave's breaks
+#pragma unroll
+    for (int r = 0; r < R; ++r) nbw += (uint32_t)__builtin_popcountll(bm[r]);
+    if (lane == 0) wbrk[wv] = nbw;
     __syncthreads();
+    if (brk_cnt) {                                            // the chunk's breaks, in order
+        uint32_t tot = 0, pre = 0;
+#pragma unroll
+        for (int w = 0; w < kBkWaves; ++w) {
+            const uint32_t x = wbrk[w];
+            tot += x;
+            pre += w < wv ? x : 0u;
+        }
+        if (threadIdx.x == 0) brk_cnt[c] = tot;
+        if (tot <= (uint32_t)kRunsMax && nbw) {
+            const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if ((bm[r] >> lane) & 1ull)
+                    brk_ent[c * kRunsMax + pre + (uint32_t)__builtin_popcountll(bm[r] & below)] =
+                        uint2{(uint32_t)(i0 + (size_t)r * 64), k[r]};
+                pre += (uint32_t)__builtin_popcountll(bm[r]);
+            }
+        }
+    }
     // thread d owns digit d: the chunk's count, its chunk-local run start (block scan)
     const uint32_t d = threadIdx.x;
     uint32_t tc = 0;
@@ -698,8 +757,10 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
                                                          const uint32_t* __restrict__ rcnt,
                                                          const uint32_t* __restrict__ rst, uint32_t nch,
                                                          uint32_t CH, int lbits, uint32_t* __restrict__ nforeign,
-                                                         uint32_t skip, const uint32_t* __restrict__ unsorted,
-                                                         uint32_t epoch, int sorted_copy) {
+                                                         uint32_t skip, uint32_t* __restrict__ unsorted,
+                                                         uint32_t epoch, int sorted_copy,
+                                                         const uint32_t* __restrict__ brk_cnt,
+                                                         const uint2* __restrict__ brk_ent, uint32_t npk) {
     __shared__ uint32_t s_dst[kBkMaxChunks + 1], s_src[kBkMaxChunks];
     __shared__ uint32_t base[kBkWaves][kRsBins];
     __shared__ uint32_t gst[kRsBins];                 // bucket digit counts, then output positions
@@ -710,6 +771,44 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
     // run kernel reads it there (sorted_copy = 0), so only the foreign bucket's size is needed
     const bool in_order = unsorted[0] != epoch;
     if (in_order && !sorted_copy && b != skip) return;
+    if (!in_order && brk_cnt) {
+        // dense ascending runs (brk_cnt != NULL only for the register-resident run kernel):
+        // every block sums the chunks' break counts (the same answer everywhere); at most
+        // kRunsMax of them and block 0 writes the run table, nobody sorts
+        uint32_t part = 0;
+        for (uint32_t c = threadIdx.x; c < nch; c += kBkThr) part += brk_cnt[c];
+        const uint32_t inc = wave_incl_scan(part);
+        if (lane == 63) red[wv] = inc;
+        __syncthreads();
+        uint32_t total = 0;
+#pragma unroll
+        for (int w = 0; w < kBkWaves; ++w) total += red[w];
+        if (total <= (uint32_t)kRunsMax) {
+            if (b != 0) return;
+            // thread t: chunks 2t and 2t+1 (nch <= 2 x kBkThr), entries in chunk order
+            const uint32_t c0 = 2u * threadIdx.x;
+            const uint32_t n0 = c0 < nch ? brk_cnt[c0] : 0u, n1 = c0 + 1 < nch ? brk_cnt[c0 + 1] : 0u;
+            const uint32_t ex = block_digit_scan(n0 + n1, red2, 0u);
+            uint32_t* runs = unsorted + (kCtlRuns - kCtlEpochs);
+            for (uint32_t j = 0; j < n0; ++j) {
+                const uint2 e = brk_ent[(size_t)c0 * kRunsMax + j];
+                runs[kRunsStart + ex + j] = e.x;
+                runs[kRunsKey + ex + j] = e.y;
+            }
+            for (uint32_t j = 0; j < n1; ++j) {
+                const uint2 e = brk_ent[(size_t)(c0 + 1) * kRunsMax + j];
+                runs[kRunsStart + ex + n0 + j] = e.x;
+                runs[kRunsKey + ex + n0 + j] = e.y;
+            }
+            if (threadIdx.x == 0) {
+                runs[0] = total;
+                runs[kRunsStart + total] = npk;
+                unsorted[2] = epoch;                  // the run table is this call's
+            }
+            return;
+        }
+        __syncthreads();                              // red[] is reused below
+    }
     BK_STAMP(0);
     // this bucket's run in every chunk: thread t owns chunks [t*per, t*per + per).  A chunk's
     // run start rst[b][c] is the number of its packets in lower buckets, so the rst row also
@@ -1073,6 +1172,7 @@ struct PsFuse {
     uint8_t* acks;
     size_t ack_stride;
     int on, keep_fwd;   // keep_fwd = 0: completed packets are consumed, not written back
+    uint2* ack_desc;    // the ack rows' descriptors (header bytes 4..11), or NULL
 };
 
 // the run kernel's work for waves wave, wave + nwaves, ... (k_switch_run2: every wave of
@@ -1082,6 +1182,209 @@ struct PsFuse {
 // only after the first batch's packet loads are issued, so a segment waits for one memory
 // round trip instead of three (no gain where the kernel is bandwidth-bound, and it costs
 // registers there: profiles/r02/lab/switch_lab_state_late.log)
+// One slot segment -- packets q_begin .. q_end-1 of slot `slot`, in arrival order (after the
+// PS ack that leads it, when ack_led) -- through count (ngaa.p4:64-82), frag (fragcheck.p4:14-57) and
+// the V Processor registers (processor.p4:14-24) with the slot's state in registers.
+// pid_batch(q0, nb, pid) gives the packet ids of the segment's packets q0 .. q0+nb-1 (wave-
+// uniform): the sorted run reads them from its window, the structured run (a batch of
+// dense ascending runs) from its run table.
+template <bool kPs, bool kLat, typename PidFn>
+__device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                            size_t stride, uint8_t* __restrict__ actions, const PsFuse& ps,
+                                            uint32_t slot, bool ack_led, size_t q_begin, size_t q_end,
+                                            PidFn&& pid_batch) {
+    constexpr bool kActBatch = INA_SWITCH_ACT_BATCH;
+    const int lane = threadIdx.x & 63;
+    const int V = st.V;
+    const int L = V >> 2;                       // lanes holding values
+    const bool vl = lane < L;
+    const bool wide = L == 64;                  // tail chunk lives in lane 63's t[]
+    // slot state: count and frag are wave-uniform (SGPRs, scalar branches); the V
+    // registers are loaded only if a packet adds to them before any overwrite
+    // (count_reg == 1 overwrites, processor.p4:16-21), i.e. rarely
+    uint32_t cnt = 0, frag = 0, cnt_ld = 0, frag_ld = 0;
+    bool st_ready = false;
+    if constexpr (kLat) {
+        cnt_ld = st.count[slot];
+        frag_ld = st.frag[slot];
+    } else {
+        cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
+        frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
+    }
+    u32x4s reg = {0u, 0u, 0u, 0u};
+    bool have_reg = false;
+    for (size_t q0 = q_begin; q0 < q_end; q0 += kB) {
+        const int nb = (int)((q_end - q0) < (size_t)kB ? (q_end - q0) : (size_t)kB);
+        u32x4s a[kB];
+        uint32_t pid[kB];
+        pid_batch(q0, nb, pid);
+        // tail chunks 64 (V = 256 only): lane b holds packet b's, 4 VGPRs for the whole
+        // batch instead of 4 per packet; lane 63 takes them by readlane when it needs
+        // them.  Issued first, so packet 0 can start once its own load is back.
+        // Every load is unconditional (slots past the batch re-read packet 0, lanes past
+        // L re-read chunk 0) so no load sits in a branch: the compiler's wait counting
+        // stays exact and packet b waits only for its own data.
+#pragma unroll
+        for (int b = 1; b < kB; ++b) pid[b] = b < nb ? pid[b] : pid[0];
+        u32x4s tl = {0u, 0u, 0u, 0u};
+        uint32_t mypid = pid[0];                 // lane b: packet b's id
+#pragma unroll
+        for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
+        uint32_t act_v = 0;                      // lane b: packet b's action (kActBatch)
+        if (wide) {
+#if INA_SWITCH_TAIL_NT
+            tl = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
+#else
+            tl = *(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
+#endif
+        }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[b] * stride);
+            a[b] = sw_ld(pk + (lane <= L ? lane : 0));
+        }
+        if constexpr (kLat) {
+            if (!st_ready) {
+                cnt = __builtin_amdgcn_readfirstlane(cnt_ld);
+                frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(frag_ld);
+                st_ready = true;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            if (b >= nb) break;
+            const uint32_t h1 = __builtin_amdgcn_readlane(a[b].y, 0),
+                           h2 = __builtin_amdgcn_readlane(a[b].z, 0),
+                           h3 = __builtin_amdgcn_readlane(a[b].w, 0);
+            const uint32_t hcount = h1 & 0xFFu, flags = (h1 >> 8) & 0xFFu;
+            // keep the state machine scalar (SGPRs + scalar branches)
+            const uint32_t frag_in =
+                __builtin_amdgcn_readfirstlane(__builtin_bswap32((h2 >> 24) | (h3 << 8)));
+            uint8_t act;
+            if ((flags >> 6) & 1u) {                     // ack: reset_id (fragcheck.p4:26-31)
+                frag = 0;
+                act = INA_ACT_FWD_ACK;
+            } else {
+                if (frag == 0) frag = frag_in;           // write_read_id (fragcheck.p4:14-24)
+                if (frag != frag_in) {                   // collision (ngaa.p4:177-181):
+                    act = INA_ACT_FWD_COLLISION;         // only the flag byte changes
+                    if (lane == 0)
+                        reinterpret_cast<uint32_t*>(pkts + (size_t)pid[b] * stride)[1] =
+                            a[b].y | ((uint32_t)INA_FLAG_COLLISION << 8);
+                } else {
+                    cnt = (cnt + 1u) & 0xFFu;            // read_add_count (ngaa.p4:66-78)
+                    if (cnt == hcount) cnt = 0;
+                    cnt = __builtin_amdgcn_readfirstlane(cnt);
+                    const bool first = cnt == 1u;
+                    u32x4s c;                            // chunk l+1
+                    c.x = from_next_lane(a[b].x); c.y = from_next_lane(a[b].y);
+                    c.z = from_next_lane(a[b].z); c.w = from_next_lane(a[b].w);
+                    uint32_t tw = 0;                     // old byte 1039 (padding) for the tail
+                    if (wide) {
+                        const uint32_t tx = __builtin_amdgcn_readlane(tl.x, b);
+                        const uint32_t ty = __builtin_amdgcn_readlane(tl.y, b);
+                        const uint32_t tz = __builtin_amdgcn_readlane(tl.z, b);
+                        tw = __builtin_amdgcn_readlane(tl.w, b);
+                        if (lane == 63) c = u32x4s{tx, ty, tz, tw};
+                    }
+                    u32x4s v;                            // values 4l..4l+3
+                    v.x = dec_be(c.x, a[b].w);
+                    v.y = dec_be(c.y, c.x);
+                    v.z = dec_be(c.z, c.y);
+                    v.w = dec_be(c.w, c.z);
+                    if (first) {                         // processor.p4:16-21
+                        reg = v;
+                    } else if (have_reg) {
+                        reg += v;
+                    } else {                             // adds to a stored register:
+                        reg = vl ? *reinterpret_cast<const u32x4s*>(   // load it now
+                                       st.regs + (size_t)slot * V + 4 * lane)
+                                 : u32x4s{0u, 0u, 0u, 0u};
+                        reg += v;
+                    }
+                    have_reg = true;
+                    act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
+                    // the PS consumes a completed packet of its bucket (ps_slot in range;
+                    // wave-uniform); one outside the bucket is forwarded like the two-call
+                    // path forwards it, whatever keep_fwd says
+                    const uint32_t ps_slot = frag_in - ps.seq0;
+                    const bool consumed = kPs && act == INA_ACT_FWD_AGG && ps_slot < ps.nslots;
+                    if (consumed) {                      // launch.py:46-50 with the switch's sum
+                        {
+                            const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)lane;
+                            if (vl && e0 + 4 <= ps.n) {
+                                const f32x4s l = *reinterpret_cast<const f32x4s*>(ps.local + e0);
+                                f32x4s r;
+                                r.x = __fadd_rn(l.x, __fmul_rn(__fmul_rn((float)(int32_t)reg.x, ps.inv), ps.ws));
+                                r.y = __fadd_rn(l.y, __fmul_rn(__fmul_rn((float)(int32_t)reg.y, ps.inv), ps.ws));
+                                r.z = __fadd_rn(l.z, __fmul_rn(__fmul_rn((float)(int32_t)reg.z, ps.inv), ps.ws));
+                                r.w = __fadd_rn(l.w, __fmul_rn(__fmul_rn((float)(int32_t)reg.w, ps.inv), ps.ws));
+                                // nt: 249.9 -> 241.3 us for the fused pass, the
+                                // steady-state step 0.71 -> 0.70 ms (default policy;
+                                // write-through 247.8; profiles/r03/lab/psout_lab.log)
+                                __builtin_nontemporal_store(r, reinterpret_cast<f32x4s*>(ps.out + e0));
+                            } else if (vl) {
+                                const uint32_t rv[4] = {reg.x, reg.y, reg.z, reg.w};
+                                for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
+                                    ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
+                                        __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
+                            }
+                            if (lane == 0 && ps.acks) {      // the PS ack (fragcheck.p4:26-31)
+                                u32x4s hd = a[b];
+                                hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+                                hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                                *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
+                                // its descriptor, so the next switch batch (these acks in
+                                // front of the next step's packets) needs no gather pass
+                                if (ps.ack_desc) ps.ack_desc[ps_slot] = uint2{hd.y, hd.z};
+                            }
+                        }
+                    }
+                    if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
+                        // out_value -> payload (processor.p4:22): chunk c from lane c-1
+                        u32x4s p;
+                        p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
+                        p.z = from_prev_lane(reg.z); p.w = from_prev_lane(reg.w);
+                        u32x4s e = a[b];
+                        if (lane == 0) {
+                            e.w = (e.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                        } else {
+                            e.x = enc_lo(p.x, p.y);
+                            e.y = enc_lo(p.y, p.z);
+                            e.z = enc_lo(p.z, p.w);
+                            e.w = enc_lo(p.w, lane < L ? reg.x : e.w);
+                        }
+                        if (lane <= L)
+                            sw_st(e, reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride) + lane);
+                        if (wide && lane == 63) {        // tail chunk 64 from lane 63's values
+                            u32x4s o;
+                            o.x = enc_lo(reg.x, reg.y);
+                            o.y = enc_lo(reg.y, reg.z);
+                            o.z = enc_lo(reg.z, reg.w);
+                            o.w = enc_lo(reg.w, tw);
+                            sw_st(o, reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride) + 64);
+                        }
+                    }
+                }
+            }
+            if constexpr (kActBatch) act_v = lane == b ? (uint32_t)act : act_v;
+            else if (lane == 0) actions[pid[b]] = act;
+        }
+        if constexpr (kActBatch)
+            if (lane < nb) actions[mypid] = (uint8_t)act_v;   // one store for the batch
+    }
+    if (lane == 0) {
+        st.count[slot] = (uint8_t)cnt;
+        st.frag[slot] = frag;
+    }
+    // the slot registers are written once per call and read back only by a later batch
+    // (and then rarely: the first packet of a fresh segment overwrites them), so they
+    // are stored nt and do not displace the packet lines the gather shares in L2:
+    // bench.py's switch leg 228.4 -> 213.9 us worker-major, 217.2 -> 195.1 round-robin
+    // (tools/lab/psout_ab.sh, profiles/r03/lab/switch_reg_nt_lab.log)
+    if (have_reg && vl) __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane));
+}
+
 template <bool kPs, bool kLat = false>
 __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                  size_t npk, size_t stride,
@@ -1090,12 +1393,7 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                                  uint8_t* __restrict__ actions, uint32_t win,
                                                  uint32_t kmask, const PsFuse& ps, size_t wave,
                                                  size_t nwaves) {
-    constexpr bool kActBatch = INA_SWITCH_ACT_BATCH;
     const int lane = threadIdx.x & 63;
-    const int V = st.V;
-    const int L = V >> 2;                       // lanes holding values
-    const bool vl = lane < L;
-    const bool wide = L == 64;                  // tail chunk lives in lane 63's t[]
     const uint32_t NS = st.num_slots;
     // each wave takes windows of 64 sorted positions and processes the segments that
     // START in its window (a segment may run past the window's end)
@@ -1141,25 +1439,9 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                 }
             }
         }
-        // slot state: count and frag are wave-uniform (SGPRs, scalar branches); the V
-        // registers are loaded only if a packet adds to them before any overwrite
-        // (count_reg == 1 overwrites, processor.p4:16-21), i.e. rarely
         const bool ack_led = (am >> hl) & 1ull;
-        uint32_t cnt = 0, frag = 0, cnt_ld = 0, frag_ld = 0;
-        bool st_ready = false;
-        if constexpr (kLat) {
-            cnt_ld = st.count[slot];
-            frag_ld = st.frag[slot];
-        } else {
-            cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
-            frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
-        }
-        u32x4s reg = {0u, 0u, 0u, 0u};
-        bool have_reg = false;
-        for (size_t q0 = pos + (ack_led ? 1 : 0); q0 < end; q0 += kB) {
-            const int nb = (int)((end - q0) < (size_t)kB ? (end - q0) : (size_t)kB);
-            u32x4s a[kB];
-            uint32_t pid[kB];
+        run_segment<kPs, kLat>(st, pkts, stride, actions, ps, slot, ack_led, pos + (ack_led ? 1 : 0), end,
+                               [&](size_t q0, int nb, uint32_t (&pid)[kB]) {
             // packet ids first (no load in the common in-window case; one coalesced load
             // otherwise), so the kB packet loads below issue back to back with no
             // s_waitcnt between them
@@ -1173,169 +1455,80 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
 #pragma unroll
                 for (int b = 0; b < kB; ++b) pid[b] = __builtin_amdgcn_readlane(my, b);
             }
-            // tail chunks 64 (V = 256 only): lane b holds packet b's, 4 VGPRs for the whole
-            // batch instead of 4 per packet; lane 63 takes them by readlane when it needs
-            // them.  Issued first, so packet 0 can start once its own load is back.
-            // Every load is unconditional (slots past the batch re-read packet 0, lanes past
-            // L re-read chunk 0) so no load sits in a branch: the compiler's wait counting
-            // stays exact and packet b waits only for its own data.
+        });
+        }
+    }
+}
+
+// The run kernel's work over a batch of dense ascending runs (the run table the bucket
+// pass wrote, see kRunsMax): lane r holds run r; each wave takes one contiguous range of
+// slots (one pass of the grid) and runs slot s's segment -- the packets start_r + s -
+// first_r of the runs that hold s, in run order = arrival order -- through run_segment.
+// A PS ack leading its segment is done without reading it, as in switch_run2_body.
+template <bool kPs>
+__device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                                 size_t stride, uint8_t* __restrict__ actions,
+                                                 uint32_t kmask, const PsFuse& ps,
+                                                 const uint32_t* __restrict__ runs, size_t wave,
+                                                 size_t nwaves) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t NS = st.num_slots;
+    const uint32_t R = __builtin_amdgcn_readfirstlane(runs[0]);
+    uint32_t rpos = 0, rslot = 0, rlen = 0;
+    bool rack = false;
+    if ((uint32_t)lane < R) {
+        rpos = runs[kRunsStart + lane];
+        rlen = runs[kRunsStart + lane + 1] - rpos;
+        const uint32_t rk = runs[kRunsKey + lane];
+        rslot = rk & kmask;
+        rack = (rk & ~kmask) != 0u;
+        if (rslot >= NS) rlen = 0;                    // foreign packets: A set their action
+    }
+    // the slots the runs cover: [lo, hi)
+    uint32_t lo = rlen ? rslot : 0xFFFFFFFFu, hi = rlen ? rslot + rlen : 0u;
 #pragma unroll
-            for (int b = 1; b < kB; ++b) pid[b] = b < nb ? pid[b] : pid[0];
-            u32x4s tl = {0u, 0u, 0u, 0u};
-            uint32_t mypid = pid[0];                 // lane b: packet b's id
-#pragma unroll
-            for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
-            uint32_t act_v = 0;                      // lane b: packet b's action (kActBatch)
-            if (wide) {
-#if INA_SWITCH_TAIL_NT
-                tl = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
-#else
-                tl = *(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
-#endif
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    if (lo >= hi) return;
+    const size_t per = ((size_t)(hi - lo) + nwaves - 1) / nwaves;
+    const size_t s_begin = (size_t)lo + wave * per;
+    const size_t s_end = s_begin + per < (size_t)hi ? s_begin + per : (size_t)hi;
+    for (size_t s = s_begin; s < s_end; ++s) {
+        const uint32_t slot = (uint32_t)s;
+        const uint32_t off = slot - rslot;
+        const bool in = off < rlen;                   // wraps above for slots below the run
+        unsigned long long m = __ballot(in);
+        if (!m) continue;
+        const uint32_t pidv = rpos + off;
+        const int l0 = __builtin_ctzll(m);
+        const bool ack_led = (__ballot(in && rack) >> l0) & 1ull;
+        if (ack_led) {                                // reset_id (fragcheck.p4:26-31), unread
+            const uint32_t p0 = __builtin_amdgcn_readlane(pidv, l0);
+            m &= m - 1;
+            if (lane == 0) {
+                actions[p0] = INA_ACT_FWD_ACK;
+                if (!m) st.frag[slot] = 0u;           // a lone ack
             }
+            if (!m) continue;
+        }
+        run_segment<kPs, false>(st, pkts, stride, actions, ps, slot, ack_led, 0,
+                                (size_t)__builtin_popcountll(m),
+                                [&](size_t, int nb, uint32_t (&pid)[kB]) {
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
-                const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[b] * stride);
-                a[b] = sw_ld(pk + (lane <= L ? lane : 0));
-            }
-            if constexpr (kLat) {
-                if (!st_ready) {
-                    cnt = __builtin_amdgcn_readfirstlane(cnt_ld);
-                    frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(frag_ld);
-                    st_ready = true;
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < kB; ++b) {
-                if (b >= nb) break;
-                const uint32_t h1 = __builtin_amdgcn_readlane(a[b].y, 0),
-                               h2 = __builtin_amdgcn_readlane(a[b].z, 0),
-                               h3 = __builtin_amdgcn_readlane(a[b].w, 0);
-                const uint32_t hcount = h1 & 0xFFu, flags = (h1 >> 8) & 0xFFu;
-                // keep the state machine scalar (SGPRs + scalar branches)
-                const uint32_t frag_in =
-                    __builtin_amdgcn_readfirstlane(__builtin_bswap32((h2 >> 24) | (h3 << 8)));
-                uint8_t act;
-                if ((flags >> 6) & 1u) {                     // ack: reset_id (fragcheck.p4:26-31)
-                    frag = 0;
-                    act = INA_ACT_FWD_ACK;
+                if (b < nb) {
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    pid[b] = __builtin_amdgcn_readlane(pidv, l);
                 } else {
-                    if (frag == 0) frag = frag_in;           // write_read_id (fragcheck.p4:14-24)
-                    if (frag != frag_in) {                   // collision (ngaa.p4:177-181):
-                        act = INA_ACT_FWD_COLLISION;         // only the flag byte changes
-                        if (lane == 0)
-                            reinterpret_cast<uint32_t*>(pkts + (size_t)pid[b] * stride)[1] =
-                                a[b].y | ((uint32_t)INA_FLAG_COLLISION << 8);
-                    } else {
-                        cnt = (cnt + 1u) & 0xFFu;            // read_add_count (ngaa.p4:66-78)
-                        if (cnt == hcount) cnt = 0;
-                        cnt = __builtin_amdgcn_readfirstlane(cnt);
-                        const bool first = cnt == 1u;
-                        u32x4s c;                            // chunk l+1
-                        c.x = from_next_lane(a[b].x); c.y = from_next_lane(a[b].y);
-                        c.z = from_next_lane(a[b].z); c.w = from_next_lane(a[b].w);
-                        uint32_t tw = 0;                     // old byte 1039 (padding) for the tail
-                        if (wide) {
-                            const uint32_t tx = __builtin_amdgcn_readlane(tl.x, b);
-                            const uint32_t ty = __builtin_amdgcn_readlane(tl.y, b);
-                            const uint32_t tz = __builtin_amdgcn_readlane(tl.z, b);
-                            tw = __builtin_amdgcn_readlane(tl.w, b);
-                            if (lane == 63) c = u32x4s{tx, ty, tz, tw};
-                        }
-                        u32x4s v;                            // values 4l..4l+3
-                        v.x = dec_be(c.x, a[b].w);
-                        v.y = dec_be(c.y, c.x);
-                        v.z = dec_be(c.z, c.y);
-                        v.w = dec_be(c.w, c.z);
-                        if (first) {                         // processor.p4:16-21
-                            reg = v;
-                        } else if (have_reg) {
-                            reg += v;
-                        } else {                             // adds to a stored register:
-                            reg = vl ? *reinterpret_cast<const u32x4s*>(   // load it now
-                                           st.regs + (size_t)slot * V + 4 * lane)
-                                     : u32x4s{0u, 0u, 0u, 0u};
-                            reg += v;
-                        }
-                        have_reg = true;
-                        act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
-                        // the PS consumes a completed packet of its bucket (ps_slot in range;
-                        // wave-uniform); one outside the bucket is forwarded like the two-call
-                        // path forwards it, whatever keep_fwd says
-                        const uint32_t ps_slot = frag_in - ps.seq0;
-                        const bool consumed = kPs && act == INA_ACT_FWD_AGG && ps_slot < ps.nslots;
-                        if (consumed) {                      // launch.py:46-50 with the switch's sum
-                            {
-                                const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)lane;
-                                if (vl && e0 + 4 <= ps.n) {
-                                    const f32x4s l = *reinterpret_cast<const f32x4s*>(ps.local + e0);
-                                    f32x4s r;
-                                    r.x = __fadd_rn(l.x, __fmul_rn(__fmul_rn((float)(int32_t)reg.x, ps.inv), ps.ws));
-                                    r.y = __fadd_rn(l.y, __fmul_rn(__fmul_rn((float)(int32_t)reg.y, ps.inv), ps.ws));
-                                    r.z = __fadd_rn(l.z, __fmul_rn(__fmul_rn((float)(int32_t)reg.z, ps.inv), ps.ws));
-                                    r.w = __fadd_rn(l.w, __fmul_rn(__fmul_rn((float)(int32_t)reg.w, ps.inv), ps.ws));
-                                    // nt: 249.9 -> 241.3 us for the fused pass, the
-                                    // steady-state step 0.71 -> 0.70 ms (default policy;
-                                    // write-through 247.8; profiles/r03/lab/psout_lab.log)
-                                    __builtin_nontemporal_store(r, reinterpret_cast<f32x4s*>(ps.out + e0));
-                                } else if (vl) {
-                                    const uint32_t rv[4] = {reg.x, reg.y, reg.z, reg.w};
-                                    for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
-                                        ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
-                                            __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
-                                }
-                                if (lane == 0 && ps.acks) {      // the PS ack (fragcheck.p4:26-31)
-                                    u32x4s hd = a[b];
-                                    hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
-                                    hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
-                                    *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
-                                }
-                            }
-                        }
-                        if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
-                            // out_value -> payload (processor.p4:22): chunk c from lane c-1
-                            u32x4s p;
-                            p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
-                            p.z = from_prev_lane(reg.z); p.w = from_prev_lane(reg.w);
-                            u32x4s e = a[b];
-                            if (lane == 0) {
-                                e.w = (e.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
-                            } else {
-                                e.x = enc_lo(p.x, p.y);
-                                e.y = enc_lo(p.y, p.z);
-                                e.z = enc_lo(p.z, p.w);
-                                e.w = enc_lo(p.w, lane < L ? reg.x : e.w);
-                            }
-                            if (lane <= L)
-                                sw_st(e, reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride) + lane);
-                            if (wide && lane == 63) {        // tail chunk 64 from lane 63's values
-                                u32x4s o;
-                                o.x = enc_lo(reg.x, reg.y);
-                                o.y = enc_lo(reg.y, reg.z);
-                                o.z = enc_lo(reg.z, reg.w);
-                                o.w = enc_lo(reg.w, tw);
-                                sw_st(o, reinterpret_cast<u32x4s*>(pkts + (size_t)pid[b] * stride) + 64);
-                            }
-                        }
-                    }
+                    pid[b] = 0u;
                 }
-                if constexpr (kActBatch) act_v = lane == b ? (uint32_t)act : act_v;
-                else if (lane == 0) actions[pid[b]] = act;
             }
-            if constexpr (kActBatch)
-                if (lane < nb) actions[mypid] = (uint8_t)act_v;   // one store for the batch
-        }
-        if (lane == 0) {
-            st.count[slot] = (uint8_t)cnt;
-            st.frag[slot] = frag;
-        }
-        // the slot registers are written once per call and read back only by a later batch
-        // (and then rarely: the first packet of a fresh segment overwrites them), so they
-        // are stored nt and do not displace the packet lines the gather shares in L2:
-        // bench.py's switch leg 228.4 -> 213.9 us worker-major, 217.2 -> 195.1 round-robin
-        // (tools/lab/psout_ab.sh, profiles/r03/lab/switch_reg_nt_lab.log)
-        if (have_reg && vl) __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane));
-        }
+        });
     }
 }
 
@@ -1368,19 +1561,27 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                           const uint32_t* __restrict__ keys_a,
                                                           const uint32_t* __restrict__ ids_a,
                                                           const uint32_t* __restrict__ unsorted) {
+    const size_t wave = switch_block_index() * (kSwBlock / 64) + wave_in_block();
+    const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
+    // (unsorted[1]: the epoch of the sort that filled the scratch, written by its chunk pass,
+    // so a run queued apart from its sort needs no host-side state)
+    if (unsorted) {
+        const uint32_t ep = unsorted[1];
+        if (unsorted[0] != ep) {
+            // a batch already in slot order: the chunk sort's own output is the sorted order
+            keys = keys_a;
+            ids = ids_a;
+        } else if (unsorted[2] == ep) {
+            // a batch of dense ascending runs: the bucket pass wrote the run table, not a sort
+            switch_runs_body<kPs>(st, pkts, stride, actions, kmask, ps, unsorted + (kCtlRuns - kCtlEpochs),
+                                  wave, nwaves);
+            return;
+        }
+    }
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
-    // a batch already in slot order: the chunk sort's own output is the sorted order
-    // (unsorted[1]: the epoch of the sort that filled the scratch, written by its chunk pass,
-    // so a run queued apart from its sort needs no host-side state)
-    if (unsorted && unsorted[0] != unsorted[1]) {
-        keys = keys_a;
-        ids = ids_a;
-    }
-    switch_run2_body<kPs>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps,
-                          switch_block_index() * (kSwBlock / 64) + wave_in_block(),
-                          ((size_t)gridDim.x * kSwBlock) >> 6);
+    switch_run2_body<kPs>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps, wave, nwaves);
 }
 
 // batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
@@ -1437,36 +1638,50 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
 // sort scratch after the four key / id arrays, sized for the SMALLEST chunk whatever tier
 // npk falls in (so the size is monotonic in npk: a buffer sized for a batch serves every
 // smaller batch): per (digit, chunk) counts -- the digit passes' histogram, or A's run
-// lengths -- and A's run starts, the digit passes' digit totals, and the size of the
-// foreign-only bucket B leaves out
+// lengths -- and A's run starts, the digit passes' digit totals, the control block (the
+// size of the foreign-only bucket B leaves out, the epochs, the run table) and A's per-chunk
+// breaks of the dense runs (count + kRunsMax entries per chunk)
 struct SortAux {
     uint32_t* hist;               // [2^bits][nch]
     uint32_t* rst;                // [2^bits][nch]
     uint32_t* totals;             // [512]
-    uint32_t* nforeign;           // [1]
-    uint32_t* unsorted;           // [2]: the epoch of the last call whose keys were out of order,
-                                  // the epoch of the last chunk pass
+    uint32_t* nforeign;           // control block word kCtlForeign
+    uint32_t* unsorted;           // [3]: the epoch of the last call whose keys were out of order,
+                                  // the epoch of the last chunk pass, the epoch of the last run
+                                  // table; the run table follows
+    uint32_t* brk_cnt;            // [nch]
+    uint2* brk_ent;               // [nch][kRunsMax]
 };
+
+static size_t sort_nch_cap(size_t npk) {
+    const size_t chunk = (size_t)kRsWaves * 64 * (size_t)INA_RS_ROUNDS_SMALL;
+    return (npk + chunk - 1) / chunk;
+}
 
 static size_t sort_hist_cap(size_t npk, uint32_t num_slots) {
     const SortPlan p = sort_plan(npk, num_slots);
-    const size_t chunk = (size_t)kRsWaves * 64 * (size_t)INA_RS_ROUNDS_SMALL;
-    return ((size_t)1 << p.bits) * ((npk + chunk - 1) / chunk);
+    return ((size_t)1 << p.bits) * sort_nch_cap(npk);
 }
 
 static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
     const size_t hist = align_up(sort_hist_cap(npk, num_slots) * 4, 256);
-    return 2 * hist + align_up((size_t)kRsBins * 4, 256) + 256;
+    const size_t nc = sort_nch_cap(npk);
+    return 2 * hist + align_up((size_t)kRsBins * 4, 256) + 1024 + align_up(nc * 4, 256) +
+           nc * (size_t)kRunsMax * 8;
 }
 
 static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
     const size_t hist = align_up(sort_hist_cap(npk, num_slots) * 4, 256);
+    const size_t nc = sort_nch_cap(npk);
     SortAux a;
     a.hist = reinterpret_cast<uint32_t*>(aux);
     a.rst = reinterpret_cast<uint32_t*>(aux + hist);
     a.totals = reinterpret_cast<uint32_t*>(aux + 2 * hist);
-    a.nforeign = reinterpret_cast<uint32_t*>(aux + 2 * hist + align_up((size_t)kRsBins * 4, 256));
-    a.unsorted = a.nforeign + 1;
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(aux + 2 * hist + align_up((size_t)kRsBins * 4, 256));
+    a.nforeign = ctl + kCtlForeign;
+    a.unsorted = ctl + kCtlEpochs;
+    a.brk_cnt = ctl + 256;
+    a.brk_ent = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(a.brk_cnt) + align_up(nc * 4, 256));
     return a;
 }
 
@@ -1606,6 +1821,9 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const int lb = eb - sp.bits;                       // low digit bits (0: one-digit keys)
         const uint2* dsc = reinterpret_cast<const uint2*>(desc);
         const int ah = ack_hint ? 1 : 0;
+        // dense ascending runs skip the sort (run table, switch_runs_body): the register-
+        // resident run kernel only (ina_set_tuning key 18 = 0 turns it off)
+        const bool runs_on = fast && g_runs.load() != 0;
         // never 0 (fresh scratch reads as "unsorted": the safe side); a stale epoch equal to
         // this one (2^32 calls later) also only costs the full sort
         if (do_sort) {
@@ -1614,7 +1832,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
 #define INA_A_LAUNCH(RR)                                                                              \
         hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true> : &k_sort_chunks<RR, false>), dim3(gc),   \
                            dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id,  \
-                           actions, sp.bits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, ax.unsorted, epoch)
+                           actions, sp.bits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, ax.unsorted, epoch, \
+                           runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
         if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
         else INA_A_LAUNCH(kR0 / 4);
@@ -1637,7 +1856,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         if (do_sort)
             hipLaunchKernelGGL((big ? &k_sort_buckets<kLcRoundsBig> : &k_sort_buckets<kLcRounds>), dim3(gb),
                                dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
-                               ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1);
+                               ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1,
+                               runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, (uint32_t)npk);
         if (fast) unsorted = ax.unsorted;
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {
@@ -1731,7 +1951,7 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
                              const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
                              uint32_t seq0, const float* local, int k, double weight_step,
                              float* out, size_t n, uint8_t* acks, size_t ack_stride,
-                             int keep_forwarded, ina_stream_t stream, int phase);
+                             ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream, int phase);
 
 int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
                                   const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
@@ -1739,7 +1959,16 @@ int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, s
                                   float* out, size_t n, uint8_t* acks, size_t ack_stride,
                                   int keep_forwarded, ina_stream_t stream) {
     return switch_apply_impl(st, pkts, npk, stride, desc, actions, scratch, seq0, local, k, weight_step,
-                             out, n, acks, ack_stride, keep_forwarded, stream, 0);
+                             out, n, acks, ack_stride, nullptr, keep_forwarded, stream, 0);
+}
+
+int ina_switch_process_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                                     const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                                     uint32_t seq0, const float* local, int k, double weight_step,
+                                     float* out, size_t n, uint8_t* acks, size_t ack_stride,
+                                     ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream) {
+    return switch_apply_impl(st, pkts, npk, stride, desc, actions, scratch, seq0, local, k, weight_step,
+                             out, n, acks, ack_stride, ack_desc, keep_forwarded, stream, 0);
 }
 
 int ina_switch_sort_desc(const ina_switch_state_t* st, const uint8_t* pkts, size_t npk, size_t stride,
@@ -1763,14 +1992,23 @@ int ina_switch_run_sorted_apply(const ina_switch_state_t* st, uint8_t* pkts, siz
                                 double weight_step, float* out, size_t n, uint8_t* acks,
                                 size_t ack_stride, int keep_forwarded, ina_stream_t stream) {
     return switch_apply_impl(st, pkts, npk, stride, nullptr, actions, scratch, seq0, local, k, weight_step,
-                             out, n, acks, ack_stride, keep_forwarded, stream, 2);
+                             out, n, acks, ack_stride, nullptr, keep_forwarded, stream, 2);
+}
+
+int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                                        uint8_t* actions, void* scratch, uint32_t seq0, const float* local,
+                                        int k, double weight_step, float* out, size_t n, uint8_t* acks,
+                                        size_t ack_stride, ina_nga_desc_t* ack_desc, int keep_forwarded,
+                                        ina_stream_t stream) {
+    return switch_apply_impl(st, pkts, npk, stride, nullptr, actions, scratch, seq0, local, k, weight_step,
+                             out, n, acks, ack_stride, ack_desc, keep_forwarded, stream, 2);
 }
 
 static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
                              const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
                              uint32_t seq0, const float* local, int k, double weight_step,
                              float* out, size_t n, uint8_t* acks, size_t ack_stride,
-                             int keep_forwarded, ina_stream_t stream, int phase) {
+                             ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream, int phase) {
     if (k < -126 || k > 127) return set_error(INA_EINVAL, "k out of range [-126,127]%s", "");
     if (npk == 0) return INA_OK;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
@@ -1778,6 +2016,8 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
         return set_error(INA_EINVAL, "local/out must be 16-byte aligned%s", "");
     if (acks && (((uintptr_t)acks & 15u) || ack_stride % 16))
         return set_error(INA_EINVAL, "ack rows must be 16-byte aligned%s", "");
+    if (ack_desc && (!acks || ((uintptr_t)ack_desc & 7u)))
+        return set_error(INA_EINVAL, "ack descriptors need ack rows and 8-byte alignment%s", "");
     if (!st || st->V <= 0) return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
     // the PS step needs the layout ina_apply_completed_nga and the fused run kernel take
     // (16-byte aligned rows and slot registers); refuse before the switch touches its state
@@ -1788,14 +2028,28 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
     const size_t nslots = (n + (size_t)st->V - 1) / (size_t)st->V;
     PsFuse ps{local, out, n, ldexpf(1.0f, -k), (float)weight_step, seq0,
               nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,
-              keep_forwarded ? 1 : 0};
+              keep_forwarded ? 1 : 0, reinterpret_cast<uint2*>(ack_desc)};
     bool fused = false;
     if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused, phase))
         return rc;
     if (fused) return INA_OK;
     // layouts the register-resident run kernel does not take: the two steps one by one
-    return ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,
-                                   n, acks, ack_stride, stream);
+    if (int rc = ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,
+                                         n, acks, ack_stride, stream))
+        return rc;
+    return ack_desc ? ina_nga_descriptors(acks, nslots, ack_stride, ack_desc, stream) : INA_OK;
+}
+
+int ina_switch_batch_path(const void* scratch, size_t npk, uint32_t num_slots, int* path) {
+    if (!scratch || !path || npk == 0 || npk > 0x7FFFFFFFu || num_slots == 0)
+        return set_error(INA_EINVAL, "bad arguments%s", "");
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(align_up((uintptr_t)scratch, 256));
+    const SortAux ax = sort_aux(const_cast<uint8_t*>(base) + 4 * align_up(npk * 4, 256), npk, num_slots);
+    uint32_t e[3];
+    if (hipMemcpy(e, ax.unsorted, sizeof(e), hipMemcpyDeviceToHost) != hipSuccess)
+        return set_error(INA_EHIP, "reading the control block%s", "");
+    *path = e[0] != e[1] ? INA_PATH_IN_ORDER : e[2] == e[1] ? INA_PATH_RUNS : INA_PATH_SORTED;
+    return INA_OK;
 }
 
 int ina_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_default,

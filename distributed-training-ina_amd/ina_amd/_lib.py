@@ -82,10 +82,15 @@ SIGNATURES = {
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
     "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],
     "ina_switch_scratch_bytes": [_sz, _u32],
+    "ina_switch_batch_path": [_vp, _sz, _u32, C.POINTER(C.c_int)],
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
     "ina_switch_process_apply": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i, _d,
                                  _vp, _sz, _vp, _sz, _i, _vp],
     "ina_switch_process_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _vp],
+    "ina_switch_process_apply_ackdesc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _u32, _vp,
+                                         _i, _d, _vp, _sz, _vp, _sz, _vp, _i, _vp],
+    "ina_switch_run_sorted_apply_ackdesc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i,
+                                            _d, _vp, _sz, _vp, _sz, _vp, _i, _vp],
     "ina_switch_process_apply_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _u32, _vp,
                                       _i, _d, _vp, _sz, _vp, _sz, _i, _vp],
     "ina_route_ipv4": [_vp, _vp, _u32, _sz, _vp, _vp, _i, _vp, _vp],

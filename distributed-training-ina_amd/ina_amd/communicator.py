@@ -21,9 +21,13 @@ The process fan-outs (multi_process_send, multi_process_send_futures_P) start th
 workers with the "spawn" method, never fork: send_gradients runs HIP (the packets are
 built on the GPU), and a child forked from a parent that has initialised HIP is not
 supported.  A `send_fd` travels to the spawned workers as a socket object (its
-descriptor is duplicated into the child by multiprocessing's resource sharer).  The
-pools are started and warmed (HIP initialised in every worker) before the clock starts,
-so the printed throughput times the sends, as the reference's forked workers did.
+descriptor is duplicated into the child by multiprocessing's resource sharer).  Timing:
+the reference starts its clock before `Pool(process_num)` (communicator.py:45-47,
+95-97), so its printed time includes starting forked workers.  A spawned worker costs
+far more to start (interpreter, imports, HIP initialisation), so the process fan-outs
+print two lines: the reference's line over the reference's timed region (pool start-up
+included, comparable with the reference's output), then the same figures for the sends
+alone, timed after every worker is started and warm.
 """
 from __future__ import annotations
 
@@ -84,11 +88,16 @@ def _slices(process_num, data):
         offset += per * TENSOR_NUM_PER_PACKET
 
 
-def _report(process_num, data, start):
+def _report(process_num, data, start, sends_start=None):
+    """The reference's line (communicator.py:65); with sends_start, a second line for the
+    sends alone (the spawned pool's start-up excluded)."""
     end = time.time()
     data_size = data.nbytes / 1e9
     print("{} processes cost: {} sec; Throuthput {} GBps".format(
         process_num, end - start, data_size / max(end - start, 1e-12)))
+    if sends_start is not None:
+        print("{} processes, sends only (pool started and warm): {} sec; Throughput {} GBps".format(
+            process_num, end - sends_start, data_size / max(end - sends_start, 1e-12)))
 
 
 _SPAWN = multiprocessing.get_context("spawn")    # never fork a HIP-initialised parent
@@ -137,10 +146,11 @@ def _warm_pool_args(process_num):
 
 def multi_process_send(process_num, data):
     sock = _shared_socket()
+    start = time.time()                               # the reference's clock: before Pool()
     try:
         with _SPAWN.Pool(process_num, **_warm_pool_args(process_num)) as pool:
             pool.map(_noop, range(process_num), chunksize=1)   # every worker started and warm
-            start = time.time()
+            sends = time.time()
             rs = [pool.apply_async(_child_send, (sock, s, n, ip2int(dst_ip_str), 0, 0, off))
                   for s, n, off in _slices(process_num, data)]
             for r in rs:
@@ -148,7 +158,7 @@ def multi_process_send(process_num, data):
     finally:
         if sock is not None:
             sock.close()
-    _report(process_num, data, start)
+    _report(process_num, data, start, sends)
 
 
 def multi_thread_send_futures(process_num, data):
@@ -163,13 +173,14 @@ def multi_thread_send_futures(process_num, data):
 
 def multi_process_send_futures_P(process_num, data):
     sock = _shared_socket()
+    start = time.time()                               # the reference's clock: before the pool
     try:
         # process_num workers (one per slice; the reference's default pool size only adds
-        # idle processes), started and warmed before the clock starts
+        # idle processes), started and warmed before the sends' clock starts
         with ProcessPoolExecutor(max_workers=process_num, mp_context=_SPAWN,
                                  **_warm_pool_args(process_num)) as ex:
             list(ex.map(_noop, range(process_num)))
-            start = time.time()
+            sends = time.time()
             fs = [ex.submit(_child_send, sock, s, n, ip2int(dst_ip_str), 0, 0, off)
                   for s, n, off in _slices(process_num, data)]
             for f in fs:
@@ -177,7 +188,7 @@ def multi_process_send_futures_P(process_num, data):
     finally:
         if sock is not None:
             sock.close()
-    _report(process_num, data, start)
+    _report(process_num, data, start, sends)
 
 
 class myThread(threading.Thread):   # communicator.py:120-131

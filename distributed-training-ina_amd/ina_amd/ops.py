@@ -18,6 +18,7 @@ These are the kernels that replace the reference's CPU / switch arithmetic:
 from __future__ import annotations
 
 import ctypes as C
+import numbers
 
 import torch
 
@@ -272,6 +273,18 @@ def ps_apply(local: torch.Tensor, sum_int: torch.Tensor, k: int, weight_step: fl
 
 
 # -- packets -----------------------------------------------------------------------------------
+def _ack_desc_arg(ack_desc, acks):
+    """The ack rows' descriptor output of process_apply / run_apply: a device pointer or None."""
+    if ack_desc is None:
+        return None
+    if acks is None:
+        raise ValueError("ack_desc needs acks")
+    _req(ack_desc, torch.int64, "ack_desc")
+    _fits(ack_desc, acks.shape[0], "ack_desc")
+    _same_device(acks, ack_desc)
+    return ack_desc.data_ptr()
+
+
 def _desc_arg(desc, npk, dev):
     """Descriptor output/input: True -> a new int64 [npk] tensor; a tensor -> checked."""
     if desc is None or desc is False:
@@ -364,7 +377,7 @@ def quantize_pack_nga_multi(xs, k: int, V: int, bitmaps, count: int, switch_id: 
             raise ValueError("base and xs differ in length")
         _same_device(xs[0], base)
     bitmaps = list(bitmaps)
-    seqs = [int(seq0)] * W if isinstance(seq0, int) else list(seq0)
+    seqs = [int(seq0)] * W if isinstance(seq0, numbers.Integral) else list(seq0)
     if len(bitmaps) != W or len(seqs) != W:
         raise ValueError("one bitmap and one seq0 per worker")
     stride = stride or nga_stride(V)
@@ -402,7 +415,7 @@ def make_descriptors(n_packets: int, W: int, count: int, switch_id: int, seq0,
     (no overflow bits) -- a switch's sort() can take them before the payload exists.
     seq0: one int for every worker or one per worker.  Returns the W tensors."""
     W = int(W)
-    seqs = [int(seq0)] * W if isinstance(seq0, int) else list(seq0)
+    seqs = [int(seq0)] * W if isinstance(seq0, numbers.Integral) else list(seq0)
     if len(seqs) != W or not 1 <= W <= _lib.MAX_WORKERS:
         raise ValueError("one seq0 per worker, 1..64 workers")
     if outs is None:
@@ -578,6 +591,25 @@ class Switch:
                                        self.regs.data_ptr())
         self._scratch = None
         self._sorted = None        # (batch, scratch) of a sort() awaiting its run()
+        # the scratch (key / id arrays, epochs, run table) is reused by every call: an event
+        # recorded after each call, waited on by the next call's stream when that stream
+        # differs, so a sort queued on a side stream never overwrites what a run on the main
+        # stream still reads (and a run never starts before its side-stream sort)
+        self._done = None
+        self._done_stream = None
+        self._sorted_desc = None
+
+    def _begin(self, ts: torch.cuda.Stream) -> int:
+        """Orders this call after the previous call on the scratch; returns ts's handle."""
+        if self._done is not None and self._done_stream != ts.cuda_stream:
+            ts.wait_event(self._done)
+        return ts.cuda_stream
+
+    def _end(self, ts: torch.cuda.Stream) -> None:
+        if self._done is None:
+            self._done = torch.cuda.Event()
+        self._done.record(ts)
+        self._done_stream = ts.cuda_stream
 
     def process(self, pkts: torch.Tensor, actions: torch.Tensor | None = None,
                 desc: torch.Tensor | None = None) -> torch.Tensor:
@@ -597,11 +629,26 @@ class Switch:
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
         self._sorted = None                       # the scratch is reused below
+        ts = torch.cuda.current_stream(pkts.device)
+        st = self._begin(ts)
         check(load().ina_switch_process_desc(C.byref(self._state), pkts.data_ptr(), npk, stride,
                                              d.data_ptr() if d is not None else None,
                                              actions.data_ptr(), self._scratch.data_ptr(),
-                                             _stream(pkts)), "switch_process")
+                                             st), "switch_process")
+        self._end(ts)
         return actions
+
+    def batch_path(self, npk: int) -> str:
+        """Which slot-sort path the last call over this switch's scratch took for its batch of
+        npk packets (chunk + bucket sort batches only): "in_order" (no sort), "runs" (dense
+        ascending runs, no sort) or "sorted".  Synchronises the device (a diagnostic)."""
+        if self._scratch is None:
+            raise ValueError("no batch has run on this switch")
+        torch.cuda.synchronize(self._scratch.device)
+        p = C.c_int(0)
+        check(load().ina_switch_batch_path(self._scratch.data_ptr(), npk, self.num_slots, C.byref(p)),
+              "switch_batch_path")
+        return {1: "in_order", 2: "runs", 3: "sorted"}[p.value]
 
     def _scratch_for(self, npk, dev):
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
@@ -614,8 +661,10 @@ class Switch:
         """The slot sort of process(pkts, desc=desc) alone (ina_switch_sort_desc): it reads
         only the descriptors, so it may be queued before -- or on `stream`, beside -- the
         kernels still filling pkts' payload; run() / run_apply() finish the batch over the
-        same scratch (order them after it; the scratch is this switch's, one batch at a time).
-        Returns the actions tensor to hand to run()."""
+        same scratch (the scratch is this switch's, one batch at a time).  Every call on this
+        switch records an event that the next call's stream waits on when the streams
+        differ, so a sort on a side stream starts after the previous run and run() after its
+        sort without the caller ordering them.  Returns the actions tensor to hand to run()."""
         _req(pkts, torch.uint8, "pkts")
         npk, stride = pkts.shape
         d = _desc_arg(desc, npk, pkts.device)
@@ -626,13 +675,29 @@ class Switch:
         _fits(actions, npk, "actions")
         _same_device(pkts, actions)
         scratch = self._scratch_for(npk, pkts.device)
-        st = stream.cuda_stream if stream is not None else _stream(pkts)
+        ts = stream if stream is not None else torch.cuda.current_stream(pkts.device)
         if stream is not None:
             scratch.record_stream(stream)        # in use there until run() joins it
+        st = self._begin(ts)
         check(load().ina_switch_sort_desc(C.byref(self._state), pkts.data_ptr(), npk, stride, d.data_ptr(),
                                           actions.data_ptr(), scratch.data_ptr(), st), "switch_sort")
+        self._end(ts)
         self._sorted = (pkts.data_ptr(), npk, stride, actions.data_ptr(), scratch.data_ptr())
+        self._sorted_desc = d
         return actions
+
+    def check_sorted_desc(self, pkts: torch.Tensor) -> None:
+        """Optional guard for the two-phase switch: the descriptors sort() ordered the batch
+        by (typically made from the header parameters by make_descriptors) must equal the
+        packed headers' bytes 4..11 (nga_descriptors).  A mismatch (wrong seq0, num_slots,
+        count or switch id) would aggregate into the wrong slots silently, so it raises
+        ValueError.  Call between sort() and run(); synchronises the device."""
+        if self._sorted is None:
+            raise ValueError("check_sorted_desc() needs a sort() awaiting its run()")
+        got = nga_descriptors(pkts)
+        if not torch.equal(got, self._sorted_desc[: got.numel()]):
+            bad = int((got != self._sorted_desc[: got.numel()]).nonzero()[0])
+            raise ValueError(f"sort() descriptors disagree with the packed headers (first at packet {bad})")
 
     def _take_sorted(self, pkts, actions):
         # the run reads the sort's scratch as it stands: a run without its own sort (or for
@@ -653,14 +718,18 @@ class Switch:
         _fits(actions, npk, "actions")
         _same_device(pkts, actions)
         scratch = self._take_sorted(pkts, actions)
+        ts = torch.cuda.current_stream(pkts.device)
+        st = self._begin(ts)
         check(load().ina_switch_run_sorted(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                           actions.data_ptr(), scratch.data_ptr(), _stream(pkts)),
+                                           actions.data_ptr(), scratch.data_ptr(), st),
               "switch_run_sorted")
+        self._end(ts)
         return actions
 
     def run_apply(self, pkts: torch.Tensor, actions: torch.Tensor, seq0: int, local: torch.Tensor,
                   k: int, weight_step: float, out: torch.Tensor | None = None,
-                  acks: torch.Tensor | None = None, keep_forwarded: bool = True):
+                  acks: torch.Tensor | None = None, keep_forwarded: bool = True,
+                  ack_desc: torch.Tensor | None = None):
         """Second phase of process_apply() after sort().  Returns (actions, out)."""
         _req(pkts, torch.uint8, "pkts")
         _req(local, torch.float32, "local")
@@ -670,22 +739,29 @@ class Switch:
         _fits(out, local.numel())
         _check_apply(pkts, actions, self.V, local, out, acks)
         ack_ptr, ack_stride = (acks.data_ptr(), acks.shape[1]) if acks is not None else (None, 0)
+        ad = _ack_desc_arg(ack_desc, acks)
         scratch = self._take_sorted(pkts, actions)
-        check(load().ina_switch_run_sorted_apply(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                                 actions.data_ptr(), scratch.data_ptr(), seq0 & 0xFFFFFFFF,
-                                                 local.data_ptr(), k, weight_step, out.data_ptr(),
-                                                 local.numel(), ack_ptr, ack_stride, int(keep_forwarded),
-                                                 _stream(pkts)), "switch_run_sorted_apply")
+        ts = torch.cuda.current_stream(pkts.device)
+        st = self._begin(ts)
+        check(load().ina_switch_run_sorted_apply_ackdesc(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                                         actions.data_ptr(), scratch.data_ptr(),
+                                                         seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
+                                                         out.data_ptr(), local.numel(), ack_ptr, ack_stride,
+                                                         ad, int(keep_forwarded), st),
+              "switch_run_sorted_apply")
+        self._end(ts)
         return actions, out
 
     def process_apply(self, pkts: torch.Tensor, seq0: int, local: torch.Tensor, k: int,
                       weight_step: float, out: torch.Tensor | None = None,
                       acks: torch.Tensor | None = None, keep_forwarded: bool = True,
-                      actions: torch.Tensor | None = None, desc: torch.Tensor | None = None):
+                      actions: torch.Tensor | None = None, desc: torch.Tensor | None = None,
+                      ack_desc: torch.Tensor | None = None):
         """process() + apply_completed() in one pass (the PS on the switch's GPU): completed
         slots update out = local + weight_step * sum * 2^-k and write their PS ack rows.
         keep_forwarded=False leaves completed packets as they arrived (consumed here).
-        Returns (actions, out)."""
+        ack_desc (int64 [ack rows]): also written beside every ack row -- its descriptor, as
+        nga_descriptors(acks) would give -- for the next batch's sort.  Returns (actions, out)."""
         _req(pkts, torch.uint8, "pkts")
         _req(local, torch.float32, "local")
         npk, stride = pkts.shape
@@ -702,13 +778,17 @@ class Switch:
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
         self._sorted = None
-        check(load().ina_switch_process_apply_desc(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                              d.data_ptr() if d is not None else None,
-                                              actions.data_ptr(), self._scratch.data_ptr(),
-                                              seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
-                                              out.data_ptr(), local.numel(), ack_ptr, ack_stride,
-                                              int(keep_forwarded), _stream(pkts)),
+        ts = torch.cuda.current_stream(pkts.device)
+        st = self._begin(ts)
+        ad = _ack_desc_arg(ack_desc, acks)
+        check(load().ina_switch_process_apply_ackdesc(C.byref(self._state), pkts.data_ptr(), npk, stride,
+                                                      d.data_ptr() if d is not None else None,
+                                                      actions.data_ptr(), self._scratch.data_ptr(),
+                                                      seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
+                                                      out.data_ptr(), local.numel(), ack_ptr, ack_stride,
+                                                      ad, int(keep_forwarded), st),
               "switch_process_apply")
+        self._end(ts)
         return actions, out
 
 
@@ -747,7 +827,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                switch_window: int | None = None, switch_ack_fast: bool | None = None,
                switch_sort: int | None = None, switch_sort_rounds: int | None = None,
                ew_blocks: int | None = None, switch_tiny_max: int | None = None,
-               host_zero_copy: bool | None = None, switch_bucket_tile: int | None = None):
+               host_zero_copy: bool | None = None, switch_bucket_tile: int | None = None,
+               switch_runs: bool | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -769,7 +850,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     sum_reduce_host reduce pinned, device-mapped host buffers in place over PCIe (True,
     the default) instead of through the chunked copy pipeline; switch_bucket_tile the slot
     sort's bucket tile in 64-item rounds per wave (0 = auto: 8 when the average bucket
-    exceeds 3,584 packets, else 4; or 4, 8); unroll is the
+    exceeds 3,584 packets, else 4; or 4, 8); switch_runs lets batches of at most 64 runs of
+    consecutive slots (worker-major arrival, PS acks in front) skip the slot sort (True, the
+    default; False always sorts); unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
@@ -802,6 +885,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(16, int(bool(host_zero_copy))), "set_tuning")
     if switch_bucket_tile is not None:
         check(lib.ina_set_tuning(17, int(switch_bucket_tile)), "set_tuning")
+    if switch_runs is not None:
+        check(lib.ina_set_tuning(18, int(bool(switch_runs))), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

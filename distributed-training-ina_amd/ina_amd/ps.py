@@ -14,7 +14,12 @@ and meaning of launch.py:42-52 (sync: weight 1/(W+1)) and launch_async.py:42-57
                          deltas' absmax (ops.scale_for_workers).
 
 Worker.updated_paras may be CPU tensors (unpickled from the worker socket,
-worker.py:78) or device tensors; CPU ones are staged through pinned memory.
+worker.py:78) or device tensors; CPU ones are staged through pinned memory.  The global
+model may live on the GPU or -- as launch.py:38,207 leaves it when the PS sees no GPU of
+its own -- on the CPU: its parameters are then staged to the aggregating GPU (`device`,
+default the current one) through pinned memory, the same kernel runs, and the result is
+written back into the CPU parameters.  There is no CPU compute path: without a GPU the
+call raises.
 communication_parallel (launch.py:111-130) and the TCP framing helpers
 (trans.py:43-54, worker.py:63-79) are kept with the reference's wire format.
 """
@@ -47,11 +52,17 @@ def _staged(t: torch.Tensor, dev: torch.device) -> torch.Tensor:
 
 
 def aggregate(global_model, worker_list, step_size, worker_num: int | None = None,
-              mode: str = "fp32", k: int | str = 16):
-    dev = _device_of(global_model)
-    if dev.type != "cuda":
-        raise ValueError("aggregate: global_model must live on the GPU (global_model.to('cuda'))")
+              mode: str = "fp32", k: int | str = 16, device: str | torch.device | None = None):
+    home = _device_of(global_model)
+    if home.type == "cuda":
+        dev = home
+    else:                                            # a CPU model: aggregate on a GPU
+        if not torch.cuda.is_available():
+            raise ValueError("aggregate: no GPU to aggregate on (the INA path has no CPU fallback)")
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     local = torch.nn.utils.parameters_to_vector(global_model.parameters()).detach()
+    if home.type != "cuda":
+        local = _staged(local, dev)
     if worker_num is not None:                       # launch_async.py:45-47
         weight = 1.0 / worker_num
         worker_list = worker_list[:worker_num]
@@ -65,6 +76,10 @@ def aggregate(global_model, worker_list, step_size, worker_num: int | None = Non
         out = combine_ina(local, paras, k, ws)
     else:
         raise ValueError(f"unknown mode {mode!r}")
+    if home.type != "cuda":                          # back into the CPU parameters
+        host = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+        host.copy_(out)                              # synchronous: the update is complete
+        out = host
     torch.nn.utils.vector_to_parameters(out, global_model.parameters())
     return out
 

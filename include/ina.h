@@ -77,7 +77,9 @@ const char* ina_last_error_string(void);
  * one-workgroup path, so it is capped by key 9's threshold), 16 host reduce on pinned
  * device-mapped buffers in place over PCIe (1, default) or through the chunked copy
  * pipeline (0), 17 the slot sort's bucket tile in 64-item rounds per wave (0 auto: 8 when
- * the average bucket exceeds 3,584 packets, else 4; or 4, 8).
+ * the average bucket exceeds 3,584 packets, else 4; or 4, 8), 18 switch batches made of at
+ * most 64 runs of consecutive slots (worker-major arrival, PS acks in front) skip the slot
+ * sort and run from a table of the runs (1, default; 0 = always sort).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 
@@ -290,6 +292,17 @@ int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, s
                                   void* scratch, uint32_t seq0, const float* local, int k,
                                   double weight_step, float* out, size_t n, uint8_t* acks,
                                   size_t ack_stride, int keep_forwarded, ina_stream_t stream);
+/* The same with the ack rows' descriptors written beside them: ack_desc[slot] = bytes 4..11
+ * of ack row `slot` (ina_nga_descriptors' format) for every row the call writes, so the
+ * next batch -- these acks in front of the next step's packets -- is sorted from
+ * descriptors without a gather pass over the ack rows.  ack_desc needs acks (8-byte
+ * aligned, one entry per row). */
+int ina_switch_process_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
+                                     size_t stride, const ina_nga_desc_t* desc, uint8_t* actions,
+                                     void* scratch, uint32_t seq0, const float* local, int k,
+                                     double weight_step, float* out, size_t n, uint8_t* acks,
+                                     size_t ack_stride, ina_nga_desc_t* ack_desc, int keep_forwarded,
+                                     ina_stream_t stream);
 /* The same calls in two phases.  With descriptors the slot sort reads nothing but them, so
  * it can be queued as soon as they exist -- before, or on another stream beside, the
  * kernels that still fill the packets' payload (descriptors from the header parameters
@@ -309,6 +322,19 @@ int ina_switch_run_sorted_apply(const ina_switch_state_t* st, uint8_t* pkts, siz
                                 uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
                                 double weight_step, float* out, size_t n, uint8_t* acks,
                                 size_t ack_stride, int keep_forwarded, ina_stream_t stream);
+int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
+                                        size_t stride, uint8_t* actions, void* scratch, uint32_t seq0,
+                                        const float* local, int k, double weight_step, float* out,
+                                        size_t n, uint8_t* acks, size_t ack_stride,
+                                        ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream);
+
+/* Diagnostic: which slot-sort path the last chunk + bucket sort over `scratch` took (a batch
+ * of npkts packets, pools of < 2^18 slots, more than 768 packets; the small-batch paths and
+ * the digit passes do not record one).  Synchronous (reads 12 bytes of the scratch). */
+#define INA_PATH_IN_ORDER 1   /* already in slot order: no sort */
+#define INA_PATH_RUNS 2       /* at most 64 runs of consecutive slots: a run table, no sort */
+#define INA_PATH_SORTED 3     /* the bucket sort */
+int ina_switch_batch_path(const void* scratch, size_t npkts, uint32_t num_slots, int* path);
 
 /* ---- ipRoute (ngaa.p4:39-61, entries as bfrt/setup.py:85-95 installs them) -------
  * Every packet the ingress does not drop (actions FWD_AGG, FWD_COLLISION, FWD_ACK,

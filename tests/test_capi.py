@@ -158,6 +158,11 @@ def _einval_cases():
         "ina_absmax_f32": (None, None, 64, None, None),
         "ina_absmax_multi_f32": (P([None, None]), 2, None, 64, None, None),
         "ina_sum_reduce_host_i32": (P([None, None]), 2, None, 64, 0, None, None),
+        "ina_switch_batch_path": (None, 2048, 16384, None),
+        "ina_switch_process_apply_ackdesc": (ctypes.byref(st), None, 2, 144, None, None, None, 1, None, 16,
+                                             0.5, None, 64, None, 144, None, 1, None),
+        "ina_switch_run_sorted_apply_ackdesc": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
+                                                None, 64, None, 144, None, 1, None),
     }
 
 

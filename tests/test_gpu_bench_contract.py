@@ -44,6 +44,12 @@ def test_bench_json_line_contract():
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert rf["algorithmic_bytes_per_launch"] == 9 * 26_214_400 * 4
+    src = rf["traffic_source"]                  # where `traffic` came from, or why it is null
+    assert src["file"].endswith(".json")
+    if rf["traffic"] is not None:
+        assert src["matches_kernel_and_size"] is True and src["session"]
+        assert "k_sum_reduce_i32_vec<8, 4, true>" in src["kernel"] or "k_sum_reduce_i32_vec<8,4,true>" in src["kernel"]
+    assert "every 997th over the whole bucket" in d["parity_sample"]
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["value"] > 0
     aff = len(os.sched_getaffinity(0))
@@ -77,9 +83,11 @@ def test_bench_json_line_contract():
         assert all(p["frac"] > 0 for p in r["hbm_phases"].values())   # 16 MiB: may replay from MALL
     sw = d["switch_c3"]                          # the packet-stream switch, measured live
     assert sw["algorithmic_bytes"] == 819_200 * 1040 + 102_400 * (1040 + 1029) + 819_200
-    for order in ("worker_major", "round_robin"):
+    paths = {"worker_major": "runs", "round_robin": "in_order", "worker_major_sorted": "sorted",
+             "shuffled": "sorted"}
+    for order, path in paths.items():
         assert sw[order]["ok"] is True and sw[order]["slots_completed"] == 102_400
-        assert 0 < sw[order]["frac"] < 1
+        assert 0 < sw[order]["frac"] < 1 and sw[order]["batch_path"] == path, order
     pp = d["packet_path"]                        # the whole INA step, PS fused, steady state
     assert pp["parity_spot_check"] is True and pp["value"] > 0 and pp["ms_per_step"] > 0
     assert pp["roofline"]["bound"] == "hbm" and 0 < pp["roofline"]["frac"] < 1

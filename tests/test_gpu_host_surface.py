@@ -119,6 +119,32 @@ def test_aggregate_fp32_matches_reference_outputs():
         assert np.array_equal(got.view(np.uint32), c["out"].view(np.uint32)), name
 
 
+@pytest.mark.parametrize("mode", ["fp32", "ina"])
+def test_aggregate_cpu_model_matches_reference_outputs(mode):
+    """A PS whose global model stays on the CPU (launch.py:38,207 moves it to cuda only when
+    it sees a GPU): aggregate() stages it through pinned memory, runs the same kernel and
+    writes the CPU parameters back -- bit-exact against the reference's own aggregate()
+    outputs (fp32), and equal to the same call on a GPU model (ina mode)."""
+    from ina_amd import ps
+    for name, c in ps_cases().items():
+        W, K = int(c["W"]), int(c["K"])
+        cpu_model = _model_with(c["local"]).cpu()
+        assert next(cpu_model.parameters()).device.type == "cpu"
+        wl = [_Wk(torch.from_numpy(p)) for p in c["paras"]]
+        with torch.no_grad():
+            ps.aggregate(cpu_model, wl, float(c["step"]), None if K < 0 else K, mode=mode)
+        got = torch.nn.utils.parameters_to_vector(cpu_model.parameters()).detach().numpy()
+        assert next(cpu_model.parameters()).device.type == "cpu"
+        if mode == "fp32":
+            want = c["out"]
+        else:
+            gpu_model = _model_with(c["local"])
+            with torch.no_grad():
+                ps.aggregate(gpu_model, wl, float(c["step"]), None if K < 0 else K, mode=mode)
+            want = torch.nn.utils.parameters_to_vector(gpu_model.parameters()).detach().cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), name
+
+
 def test_aggregate_ina_mode_matches_oracle():
     from ina_amd import ps
     rng = np.random.default_rng(4)

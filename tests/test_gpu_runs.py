@@ -1,0 +1,332 @@
+"""GPU parity of the switch's dense-run path (csrc/ina_switch.hip, kRunsMax): a batch made of
+at most 64 runs of consecutive slots -- worker-major arrival, the PS's acks in front --
+skips the slot sort and runs each slot's segment from a table of the runs.  Slots are
+independent and keep arrival order (ngaa.p4:87-168, 120-196), so every result must equal
+the oracle's P4 restatement packet for packet: actions, rewritten packets and the switch
+registers after every batch.  65 runs, gapped runs and shuffled batches take the sort.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+POOL = 1 << 17
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ina_amd import ops  # noqa: F401  (fails loudly if libina.so is missing)
+
+
+def ops():
+    from ina_amd import ops as o
+    return o
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def runs_batch(rng, V, specs, W, stride, num_slots=POOL, collide=0.02, degree_mix=0.02):
+    """Packets for `specs` in arrival order: (seq0, length, kind), kind = worker index w
+    (bitmap w + 1), "ack" (PS acks, flag 0x40) or "foreign" (switch id 2).  Each spec is one
+    pack: packet p has frag_id = seq0 + p and index = (seq0 + p) % num_slots, so a spec is
+    one dense run unless its slots wrap the pool.  A few packets get another frag id
+    (collisions) or another degree."""
+    parts = []
+    for seq0, ln, kind in specs:
+        vals = rng.integers(-2**31, 2**31, size=ln * V, dtype=np.int64).astype(np.int32)
+        if kind == "ack":
+            p = orc.pack_nga(vals, V, 0, W, 1, seq0, flags=orc.FLAG_ACK, num_slots=num_slots, stride=stride)
+        elif kind == "foreign":
+            p = orc.pack_nga(vals, V, 1, W, 2, seq0, num_slots=num_slots, stride=stride)
+        else:
+            p = orc.pack_nga(vals, V, int(kind) + 1, W, 1, seq0, num_slots=num_slots, stride=stride)
+        parts.append(p)
+    pk = np.concatenate(parts)
+    n = len(pk)
+    for i in np.flatnonzero(rng.random(n) < collide):
+        f = int.from_bytes(pk[i, 11:15].tobytes(), "big") + 1
+        pk[i, 11:15] = np.frombuffer((f & 0xFFFFFFFF).to_bytes(4, "big"), np.uint8)
+    for i in np.flatnonzero(rng.random(n) < degree_mix):
+        pk[i, 4] = int(rng.choice([1, 2]))
+    return pk
+
+
+def check_batches(o, V, batches, want_path, use_desc=True, write_dropped=True, num_slots=POOL):
+    """Every batch through a fresh device switch and the oracle (state carried across the
+    batches): bit-exact actions, packets and registers, and the slot-sort path taken."""
+    stride = batches[0].shape[1]
+    sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=write_dropped)
+    sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+    for i, stream in enumerate(batches):
+        want_pk, want_act = sw_orc.run(stream, stride=stride)
+        d = dev(stream)
+        act = sw_dev.process(d, desc=o.nga_descriptors(d) if use_desc else None)
+        assert np.array_equal(host(act), want_act), i
+        got = host(d)
+        if write_dropped:
+            assert np.array_equal(got, want_pk), i
+        else:
+            fwd = want_act != orc.ACT_DROP
+            assert np.array_equal(got[fwd], want_pk[fwd]), i
+        if want_path is not None:
+            assert sw_dev.batch_path(len(stream)) == want_path, i
+        cnt, frag, regs = sw_orc.registers()
+        assert np.array_equal(host(sw_dev.count), cnt), i
+        assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag), i
+        assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs), i
+
+
+def worker_major(W, per, seq0=1, acks=False):
+    specs = [(seq0, per, "ack")] if acks else []
+    return specs + [(seq0, per, w) for w in range(W)]
+
+
+@pytest.mark.parametrize("V", [32, 256])
+@pytest.mark.parametrize("R", [1, 2, 9, 64, 65])
+def test_dense_runs_vs_oracle(R, V):
+    """R worker runs over the same slots (R = 9: 8 workers behind an ack run).  R <= 64 takes
+    the run table (R = 1 is already in slot order), 65 runs take the bucket sort."""
+    o = ops()
+    rng = np.random.default_rng(100 * R + V)
+    stride = o.nga_stride(V)
+    per = max(3000 // R + 1, 40)
+    specs = worker_major(8, per, acks=True) if R == 9 else [(5, per, w) for w in range(R)]
+    batches = [runs_batch(rng, V, specs, min(R, 255), stride) for _ in range(3)]
+    assert len(batches[0]) > 2048
+    path = "in_order" if R == 1 else "runs" if R <= 64 else "sorted"
+    check_batches(o, V, batches, path)
+
+
+@pytest.mark.parametrize("rounds", [0, 16])
+@pytest.mark.parametrize("at", ["in_round", "round_edge", "wave_edge", "chunk_edge", "last"])
+def test_run_breaks_at_sort_edges(at, rounds):
+    """Two runs whose boundary (a descent) falls inside a 64-packet round, on a round, wave
+    (4 rounds) or chunk (4,096 packets) edge of the chunk pass, or at the last packet: the
+    break is found by the DPP predecessor, the previous round's lane 63 or the loaded
+    predecessor of the wave -- and recorded in the right chunk."""
+    o = ops()
+    rng = np.random.default_rng(7 + len(at) + rounds)
+    V = 32
+    n = 9000
+    cut = {"in_round": 4096 + 70, "round_edge": 4096 + 128, "wave_edge": 4096 + 256,
+           "chunk_edge": 4096, "last": n - 1}[at]
+    specs = [(1000, cut, 0), (1000, n - cut, 1)]
+    o.set_tuning(switch_sort_rounds=rounds)
+    try:
+        batches = [runs_batch(rng, V, specs, 2, o.nga_stride(V)) for _ in range(2)]
+        check_batches(o, V, batches, "runs")
+    finally:
+        o.set_tuning(switch_sort_rounds=0)
+
+
+@pytest.mark.parametrize("case", ["acks_in_front", "lone_acks", "acks_behind", "foreign_mid_run",
+                                  "pool_wrap", "few_gaps", "many_gaps", "shuffled", "ack_fast_off",
+                                  "generic_kernel"])
+def test_run_batches_vs_oracle(case):
+    """Structured batches around the run table: acks leading a segment (read-free) and alone
+    in it (frag cleared only), acks behind the workers (the state machine reads them),
+    foreign packets in the middle of a run (their own runs, skipped), a pool wrap inside the
+    runs (a run breaks at slot 0), a few lost packets (more, shorter runs), many lost packets
+    and a shuffled batch (> 64 breaks: the bucket sort), keys without the ack bit (tuning
+    key 11 off: every ack is read), and V = 33 (the generic LDS-staged run kernel, which
+    reads the bucket sort's arrays, so its batches are sorted)."""
+    o = ops()
+    rng = np.random.default_rng(len(case) * 31)
+    V, W, per = (33 if case == "generic_kernel" else 64), 8, 500
+    stride = o.nga_stride(V)
+    path = "runs"
+    specs = worker_major(W, per, seq0=10, acks=True)
+    if case == "lone_acks":            # acks for 0..599, workers for 300..799
+        specs = [(10, 600, "ack")] + [(310, per, w) for w in range(W)]
+    elif case == "acks_behind":
+        specs = worker_major(W, per, seq0=10) + [(10, per, "ack")]
+    elif case == "pool_wrap":
+        specs = worker_major(W, per, seq0=POOL - 200, acks=True)
+    batches = []
+    for _ in range(2):
+        b = runs_batch(rng, V, specs, W, stride)
+        if case == "foreign_mid_run":   # 3 foreign packets inside worker 3's run
+            f = runs_batch(rng, V, [(77, 3, "foreign")], W, stride, collide=0)
+            at = per * 4 + per // 2
+            b = np.concatenate([b[:at], f, b[at:]])
+        elif case == "few_gaps":        # 5 packets lost: 5 more runs
+            b = np.delete(b, rng.choice(len(b), 5, replace=False), axis=0)
+        elif case == "many_gaps":       # every 7th packet lost: > 64 breaks
+            b = np.delete(b, np.arange(3, len(b), 7), axis=0)
+            path = "sorted"
+        elif case == "shuffled":
+            b = b[rng.permutation(len(b))]
+            path = "sorted"
+        batches.append(b)
+    if case == "generic_kernel":
+        path = "sorted"
+    if case == "ack_fast_off":
+        o.set_tuning(switch_ack_fast=False)
+    try:
+        check_batches(o, V, batches, path)
+    finally:
+        o.set_tuning(switch_ack_fast=True)
+
+
+def test_runs_tuning_off_takes_the_sort():
+    """ina_set_tuning key 18 = 0: the same worker-major batch through the bucket sort --
+    identical results."""
+    o = ops()
+    rng = np.random.default_rng(3)
+    V = 256
+    batches = [runs_batch(rng, V, worker_major(8, 400, acks=True), 8, o.nga_stride(V)) for _ in range(2)]
+    o.set_tuning(switch_runs=False)
+    try:
+        check_batches(o, V, batches, "sorted")
+    finally:
+        o.set_tuning(switch_runs=True)
+    check_batches(o, V, batches, "runs", use_desc=False, write_dropped=False)
+
+
+@pytest.mark.parametrize("V,W,per", [(256, 8, 700), (32, 4, 3000)])
+def test_runs_fused_ps_and_two_phase_equal_sorted(V, W, per):
+    """The packet path's steady state through the run table -- the fused PS apply (one call
+    and two phases: sort, then run), the ack rows' descriptors written by the run kernel
+    (ack_desc) and used as the next step's -- equals the same steps with the run table off
+    (bucket sort, descriptors gathered from the ack rows): actions, PS update bit for bit,
+    ack rows, registers; every ack row's written descriptor equals its header bytes."""
+    o = ops()
+    rng = np.random.default_rng(V + W)
+    n = V * per - 3
+    npk = -(-n // V)
+    stride = o.nga_stride(V)
+    slots = 1 << 13
+    xs = [dev((rng.standard_normal(n) * 1e-2).astype(np.float32)) for _ in range(W)]
+    glob0 = rng.standard_normal(n).astype(np.float32) * 1e-2
+    res = {}
+    try:
+        for mode in ("sorted", "runs", "runs_two_phase"):
+            o.set_tuning(switch_runs=mode != "sorted")
+            glob = dev(glob0.copy())
+            upd = torch.empty_like(glob)
+            big = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=DEV)
+            acks, rows = big[:npk], big[npk:]
+            desc = torch.zeros((W + 1) * npk, dtype=torch.int64, device=DEV)
+            acts = torch.empty((W + 1) * npk, dtype=torch.uint8, device=DEV)
+            wrows = torch.empty((W, npk, stride), dtype=torch.uint8, device=DEV)
+            wdesc = torch.empty((W, npk), dtype=torch.int64, device=DEV)
+            sw = o.Switch(V, num_slots=slots, switch_id=1, device=DEV)
+            steps = []
+            for step in range(3):
+                o.quantize_pack_nga_multi(xs, 16, V, list(range(1, W + 1)), W, 1, 1, base=glob,
+                                          num_slots=slots, outs=list(wrows.unbind(0)),
+                                          descs=list(wdesc.unbind(0)))
+                rows.view(W * npk, stride)[:] = wrows.view(W * npk, stride)
+                if mode == "sorted" or step == 0:
+                    o.nga_descriptors(acks, out=desc[:npk])
+                else:                            # written by the previous step's run kernel
+                    desc[:npk] = adesc
+                desc[npk:] = wdesc.reshape(-1)
+                adesc = torch.zeros(npk, dtype=torch.int64, device=DEV)
+                if mode == "runs_two_phase":
+                    sw.sort(big, desc, actions=acts)
+                    sw.run_apply(big, acts, 1, glob, 16, 1.0 / (W + 1), out=upd, acks=acks,
+                                 keep_forwarded=False, ack_desc=adesc)
+                else:
+                    sw.process_apply(big, 1, glob, 16, 1.0 / (W + 1), out=upd, acks=acks,
+                                     keep_forwarded=False, actions=acts, desc=desc,
+                                     ack_desc=None if mode == "sorted" else adesc)
+                if mode != "sorted":             # the ack rows' descriptors, beside the rows
+                    assert torch.equal(adesc, o.nga_descriptors(acks)), (mode, step)
+                if step:
+                    want = "sorted" if mode == "sorted" else "runs"
+                    assert sw.batch_path((W + 1) * npk) == want, (mode, step)
+                steps.append((host(acts).copy(), host(upd).view(np.uint32).copy(), host(acks).copy()))
+                glob.copy_(upd)
+            res[mode] = (steps, host(sw.count), host(sw.frag), host(sw.regs))
+    finally:
+        o.set_tuning(switch_runs=True)
+    s0, c0, f0, r0 = res["sorted"]
+    for mode in ("runs", "runs_two_phase"):
+        s1, c1, f1, r1 = res[mode]
+        for (a0, u0, k0), (a1, u1, k1) in zip(s0, s1):
+            assert np.array_equal(a0, a1), mode
+            assert np.array_equal(u0, u1), mode
+            assert np.array_equal(k0, k1), mode
+        assert np.array_equal(c0, c1) and np.array_equal(f0, f1) and np.array_equal(r0, r1), mode
+    assert int((s0[2][0] == orc.ACT_FWD_AGG).sum()) == npk
+    assert bool((s0[2][0][:npk] == orc.ACT_FWD_ACK).all())
+
+
+def test_two_phase_orders_itself_across_streams():
+    """sort() on a side stream with no wait_stream by the caller, then run() on the main
+    stream, step after step over the same scratch: the switch's own events order every call
+    after the previous one (a side-stream sort never overwrites the key / id arrays or the
+    run table a pending run still reads).  Equal to one-call process() step by step."""
+    o = ops()
+    rng = np.random.default_rng(11)
+    V, W, per = 256, 8, 600
+    stride = o.nga_stride(V)
+    batches = [runs_batch(rng, V, worker_major(W, per, acks=True), W, stride) for _ in range(4)]
+    batches.append(batches[0][rng.permutation(len(batches[0]))])          # and a sorted one
+    res = {}
+    side = torch.cuda.Stream(DEV)
+    for two in (False, True):
+        sw = o.Switch(V, num_slots=POOL, switch_id=1, device=DEV, write_dropped=True)
+        got = []
+        for b in batches:
+            d = dev(b)
+            desc = o.nga_descriptors(d)
+            torch.cuda.synchronize()
+            if two:
+                acts = torch.empty(len(b), dtype=torch.uint8, device=DEV)
+                with torch.cuda.stream(side):
+                    torch.cuda._sleep(2_000_000)          # the sort is queued late on purpose
+                    sw.sort(d, desc, actions=acts)
+                sw.run(d, acts)
+            else:
+                acts = sw.process(d, desc=desc)
+            got.append((host(acts).copy(), host(d).copy()))
+        res[two] = (got, host(sw.count), host(sw.frag), host(sw.regs))
+    (g0, c0, f0, r0), (g1, c1, f1, r1) = res[False], res[True]
+    for (a0, p0), (a1, p1) in zip(g0, g1):
+        assert np.array_equal(a0, a1) and np.array_equal(p0, p1)
+    assert np.array_equal(c0, c1) and np.array_equal(f0, f1) and np.array_equal(r0, r1)
+
+
+@pytest.mark.parametrize("bad", ["seq0", "num_slots", "count"])
+def test_two_phase_descriptor_mismatch_is_caught(bad):
+    """Descriptors made from header parameters that disagree with the packed headers would
+    aggregate into the wrong slots without an error; check_sorted_desc() compares them with
+    the headers' bytes 4..11 between sort() and run() and raises."""
+    o = ops()
+    V, W, npk = 32, 4, 900
+    slots = 1 << 13
+    stride = o.nga_stride(V)
+    rows = torch.empty((W, npk, stride), dtype=torch.uint8, device=DEV)
+    for w in range(W):
+        o.pack_nga(dev(np.arange(npk * V, dtype=np.int32)), V, w + 1, W, 1, 5, num_slots=slots, out=rows[w])
+    big = rows.view(W * npk, stride)
+    seq0 = 6 if bad == "seq0" else 5
+    ns = 500 if bad == "num_slots" else slots          # indices wrap at 500 instead of 8192
+    count = W + 1 if bad == "count" else W
+    descs = torch.empty((W, npk), dtype=torch.int64, device=DEV)
+    o.make_descriptors(npk, W, count, 1, seq0, num_slots=ns, outs=list(descs.unbind(0)), device=DEV)
+    sw = o.Switch(V, num_slots=slots, switch_id=1, device=DEV)
+    sw.sort(big, descs.view(-1))
+    with pytest.raises(ValueError, match="disagree"):
+        sw.check_sorted_desc(big)
+    good = torch.empty_like(descs)
+    o.make_descriptors(npk, W, W, 1, 5, num_slots=slots, outs=list(good.unbind(0)), device=DEV)
+    acts = sw.sort(big, good.view(-1))
+    sw.check_sorted_desc(big)                           # the matching ones pass
+    sw.run(big, acts)
+    assert int((host(acts) == orc.ACT_FWD_AGG).sum()) == npk

@@ -25,6 +25,11 @@ for st in $STAGES; do
       nm=${st#lab:}
       timeout -k 10 300 python tools/lab/$nm.py > "$OUT/$nm.log" 2>&1
       rc=$?; cat "$OUT/$nm.log"; [ $rc -ne 0 ] && fatal "$st" $rc ;;
+    pfile:*)
+      f=${st#pfile:}
+      timeout -k 10 600 python -u -m pytest tests/$f -m gpu -q -rf --timeout 120 --timeout-method thread \
+        > "$OUT/pfile_${f%.py}.log" 2>&1
+      rc=$?; tail -15 "$OUT/pfile_${f%.py}.log"; ok_or_fail "$st" $rc ;;
     ptest:*)
       timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread \
         -k "${PTEST_K:-${st#ptest:}}" > "$OUT/ptest.log" 2>&1

@@ -28,7 +28,8 @@ def main():
     read_b = 2 * fetch_kib * 1024
     write_b = write_kib * 1024
     algo = (W + 1) * n * 4
-    res = {"kernel": name, "workers": W, "values": n, "dispatches": [nf, nw],
+    res = {"kernel": name, "session": sess.rstrip("/").split("/")[-1] if "/" in sess else sess,
+           "workers": W, "values": n, "dispatches": [nf, nw],
            "FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib,
            "hbm_read_bytes": int(read_b), "hbm_write_bytes": int(write_b),
            "hbm_bytes_per_launch": int(read_b + write_b), "algorithmic_bytes": algo,
