@@ -905,7 +905,7 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
 
 
 # -- the packet-stream switch on config 3 ----------------------------------------
-def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
+def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 17, orders=None):
     """ina_switch_process over config 3 as NGA-256 packets: 8 workers x 102,400 packets
     (2^17-slot pool, keys from the pack kernels' descriptors), in worker-major and in
     round-robin arrival (a NIC interleaving the workers).  HIP events on the launch stream
@@ -916,26 +916,33 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
     At N > 1 every rank runs its own switch on its own bucket (slots are independent,
     ngaa.p4:87-168): `us` is the max over ranks, `aggregate_GBps` all ranks' bytes / that."""
     from ina_amd import ops
-    W, n, V, slots = W_WORKERS, N_VALUES, V_SLOT, 1 << 17
+    W, n = W_WORKERS, N_VALUES
     g = torch.Generator(device=dev)
     g.manual_seed(4242 + rank)
     packed = []
+    npk = -(-n // V)
+    samp = np.unique(np.concatenate([np.arange(0, npk, 997), [npk - 1]]))   # parity sample slots
+    vidx = (samp[:, None] * V + np.arange(V)).ravel()
+    vidx = vidx[vidx < n]
+    want = np.zeros(vidx.size, np.uint32)
     for w in range(W):
-        b = torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
+        b = torch.randint(-(1 << 30), 1 << 30, (n,), dtype=torch.int32, device=dev, generator=g)
+        want += b[torch.from_numpy(vidx).to(dev)].cpu().numpy().view(np.uint32)
         packed.append(ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots, desc=True))
         del b
     stream = torch.cat([p for p, _ in packed])
     desc = torch.cat([d for _, d in packed])
     del packed
+    pristine = stream.clone()                  # the timed calls rewrite packets in place
     npk_all, stride = stream.shape
-    npk = npk_all // W
     sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
     acts = torch.empty(npk_all, dtype=torch.uint8, device=dev)
     algo = npk_all * stride + npk * stride + npk * (4 * V + 5) + npk_all
     s = torch.cuda.current_stream(dev)
-    res = {"workload": "C3 as NGA-256 packets: 8 workers x 102,400 packets (819,200), 2^17-slot "
-                       "pool, keys from descriptors; ina_switch_process incl. its slot sort",
-           "algorithmic_bytes": algo, "ranks": world}
+    res = {"workload": (f"C3 as NGA-{V} packets: {W} workers x {npk:,} packets ({npk_all:,}), "
+                        f"2^{slots.bit_length() - 1}-slot pool, keys from descriptors; ina_switch_process "
+                        f"incl. its slot sort"),
+           "algorithmic_bytes": algo, "ranks": world, "V": V, "stride": stride}
     # worker_major: 8 dense runs of consecutive slots (no sort: the run table); round_robin:
     # already in slot order (no sort); worker_major_sorted: the same worker-major batch with
     # the run table off (tuning key 18 = 0: the chunk + bucket sort); shuffled: a random
@@ -946,6 +953,28 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
              "round_robin": torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1),
              "worker_major_sorted": None,
              "shuffled": torch.randperm(npk_all, device=dev, generator=gperm)}
+    for name in list(order):
+        if orders is not None and name not in orders:
+            del order[name]
+    def parity(perm):
+        """A fresh switch over a pristine copy of the batch in this arrival order: every slot
+        completes exactly once, and each sampled slot's completing packet carries the
+        wrapping int32 sum of the 8 workers' values (big-endian payload at byte 15)."""
+        cp = pristine.clone() if perm is None else pristine[perm]
+        chk = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
+        a = chk.process(cp, desc=desc if perm is None else desc[perm])
+        pos = torch.arange(npk_all, device=dev) if perm is None else torch.argsort(perm)
+        ts = torch.from_numpy(samp).to(dev)
+        cand = torch.stack([pos[w * npk + ts] for w in range(W)])          # [W, samples]
+        fwd = a[cand] == _ACT_FWD_AGG
+        ok = bool(int((a == _ACT_FWD_AGG).sum()) == npk) and bool((fwd.sum(0) == 1).all())
+        at = cand.gather(0, fwd.to(torch.int64).argmax(0, keepdim=True)).reshape(-1)
+        pay = cp[at, 15:15 + 4 * V].contiguous().cpu().numpy().view(">u4").reshape(-1, V)
+        # the last slot may be partial: its values past n are the pack's zero padding
+        got = np.concatenate([pay[i, : min(V, n - int(sl) * V)] for i, sl in enumerate(samp)]).astype(np.uint32)
+        del cp, chk, a
+        return ok and bool(np.array_equal(got, want))
+
     for name, perm in order.items():
         st, ds = (stream, desc) if perm is None else (stream[perm], desc[perm])
         ops.set_tuning(switch_runs=name != "worker_major_sorted")
@@ -979,11 +1008,15 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1):
                      "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
                      "ok": all_ranks_true(done == npk, world), "us_event_pair_per_call": round(us_pair, 2),
                      "batch_path": sw.batch_path(npk_all)}
+        del st, ds
+        res[name]["parity_spot_check"] = all_ranks_true(parity(perm), world)
         ops.set_tuning(switch_runs=True)
         if world > 1:
             res[name]["aggregate_GBps"] = round(world * algo / us / 1e3, 1)
-        del st, ds
-    del stream, desc, sw, acts
+    res["parity_sample"] = (f"{samp.size} slots (every 997th + the last): the completing packet's payload "
+                            f"vs the numpy wrapping sum of the {W} workers' values, on a fresh switch "
+                            f"in each arrival order; every slot completes exactly once")
+    del stream, desc, sw, acts, pristine
     torch.cuda.empty_cache()
     return res
 
@@ -1135,6 +1168,12 @@ def run_reduce(args, rank, world, dev, backend):
             run_leg(c5, "a2a", lambda: measure_c5(args, rank, world, dev, collective="a2a"))
     if not args.no_switch:
         run_leg(line, "switch_c3", lambda: measure_switch(dev, rank=rank, world=world))
+        # the P4 program's own format (headers.p4:40-73, parser.p4:43-55: NGA-32, 32 x bit<32>
+        # behind the 15-byte header) at config-3 size: 6,553,600 packets, a 2^20-slot pool
+        # (keys of 21 bits: the 2,048-bin chunk + bucket sort, and its run / in-order paths)
+        run_leg(line, "switch_c3_v32", lambda: measure_switch(dev, rank=rank, world=world, V=32, slots=1 << 20,
+                                                              orders=("worker_major", "round_robin",
+                                                                      "shuffled")))
         run_leg(line, "packet_path", lambda: measure_packet_path(dev, rank=rank, world=world))
     if cpu_in is not None:
         run_leg(line, "cpu_baseline", lambda: cpu_baseline(args, *cpu_in))

@@ -43,8 +43,10 @@ __device__ __forceinline__ void stream_store(T v, T* p) {
 #if INA_STORE_SC1
     static_assert(sizeof(T) == 16 || sizeof(T) == 8 || sizeof(T) == 4, "16, 8 or 4-byte stores");
     const uint64_t a = (uint64_t)(uintptr_t)p;
-    const uint64_t a0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-                        (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+    // (readfirstlane returns int: each half goes through uint32_t, or the low half's bit 31
+    // would sign-extend into the high half)
+    const uint64_t a0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
     const uint32_t d = (uint32_t)(a - a0);
     __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)a0, 0, 0x7FFFFFFF, kRawBufferWord3);

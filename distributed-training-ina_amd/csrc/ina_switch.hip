@@ -142,16 +142,16 @@ __device__ __forceinline__ void lds_count(uint32_t* h, uint32_t d, bool valid) {
 // LDS first, so each digit leaves as one contiguous run, measured no faster (pass 0
 // 15.1 -> 17.9 us, pass 1 17.9 -> 17.3 us at 819,200 packets: the passes are bound by
 // their dependent phases, not by the scattered stores; profiles/r02/lab/switch_sort_lab)
-template <int R, int NW = kRsWaves>
+template <int R, int NW = kRsWaves, int BINS = kRsBins>
 __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const uint32_t (&v)[R],
                                                 size_t i0, size_t n, int shift, int bits,
-                                                uint32_t (*base)[kRsBins], const uint32_t* gst,
+                                                uint32_t (*base)[BINS], const uint32_t* gst,
                                                 uint32_t* __restrict__ kout,
                                                 uint32_t* __restrict__ vout, int rw = R) {
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const uint32_t nb = 1u << bits;
     constexpr int kThr = NW * 64;
-    constexpr int kDPT = (kRsBins + kThr - 1) / kThr;
+    constexpr int kDPT = (BINS + kThr - 1) / kThr;
 #pragma unroll
     for (int j = 0; j < kDPT; ++j) {
         const uint32_t d = threadIdx.x + (uint32_t)j * kThr;
@@ -597,6 +597,31 @@ __device__ __forceinline__ uint32_t block_digit_scan(uint32_t x, uint32_t* wtot,
     return pre + inc - x;
 }
 
+// The chunk + bucket sort's digits: 512 bins (keys of <= 18 bits: two 9-bit digits) or, for
+// pools of 2^18 .. 2^21 slots (keys of 19-22 bits), 2,048 bins (digits of 10-11 bits; the
+// bucket pass's LDS then holds 16 x 2,048 per-wave counts, 152 KiB of the CU's 160).  With
+// 2,048 bins a thread owns kDigitsPerThread CONSECUTIVE digits d = t * DPT + j, so the
+// block scan of their sums orders them.
+constexpr int kBinsBig = 2048;
+constexpr int kBitsBig = 11;
+template <int BINS>
+constexpr int kDigitsPerThread = BINS > kBkThr ? BINS / kBkThr : 1;
+static_assert(kBinsBig % kBkThr == 0, "whole digits per thread");
+// exclusive positions of the thread's DPT consecutive digits (counts x[]), after `carry`
+template <int DPT>
+__device__ __forceinline__ void block_digit_scan_n(const uint32_t (&x)[DPT], uint32_t (&ex)[DPT],
+                                                   uint32_t* wtot, uint32_t carry) {
+    uint32_t tsum = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) tsum += x[j];
+    uint32_t e = block_digit_scan(tsum, wtot, carry);
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+        ex[j] = e;
+        e += x[j];
+    }
+}
+
 // ---- structured batches: dense ascending runs --------------------------------------------
 // A batch made of a few runs of consecutive slots -- each worker's packets for slots s, s+1,
 // ... (worker-major arrival), the PS's acks for the previous step in front of them -- needs
@@ -617,7 +642,7 @@ constexpr int kRunsStart = 1, kRunsKey = 2 + kRunsMax;
 constexpr int kCtlWords = kCtlRuns + kRunsKey + kRunsMax;
 static_assert(kCtlWords * 4 <= 1024, "control block fits its 1 KiB");
 
-template <int R, bool kDesc>
+template <int R, bool kDesc, int BINS>
 __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restrict__ pkts,
                                                         const uint2* __restrict__ desc, size_t npk,
                                                         size_t stride, uint32_t num_slots, int switch_id,
@@ -628,8 +653,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                                                         uint32_t* __restrict__ unsorted, uint32_t epoch,
                                                         uint32_t* __restrict__ brk_cnt,
                                                         uint2* __restrict__ brk_ent) {
-    __shared__ uint32_t base[kBkWaves][kRsBins];     // per-wave digit counts, then bases
-    __shared__ uint32_t gst[kRsBins];                 // the chunk's run starts (output positions)
+    __shared__ uint32_t base[kBkWaves][BINS];        // per-wave digit counts, then bases
+    __shared__ uint32_t gst[BINS];                    // the chunk's run starts (output positions)
     __shared__ uint32_t wtot[kBkWaves];
     __shared__ uint32_t wbrk[kBkWaves];               // per-wave break counts
     const int lane = threadIdx.x & 63, wv = wave_in_block();
@@ -699,21 +724,31 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
             }
         }
     }
-    // thread d owns digit d: the chunk's count, its chunk-local run start (block scan)
-    const uint32_t d = threadIdx.x;
-    uint32_t tc = 0;
-    if (d < nb) {
+    // thread t owns digits t*DPT .. t*DPT+DPT-1: the chunk's counts, their chunk-local run
+    // starts (block scan)
+    constexpr int DPT = kDigitsPerThread<BINS>;
+    uint32_t tc[DPT], ex[DPT];
 #pragma unroll
-        for (int w = 0; w < kBkWaves; ++w) tc += base[w][d];
+    for (int j = 0; j < DPT; ++j) {
+        const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+        tc[j] = 0;
+        if (d < nb) {
+#pragma unroll
+            for (int w = 0; w < kBkWaves; ++w) tc[j] += base[w][d];
+        }
     }
-    const uint32_t ex = block_digit_scan(tc, wtot, 0u);
-    if (d < nb) {
-        rcnt[(size_t)d * nch + c] = tc;
-        rst[(size_t)d * nch + c] = ex;
-        gst[d] = (uint32_t)(c * (size_t)(kBkThr * R)) + ex;
+    block_digit_scan_n<DPT>(tc, ex, wtot, 0u);
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+        const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+        if (d < nb) {
+            rcnt[(size_t)d * nch + c] = tc[j];
+            rst[(size_t)d * nch + c] = ex[j];
+            gst[d] = (uint32_t)(c * (size_t)(kBkThr * R)) + ex[j];
+        }
     }
     __syncthreads();
-    rs_tile_scatter<R, kBkWaves>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
+    rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
 }
 
 #ifndef INA_BK_TIMING
@@ -749,7 +784,7 @@ __device__ __forceinline__ void bucket_src(const uint32_t* s_dst, const uint32_t
     for (int r = 0; r < R; ++r) src[r] = s_src[lo[r]] + (i[r] - s_dst[lo[r]]);
 }
 
-template <int R>
+template <int R, int BINS>
 __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin,
                                                          uint32_t* __restrict__ kout,
@@ -762,8 +797,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
                                                          const uint32_t* __restrict__ brk_cnt,
                                                          const uint2* __restrict__ brk_ent, uint32_t npk) {
     __shared__ uint32_t s_dst[kBkMaxChunks + 1], s_src[kBkMaxChunks];
-    __shared__ uint32_t base[kBkWaves][kRsBins];
-    __shared__ uint32_t gst[kRsBins];                 // bucket digit counts, then output positions
+    __shared__ uint32_t base[kBkWaves][BINS];
+    __shared__ uint32_t gst[BINS];                    // bucket digit counts, then output positions
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const uint32_t b = blockIdx.x;
@@ -883,8 +918,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
         return;
     }
     const uint32_t nb = 1u << lbits;
-    const uint32_t d = threadIdx.x;                   // thread d owns low digit d
-    if (d < nb) gst[d] = 0;
+    constexpr int DPT = kDigitsPerThread<BINS>;       // thread t owns low digits t*DPT + j
+    for (uint32_t d = threadIdx.x; d < nb; d += kBkThr) gst[d] = 0;
     __syncthreads();
     constexpr uint32_t kTile = (uint32_t)kBkThr * (uint32_t)R;
     const uint32_t ntile = (cnt + kTile - 1) / kTile;
@@ -897,9 +932,18 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
             lds_count(gst, ok ? kin[src[0]] & (nb - 1) : 0u, ok);
         }
         __syncthreads();
-        const uint32_t x = d < nb ? gst[d] : 0u;
-        const uint32_t ex = block_digit_scan(x, red, s0);
-        if (d < nb) gst[d] = ex;
+        uint32_t x[DPT], ex[DPT];
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+            x[j] = d < nb ? gst[d] : 0u;
+        }
+        block_digit_scan_n<DPT>(x, ex, red, s0);
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+            if (d < nb) gst[d] = ex[j];
+        }
     }
     for (uint32_t t = 0; t < ntile; ++t) {
         // the tile's items split evenly over the waves in order (wave w: rw rounds of 64)
@@ -927,24 +971,38 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
             if (r < rw) lds_count(base[wv], k[r] & (nb - 1), i0 + (uint32_t)r * 64u < t_end);
         __syncthreads();
         BK_STAMP(2);
-        uint32_t tc = 0;                              // this tile's count of digit d
-        if (d < nb) {
+        uint32_t tc[DPT];                             // this tile's counts of the thread's digits
 #pragma unroll
-            for (int w = 0; w < kBkWaves; ++w) tc += base[w][d];
+        for (int j = 0; j < DPT; ++j) {
+            const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+            tc[j] = 0;
+            if (d < nb) {
+#pragma unroll
+                for (int w = 0; w < kBkWaves; ++w) tc[j] += base[w][d];
+            }
         }
         if (ntile == 1) {                             // one tile: positions from its own counts
-            const uint32_t ex = block_digit_scan(tc, red, s0);
-            if (d < nb) gst[d] = ex;
+            uint32_t ex[DPT];
+            block_digit_scan_n<DPT>(tc, ex, red, s0);
+#pragma unroll
+            for (int j = 0; j < DPT; ++j) {
+                const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+                if (d < nb) gst[d] = ex[j];
+            }
         }
         __syncthreads();
         BK_STAMP(3);
         // (staging a one-tile bucket's output in LDS to leave as one contiguous run measured
         // no faster: 244.5 -> 244.1 us worker-major, 228.3 -> 229.9 round-robin,
         // profiles/r03/lab/bucket_stage_lab.log)
-        rs_tile_scatter<R, kBkWaves>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
+        rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
         __syncthreads();
         BK_STAMP(4);
-        if (d < nb) gst[d] += tc;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+            if (d < nb) gst[d] += tc[j];
+        }
     }
 }
 
@@ -1612,6 +1670,10 @@ static int end_bit_for(uint32_t num_slots) {
 struct SortPlan {
     int passes, bits, rounds;   // rounds: 64-item rounds per wave (chunk = 4 waves x 64 x rounds)
     size_t nch, hist_elems;
+    // the chunk + bucket sort: A's high digit and B's low digit (hbits + lbits = the key's
+    // bits); wide = 2,048-bin kernels (keys of 19-22 bits); bucket_ok = keys of <= 22 bits
+    int hbits, lbits;
+    bool wide, bucket_ok;
 };
 
 static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
@@ -1619,6 +1681,13 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     const int eb = end_bit_for(num_slots);
     p.passes = (eb + kRsMaxBits - 1) / kRsMaxBits;
     p.bits = (eb + p.passes - 1) / p.passes;
+    // chunk + bucket split: the digit passes' two digits up to 18 bits (512 bins); 19-22 bits
+    // (pools of 2^18 .. 2^21 slots) in two digits of 10-11 bits (2,048 bins) instead of the
+    // three LSD passes
+    p.wide = eb > 2 * kRsMaxBits;
+    p.bucket_ok = eb <= 2 * kBitsBig;
+    p.hbits = p.wide ? (eb + 1) / 2 : p.bits;
+    p.lbits = eb - p.hbits;
     // chunk = 4 waves x 64 x rounds items: 1,024 up to 256 Ki packets (a batch of the PS's
     // acks still spreads over more than a few dozen CUs), 2,048 up to 512 Ki, 4,096 above
     // (switch_lab, profiles/r01/lab/switch_lab_rounds.log: 102,400 packets 77.7 -> 60.9 us,
@@ -1631,7 +1700,7 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     if (const int r = g_os_rounds.load()) p.rounds = r;   // ina_set_tuning key 13 (lab sweeps)
     const size_t chunk = (size_t)kRsWaves * 64 * (size_t)p.rounds;
     p.nch = (npk + chunk - 1) / chunk;
-    p.hist_elems = ((size_t)1 << p.bits) * p.nch;
+    p.hist_elems = ((size_t)1 << std::max(p.bits, p.hbits)) * p.nch;
     return p;
 }
 
@@ -1660,7 +1729,7 @@ static size_t sort_nch_cap(size_t npk) {
 
 static size_t sort_hist_cap(size_t npk, uint32_t num_slots) {
     const SortPlan p = sort_plan(npk, num_slots);
-    return ((size_t)1 << p.bits) * sort_nch_cap(npk);
+    return ((size_t)1 << std::max(p.bits, p.hbits)) * sort_nch_cap(npk);
 }
 
 static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
@@ -1784,7 +1853,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     const bool small = npk <= (size_t)g_small_sort.load();
     // chunk + bucket sort: keys of one or two digits (the low digit is one workgroup's LDS
     // bins) and at most kBkMaxChunks chunks (B's LDS rows); else the digit passes
-    const bool bucket = !small && g_sort_mode.load() == 0 && sp.passes <= 2 && sp.nch <= (size_t)kBkMaxChunks;
+    const bool bucket = !small && g_sort_mode.load() == 0 && sp.bucket_ok && sp.nch <= (size_t)kBkMaxChunks;
     const uint32_t* nforeign = nullptr;
     const uint32_t* unsorted = nullptr;     // bucket sort: the run kernel may read A's output
     uint32_t epoch = 0;
@@ -1817,8 +1886,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // A: keys + each chunk sorted by the high digit (bits lb..eb-1) -> (kn, vn) and the
         // per (digit, chunk) run lengths / starts; B: each bucket gathered in chunk order and
         // sorted on its low digit -> (kc, vc)
-        const int eb = end_bit_for(st->num_slots);
-        const int lb = eb - sp.bits;                       // low digit bits (0: one-digit keys)
+        const int lb = sp.lbits;                           // low digit bits (0: one-digit keys)
         const uint2* dsc = reinterpret_cast<const uint2*>(desc);
         const int ah = ack_hint ? 1 : 0;
         // dense ascending runs skip the sort (run table, switch_runs_body): the register-
@@ -1830,10 +1898,11 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
 #define INA_A_LAUNCH(RR)                                                                              \
-        hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true> : &k_sort_chunks<RR, false>), dim3(gc),   \
-                           dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots, st->switch_id,  \
-                           actions, sp.bits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, ax.unsorted, epoch, \
-                           runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
+        hipLaunchKernelGGL((sp.wide ? (desc ? &k_sort_chunks<RR, true, kBinsBig> : &k_sort_chunks<RR, false, kBinsBig>) \
+                                    : (desc ? &k_sort_chunks<RR, true, kRsBins> : &k_sort_chunks<RR, false, kRsBins>)), \
+                           dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
+                           st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah,  \
+                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
         if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
         else INA_A_LAUNCH(kR0 / 4);
@@ -1850,11 +1919,13 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const uint32_t CH = (uint32_t)kRsWaves * 64u * (uint32_t)sp.rounds;
         // buckets past the sentinel's (num_slots >> lb) are always empty: no block for them,
         // so at 2^17 slots 257 blocks (one per CU, one generation) instead of 512
-        const unsigned gb = std::min<unsigned>(nb, (st->num_slots >> lb) + 1u);
+        const unsigned gb = std::min<unsigned>(1u << sp.hbits, (st->num_slots >> lb) + 1u);
         const int tile = g_bucket_tile.load();
         const bool big = tile == kLcRoundsBig || (tile == 0 && npk > (size_t)gb * kBigTileAvg);
         if (do_sort)
-            hipLaunchKernelGGL((big ? &k_sort_buckets<kLcRoundsBig> : &k_sort_buckets<kLcRounds>), dim3(gb),
+            hipLaunchKernelGGL((sp.wide ? (big ? &k_sort_buckets<kLcRoundsBig, kBinsBig> : &k_sort_buckets<kLcRounds, kBinsBig>)
+                                        : (big ? &k_sort_buckets<kLcRoundsBig, kRsBins> : &k_sort_buckets<kLcRounds, kRsBins>)),
+                               dim3(gb),
                                dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
                                ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1,
                                runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, (uint32_t)npk);

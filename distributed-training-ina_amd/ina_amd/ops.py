@@ -281,6 +281,8 @@ def _ack_desc_arg(ack_desc, acks):
         raise ValueError("ack_desc needs acks")
     _req(ack_desc, torch.int64, "ack_desc")
     _fits(ack_desc, acks.shape[0], "ack_desc")
+    if not ack_desc.is_contiguous():
+        raise ValueError("ack_desc must be contiguous (one int64 per ack row)")
     _same_device(acks, ack_desc)
     return ack_desc.data_ptr()
 

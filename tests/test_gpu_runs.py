@@ -64,9 +64,11 @@ def runs_batch(rng, V, specs, W, stride, num_slots=POOL, collide=0.02, degree_mi
     return pk
 
 
-def check_batches(o, V, batches, want_path, use_desc=True, write_dropped=True, num_slots=POOL):
+def check_batches(o, V, batches, want_path, use_desc=True, write_dropped=True, num_slots=POOL,
+                  regs_each=True):
     """Every batch through a fresh device switch and the oracle (state carried across the
-    batches): bit-exact actions, packets and registers, and the slot-sort path taken."""
+    batches): bit-exact actions, packets and registers (after every batch, or only after the
+    last with regs_each=False), and the slot-sort path taken."""
     stride = batches[0].shape[1]
     sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=write_dropped)
     sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
@@ -83,6 +85,8 @@ def check_batches(o, V, batches, want_path, use_desc=True, write_dropped=True, n
             assert np.array_equal(got[fwd], want_pk[fwd]), i
         if want_path is not None:
             assert sw_dev.batch_path(len(stream)) == want_path, i
+        if not regs_each and i < len(batches) - 1:
+            continue
         cnt, frag, regs = sw_orc.registers()
         assert np.array_equal(host(sw_dev.count), cnt), i
         assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag), i
@@ -330,3 +334,103 @@ def test_two_phase_descriptor_mismatch_is_caught(bad):
     sw.check_sorted_desc(big)                           # the matching ones pass
     sw.run(big, acts)
     assert int((host(acts) == orc.ACT_FWD_AGG).sum()) == npk
+
+
+# pools of 2^18 .. 2^21 slots: keys of 19-22 bits, the 2,048-bin chunk + bucket sort (digits of
+# 10-11 bits) instead of three LSD digit passes; its in-order and run-table paths as well
+WIDE_POOLS = [1 << 18, (1 << 19) + 3, 1 << 20, (1 << 21) - 1, 1 << 21]
+
+
+@pytest.mark.parametrize("order", ["shuffled", "worker_major", "round_robin", "skewed"])
+@pytest.mark.parametrize("num_slots", WIDE_POOLS)
+def test_wide_key_pools_vs_oracle(num_slots, order):
+    """Bit-exact against the P4 restatement with state carried across batches, and the same
+    batches through the LSD digit passes (tuning key 12 = 3) -- worker-major batches wrap the
+    pool (a run breaks at slot 0), "skewed" puts every packet in three buckets (multi-tile
+    buckets of the 2,048-bin sort)."""
+    o = ops()
+    rng = np.random.default_rng(num_slots % 1000 + len(order))
+    V, W, per = 32, 8, 1200
+    stride = o.nga_stride(V)
+    seq0 = {"worker_major": num_slots - 500, "skewed": 1, "round_robin": 7}.get(order)
+    if seq0 is None:
+        seq0 = int(rng.integers(0, num_slots))
+    specs = [(seq0, per, w) for w in range(W)]
+    batches = []
+    for _ in range(2):
+        b = runs_batch(rng, V, specs, W, stride, num_slots=num_slots)
+        if order in ("shuffled", "skewed"):
+            b = b[rng.permutation(len(b))]
+        elif order == "round_robin":
+            b = b.reshape(W, per, stride).transpose(1, 0, 2).reshape(W * per, stride).copy()
+        batches.append(b)
+    want = {"shuffled": "sorted", "skewed": "sorted", "worker_major": "runs", "round_robin": "in_order"}[order]
+    check_batches(o, V, batches, want, num_slots=num_slots, regs_each=False)
+    o.set_tuning(switch_sort=3)
+    try:
+        check_batches(o, V, batches, None, num_slots=num_slots, regs_each=False)
+    finally:
+        o.set_tuning(switch_sort=0)
+
+
+@pytest.mark.parametrize("tile", [0, 8])
+def test_wide_key_multi_tile_buckets(tile):
+    """2^20-slot pool, 24,000 packets in slots 0..2,999 (three 1,024-slot buckets of 8,000
+    packets: several 4,096- or 8,192-item tiles each, the counting sweep first), shuffled."""
+    o = ops()
+    rng = np.random.default_rng(tile + 5)
+    V, W, per, ns = 32, 8, 3000, 1 << 20
+    b = runs_batch(rng, V, [(0, per, w) for w in range(W)], W, o.nga_stride(V), num_slots=ns)
+    b = b[rng.permutation(len(b))]
+    o.set_tuning(switch_bucket_tile=tile)
+    try:
+        check_batches(o, V, [b, b.copy()], "sorted", num_slots=ns, regs_each=False)
+    finally:
+        o.set_tuning(switch_bucket_tile=0)
+
+
+@pytest.mark.parametrize("order", ["worker_major", "shuffled"])
+def test_nga32_config3_full_size(order):
+    """The P4 program's own format (NGA-32, headers.p4:40-73) at config-3 size: 8 workers x
+    819,200 packets through a 2^20-slot pool (21-bit keys), worker-major (the run table) and
+    shuffled (the 2,048-bin sort).  Size-independent checks: every slot completes exactly
+    once, on the last packet of its slot; a strided sample of slots (every 997th + the last)
+    carries the wrapping int32 sum of the workers' values in its completing packet and in
+    the slot's registers."""
+    o = ops()
+    W, n, V, ns = 8, 26_214_400, 32, 1 << 20
+    npk = n // V
+    g = torch.Generator(device=DEV).manual_seed(31)
+    samp = np.unique(np.concatenate([np.arange(0, npk, 997), [npk - 1]]))
+    vidx = torch.from_numpy((samp[:, None] * V + np.arange(V)).ravel()).to(DEV)
+    want = torch.zeros(vidx.numel(), dtype=torch.int64, device=DEV)
+    rows, descs = [], []
+    for w in range(W):
+        b = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
+        want += b[vidx].to(torch.int64)
+        p, d = o.pack_nga(b, V, w + 1, W, 1, 1, num_slots=ns, desc=True)
+        rows.append(p)
+        descs.append(d)
+        del b
+    want = ((want + (1 << 31)) % (1 << 32) - (1 << 31)).to(torch.int32).view(-1, V)
+    stream, desc = torch.cat(rows), torch.cat(descs)
+    del rows, descs
+    perm = None if order == "worker_major" else torch.randperm(W * npk, device=DEV, generator=g)
+    if perm is not None:
+        stream, desc = stream[perm], desc[perm]
+    sw = o.Switch(V, num_slots=ns, switch_id=1, device=DEV)
+    act = sw.process(stream, desc=desc)
+    assert sw.batch_path(W * npk) == ("runs" if perm is None else "sorted")
+    assert int((act == orc.ACT_FWD_AGG).sum()) == npk
+    assert int((act == orc.ACT_DROP).sum()) == (W - 1) * npk
+    pos = torch.arange(W * npk, device=DEV) if perm is None else torch.argsort(perm)
+    ts = torch.from_numpy(samp).to(DEV)
+    cand = torch.stack([pos[w * npk + ts] for w in range(W)])
+    fwd = act[cand] == orc.ACT_FWD_AGG
+    assert bool((fwd.sum(0) == 1).all())
+    last = cand.max(0).values                              # completes on its last arrival
+    assert torch.equal(cand.gather(0, fwd.to(torch.int64).argmax(0, keepdim=True)).reshape(-1), last)
+    pay = stream[last, 15:15 + 4 * V].contiguous().cpu().numpy().view(">u4").astype(np.uint32)
+    assert np.array_equal(pay.reshape(-1, V), want.cpu().numpy().view(np.uint32))
+    assert torch.equal(sw.regs[ts], want)
+    assert int(sw.count[ts].max()) == 0 and int(sw.count.max()) == 0
