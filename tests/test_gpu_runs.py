@@ -432,5 +432,6 @@ def test_nga32_config3_full_size(order):
     assert torch.equal(cand.gather(0, fwd.to(torch.int64).argmax(0, keepdim=True)).reshape(-1), last)
     pay = stream[last, 15:15 + 4 * V].contiguous().cpu().numpy().view(">u4").astype(np.uint32)
     assert np.array_equal(pay.reshape(-1, V), want.cpu().numpy().view(np.uint32))
-    assert torch.equal(sw.regs[ts], want)
-    assert int(sw.count[ts].max()) == 0 and int(sw.count.max()) == 0
+    slot = (ts + 1) % ns                                   # packet p of a worker: slot (seq0 + p) % pool
+    assert torch.equal(sw.regs[slot], want)
+    assert int(sw.count.max()) == 0
