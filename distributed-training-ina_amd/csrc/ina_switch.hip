@@ -1443,7 +1443,202 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
     if (have_reg && vl) __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * lane));
 }
 
-template <bool kPs, bool kLat = false>
+// Narrow packets (V <= 32: NGA-32, the P4 program's own format, headers.p4:40-73): run_segment
+// above gives each packet the whole wave, so only V/4 + 1 of its 64 lanes work and a batch's
+// packets go one after another -- at 6.5 M NGA-32 packets the kernel was instruction-bound
+// (0.19 of the HBM roofline).  Here the wave takes a batch's 8 packets side by side: lane
+// group g = lane / 8 holds packet g, its lane l = lane % 8 chunk l (values 4l..4l+3; the
+// group's last value lane also loads the tail chunk V/4).  The count / frag state machine
+// still runs packet by packet in arrival order, in SGPRs (8 x 3 header words by readlane),
+// and leaves per-packet masks (adds, overwrites, forwards, collisions, PS consumption); the
+// Processor adds become ONE segmented inclusive scan over the 8 groups (resets at the
+// count_reg == 1 overwrites, processor.p4:16-21) -- 3 shuffle steps -- so each packet's
+// running sum, the value the P4 program writes into it (processor.p4:22), is in its group's
+// lanes at once.  Same results as run_segment, packet for packet.
+__device__ __forceinline__ uint32_t from_lane(uint32_t x, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)x);
+}
+// DPP row_shl:1 / row_shr:1: lane i reads lane i+1 / i-1 inside its 16-lane row (a group of 8
+// never needs its neighbour group: chunk l+1 of the group's last lane is the loaded tail, and
+// lane 0 of a group encodes the header chunk without its predecessor)
+__device__ __forceinline__ uint32_t from_next_in_row(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x101, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_prev_in_row(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x111, 0xF, 0xF, false);
+}
+constexpr int kNarrowMaxV = 32;
+static_assert(kB == 8, "the narrow run puts a batch of 8 packets in 8 lane groups");
+
+template <bool kPs, typename PidFn>
+__device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                                   size_t stride, uint8_t* __restrict__ actions,
+                                                   const PsFuse& ps, uint32_t slot, bool ack_led,
+                                                   size_t q_begin, size_t q_end, PidFn&& pid_batch) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 3, l = lane & 7;      // packet group, value lane
+    const int V = st.V;
+    const int L = V >> 2;                       // value lanes per group (<= 8)
+    const bool vl = l < L;
+    uint32_t cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
+    uint32_t frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
+    u32x4s reg = {0u, 0u, 0u, 0u};              // the slot's running registers, in every group
+    bool have_reg = false;
+    for (size_t q0 = q_begin; q0 < q_end; q0 += kB) {
+        const int nb = (int)((q_end - q0) < (size_t)kB ? (q_end - q0) : (size_t)kB);
+        uint32_t pid[kB];
+        pid_batch(q0, nb, pid);
+#pragma unroll
+        for (int b = 1; b < kB; ++b) pid[b] = b < nb ? pid[b] : pid[0];
+        uint32_t mypid = pid[0], lanepid = pid[0];   // group g's packet; lane b's (actions)
+#pragma unroll
+        for (int b = 1; b < kB; ++b) {
+            mypid = g == b ? pid[b] : mypid;
+            lanepid = lane == b ? pid[b] : lanepid;
+        }
+        const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride);
+        const u32x4s a = sw_ld(pk + (vl ? l : 0));   // chunk l (lanes past L re-read chunk 0)
+        const u32x4s tl = *(pk + L);                  // the tail chunk (one request per group)
+        // the state machine, packet by packet in arrival order (SGPRs, scalar branches)
+        uint32_t m_add = 0, m_first = 0, m_fwd = 0, m_coll = 0, m_ps = 0;
+        uint32_t act_v = 0, ps_slot_v = 0;
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            if (b >= nb) break;
+            const uint32_t h1 = __builtin_amdgcn_readlane(a.y, 8 * b),
+                           h2 = __builtin_amdgcn_readlane(a.z, 8 * b),
+                           h3 = __builtin_amdgcn_readlane(a.w, 8 * b);
+            const uint32_t hcount = h1 & 0xFFu, flags = (h1 >> 8) & 0xFFu;
+            const uint32_t frag_in =
+                __builtin_amdgcn_readfirstlane(__builtin_bswap32((h2 >> 24) | (h3 << 8)));
+            uint32_t act;
+            if ((flags >> 6) & 1u) {                     // ack: reset_id (fragcheck.p4:26-31)
+                frag = 0;
+                act = INA_ACT_FWD_ACK;
+            } else {
+                if (frag == 0) frag = frag_in;           // write_read_id (fragcheck.p4:14-24)
+                if (frag != frag_in) {                   // collision (ngaa.p4:177-181)
+                    act = INA_ACT_FWD_COLLISION;
+                    m_coll |= 1u << b;
+                } else {
+                    cnt = (cnt + 1u) & 0xFFu;            // read_add_count (ngaa.p4:66-78)
+                    if (cnt == hcount) cnt = 0;
+                    cnt = __builtin_amdgcn_readfirstlane(cnt);
+                    m_add |= 1u << b;
+                    if (cnt == 1u) m_first |= 1u << b;   // processor.p4:16-21 overwrite
+                    act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
+                    const uint32_t ps_slot = frag_in - ps.seq0;
+                    const bool consumed = kPs && act == INA_ACT_FWD_AGG && ps_slot < ps.nslots;
+                    if (consumed) {
+                        m_ps |= 1u << b;
+                        ps_slot_v = g == b ? ps_slot : ps_slot_v;
+                    }
+                    if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd))
+                        m_fwd |= 1u << b;
+                }
+            }
+            act_v = lane == b ? act : act_v;
+        }
+        if (lane < nb) actions[lanepid] = (uint8_t)act_v;   // one store for the batch
+        if (((m_coll >> g) & 1u) && l == 0)                // only the flag byte changes
+            reinterpret_cast<uint32_t*>(pkts + (size_t)mypid * stride)[1] = a.y | ((uint32_t)INA_FLAG_COLLISION << 8);
+        if (m_add) {
+            // values 4l..4l+3 of packet g: chunk l and chunk l+1 (the neighbour lane, or the
+            // tail for the group's last value lane)
+            u32x4s c;
+            c.x = from_next_in_row(a.x); c.y = from_next_in_row(a.y);
+            c.z = from_next_in_row(a.z); c.w = from_next_in_row(a.w);
+            if (l == L - 1) c = tl;
+            u32x4s x;
+            x.x = dec_be(c.x, a.w); x.y = dec_be(c.y, c.x); x.z = dec_be(c.z, c.y); x.w = dec_be(c.w, c.z);
+            const bool add = (m_add >> g) & 1u;
+            uint32_t f = (m_first >> g) & 1u;
+            if (!add) x = u32x4s{0u, 0u, 0u, 0u};
+            // segmented inclusive scan over the groups (a reset at each overwrite)
+#pragma unroll
+            for (int d = 1; d < kB; d <<= 1) {
+                const int src = lane - 8 * d;
+                u32x4s y;
+                y.x = from_lane(x.x, src); y.y = from_lane(x.y, src);
+                y.z = from_lane(x.z, src); y.w = from_lane(x.w, src);
+                const uint32_t fy = from_lane(f, src);
+                if (g >= d && !f) {
+                    x += y;
+                    f |= fy;
+                }
+            }
+            // the stored registers count only before the batch's first overwrite; load them
+            // if an add comes before it and no earlier batch left them in registers
+            const uint32_t before = m_first ? m_add & ((m_first & (0u - m_first)) - 1u) : m_add;
+            if (before && !have_reg)
+                reg = vl ? *reinterpret_cast<const u32x4s*>(st.regs + (size_t)slot * V + 4 * l)
+                         : u32x4s{0u, 0u, 0u, 0u};
+            const u32x4s S = f ? x : x + reg;        // packet g's running sum
+            // the registers after the batch: the last adding packet's running sum
+            const int lastb = 31 - __builtin_clz(m_add);
+            const int src = 8 * lastb + l;
+            reg.x = from_lane(S.x, src); reg.y = from_lane(S.y, src);
+            reg.z = from_lane(S.z, src); reg.w = from_lane(S.w, src);
+            have_reg = true;
+            if (kPs && ((m_ps >> g) & 1u)) {         // launch.py:46-50 with the switch's sum
+                const size_t e0 = (size_t)ps_slot_v * (size_t)V + 4 * (size_t)l;
+                if (vl && e0 + 4 <= ps.n) {
+                    const f32x4s lo = *reinterpret_cast<const f32x4s*>(ps.local + e0);
+                    f32x4s r;
+                    r.x = __fadd_rn(lo.x, __fmul_rn(__fmul_rn((float)(int32_t)S.x, ps.inv), ps.ws));
+                    r.y = __fadd_rn(lo.y, __fmul_rn(__fmul_rn((float)(int32_t)S.y, ps.inv), ps.ws));
+                    r.z = __fadd_rn(lo.z, __fmul_rn(__fmul_rn((float)(int32_t)S.z, ps.inv), ps.ws));
+                    r.w = __fadd_rn(lo.w, __fmul_rn(__fmul_rn((float)(int32_t)S.w, ps.inv), ps.ws));
+                    __builtin_nontemporal_store(r, reinterpret_cast<f32x4s*>(ps.out + e0));
+                } else if (vl) {
+                    const uint32_t rv[4] = {S.x, S.y, S.z, S.w};
+                    for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
+                        ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
+                                                   __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
+                }
+                if (l == 0 && ps.acks) {             // the PS ack (fragcheck.p4:26-31)
+                    u32x4s hd = a;
+                    hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+                    hd.w = (hd.w & 0x00FFFFFFu) | (S.x & 0xFF000000u);
+                    *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot_v * ps.ack_stride) = hd;
+                    if (ps.ack_desc) ps.ack_desc[ps_slot_v] = uint2{hd.y, hd.z};
+                }
+            }
+            if ((m_fwd >> g) & 1u) {                 // out_value -> payload (processor.p4:22)
+                u32x4s p;                            // values of lane l-1
+                p.x = from_prev_in_row(S.x); p.y = from_prev_in_row(S.y);
+                p.z = from_prev_in_row(S.z); p.w = from_prev_in_row(S.w);
+                u32x4s e = a;
+                if (l == 0) {
+                    e.w = (e.w & 0x00FFFFFFu) | (S.x & 0xFF000000u);
+                } else {
+                    e.x = enc_lo(p.x, p.y);
+                    e.y = enc_lo(p.y, p.z);
+                    e.z = enc_lo(p.z, p.w);
+                    e.w = enc_lo(p.w, S.x);
+                }
+                u32x4s* dst = reinterpret_cast<u32x4s*>(pkts + (size_t)mypid * stride);
+                if (vl) sw_st(e, dst + l);
+                if (l == L - 1) {                    // the tail chunk from the last value lane
+                    u32x4s o;
+                    o.x = enc_lo(S.x, S.y);
+                    o.y = enc_lo(S.y, S.z);
+                    o.z = enc_lo(S.z, S.w);
+                    o.w = enc_lo(S.w, tl.w);
+                    sw_st(o, dst + L);
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        st.count[slot] = (uint8_t)cnt;
+        st.frag[slot] = frag;
+    }
+    if (have_reg && g == 0 && vl)
+        __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
+}
+
+template <bool kPs, bool kLat = false, bool kNarrow = false>
 __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                  size_t npk, size_t stride,
                                                  const uint32_t* __restrict__ keys,
@@ -1498,8 +1693,7 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
             }
         }
         const bool ack_led = (am >> hl) & 1ull;
-        run_segment<kPs, kLat>(st, pkts, stride, actions, ps, slot, ack_led, pos + (ack_led ? 1 : 0), end,
-                               [&](size_t q0, int nb, uint32_t (&pid)[kB]) {
+        auto pids = [&](size_t q0, int nb, uint32_t (&pid)[kB]) {
             // packet ids first (no load in the common in-window case; one coalesced load
             // otherwise), so the kB packet loads below issue back to back with no
             // s_waitcnt between them
@@ -1513,7 +1707,11 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
 #pragma unroll
                 for (int b = 0; b < kB; ++b) pid[b] = __builtin_amdgcn_readlane(my, b);
             }
-        });
+        };
+        if constexpr (kNarrow)
+            run_segment_narrow<kPs>(st, pkts, stride, actions, ps, slot, ack_led, pos + (ack_led ? 1 : 0), end, pids);
+        else
+            run_segment<kPs, kLat>(st, pkts, stride, actions, ps, slot, ack_led, pos + (ack_led ? 1 : 0), end, pids);
         }
     }
 }
@@ -1523,7 +1721,7 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
 // slots (one pass of the grid) and runs slot s's segment -- the packets start_r + s -
 // first_r of the runs that hold s, in run order = arrival order -- through run_segment.
 // A PS ack leading its segment is done without reading it, as in switch_run2_body.
-template <bool kPs>
+template <bool kPs, bool kNarrow>
 __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                  size_t stride, uint8_t* __restrict__ actions,
                                                  uint32_t kmask, const PsFuse& ps,
@@ -1573,9 +1771,8 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
             }
             if (!m) continue;
         }
-        run_segment<kPs, false>(st, pkts, stride, actions, ps, slot, ack_led, 0,
-                                (size_t)__builtin_popcountll(m),
-                                [&](size_t, int nb, uint32_t (&pid)[kB]) {
+        const size_t nseg = (size_t)__builtin_popcountll(m);
+        auto pids = [&](size_t, int nb, uint32_t (&pid)[kB]) {
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
                 if (b < nb) {
@@ -1586,7 +1783,11 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
                     pid[b] = 0u;
                 }
             }
-        });
+        };
+        if constexpr (kNarrow)
+            run_segment_narrow<kPs>(st, pkts, stride, actions, ps, slot, ack_led, 0, nseg, pids);
+        else
+            run_segment<kPs, false>(st, pkts, stride, actions, ps, slot, ack_led, 0, nseg, pids);
     }
 }
 
@@ -1607,7 +1808,7 @@ __device__ __forceinline__ size_t switch_block_index() {
 #endif
 }
 
-template <bool kPs>
+template <bool kPs, bool kNarrow>
 __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? INA_SWITCH_WAVES : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts, size_t npk,
                                                           size_t stride,
@@ -1631,7 +1832,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
             ids = ids_a;
         } else if (unsorted[2] == ep) {
             // a batch of dense ascending runs: the bucket pass wrote the run table, not a sort
-            switch_runs_body<kPs>(st, pkts, stride, actions, kmask, ps, unsorted + (kCtlRuns - kCtlEpochs),
+            switch_runs_body<kPs, kNarrow>(st, pkts, stride, actions, kmask, ps, unsorted + (kCtlRuns - kCtlEpochs),
                                   wave, nwaves);
             return;
         }
@@ -1639,7 +1840,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
-    switch_run2_body<kPs>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps, wave, nwaves);
+    switch_run2_body<kPs, false, kNarrow>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps, wave, nwaves);
 }
 
 // batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
@@ -1984,7 +2185,11 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
         const size_t per_block = (size_t)win * (kSwBlock / 64);
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
-        auto* run = ps.on ? &k_switch_run2<true> : &k_switch_run2<false>;
+        // V <= 32 (NGA-32, the P4 program's format): 8 packets of a segment side by side per
+        // wave (run_segment_narrow); wider packets: a packet per wave instruction
+        const bool narrow = st->V <= kNarrowMaxV;
+        auto* run = ps.on ? (narrow ? &k_switch_run2<true, true> : &k_switch_run2<true, false>)
+                          : (narrow ? &k_switch_run2<false, true> : &k_switch_run2<false, false>);
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc, vc, actions,
                            win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted);
         *fused_out = ps.on != 0;

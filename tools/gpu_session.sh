@@ -59,6 +59,12 @@ for st in $STAGES; do
           python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
         rc=$?; tail -2 "$OUT/pmc_$c.err"; [ $rc -ne 0 ] && fatal "pmc $c" $rc
       done ;;
+    swtrace:*)
+      # kernel trace of tools/prof_switch.py with env overrides, e.g. swtrace:V=32,ORDER=wm,RUNS=1
+      envs=${st#swtrace:}; tag=$(echo "$envs" | tr ',=' '__')
+      ( export ${envs//,/ }; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$OUT/swtrace_$tag" -o run -- python3 tools/prof_switch.py > "$OUT/swtrace_$tag.log" 2>&1 )
+      rc=$?; tail -2 "$OUT/swtrace_$tag.log"; [ $rc -ne 0 ] && fatal "$st" $rc ;;
     swprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/swprof" -o run -- \
         python3 tools/prof_switch.py > "$OUT/swprof.log" 2>&1

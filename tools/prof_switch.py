@@ -10,12 +10,13 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "distributed-training-ina_amd"))
 from ina_amd import ops  # noqa: E402
 
-n, W, V = int(os.environ.get("N", 26_214_400)), 8, 256
+n, W, V = int(os.environ.get("N", 26_214_400)), 8, int(os.environ.get("V", 256))
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(1)
 bufs = [torch.randint(-(1 << 20), 1 << 20, (n,), dtype=torch.int32, device=dev, generator=g)
         for _ in range(W)]
-slots = 1 << 17
+slots = int(os.environ.get("SLOTS", 1 << 17))
+ops.set_tuning(switch_runs=os.environ.get("RUNS", "1") == "1")
 packed = [ops.pack_nga(b, V, w + 1, W, 1, 1, num_slots=slots, desc=True) for w, b in enumerate(bufs)]
 stream = torch.cat([p for p, _ in packed])
 desc = torch.cat([d for _, d in packed])     # the pack kernels' packet descriptors
