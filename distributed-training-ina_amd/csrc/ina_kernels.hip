@@ -1215,6 +1215,120 @@ __global__ __launch_bounds__(kBlock) void k_qpack_nga_multi_v256(QPackGroup a, c
     }
 }
 
+// ---- split NGA rows: header rows + payload rows (include/ina.h "split layout") ------------
+// The wire datagram is header (15 B) || payload (4V B).  Stored split -- a 16-byte header row
+// (the 15 wire bytes + a zero) and a 4V-byte payload row of V big-endian words -- every
+// payload row starts 16-byte aligned and covers exactly 4V/128 cache lines, so the packs
+// store whole aligned chunks (the packed NGA-256 row's 1,040 bytes touch 9 lines and its
+// body stores straddle 16-byte boundaries), and the payload stream of a bucket IS its
+// values in order, byte-swapped, zero-padded to whole packets: packing is an elementwise
+// pass.  sendmmsg / recvmmsg carry it as two iovecs per datagram (same bytes on the wire).
+__device__ __forceinline__ u32x4 nga_hdr_row(uint32_t bitmap, uint32_t fcs, uint32_t seq, uint32_t num_slots) {
+    const uint32_t bi = bswap(seq % num_slots), bf = bswap(seq);
+    return u32x4{bswap(bitmap), (fcs & 0xFFFFu) | (bi << 16),
+                 (bi >> 16) | (((fcs >> 16) & 0xFFu) << 16) | (bf << 24), bf >> 8};
+}
+__device__ __forceinline__ u32x4 bswap4(u32x4 v) {
+    return u32x4{bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w)};
+}
+
+// one worker: payload chunk t = values 4t..4t+3 byte-swapped (zero past n); header rows and
+// descriptors a thread per packet
+template <typename Src>
+__global__ __launch_bounds__(kBlock) void k_pack_nga_split(Src src, size_t n, NgaHdr h,
+                                                           const uint8_t* __restrict__ ovf,
+                                                           u32x4* __restrict__ hdr, u32x4* __restrict__ pay,
+                                                           u32x2* __restrict__ desc, size_t nch, size_t np,
+                                                           int vec) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    for (size_t t = tid; t < nch; t += gs) {
+        const size_t e0 = 4 * t;
+        u32x4 v;
+        if (vec && e0 + 4 <= n) {
+            v = src.four(e0);
+        } else {
+            v.x = e0 < n ? src.one(e0) : 0u;
+            v.y = e0 + 1 < n ? src.one(e0 + 1) : 0u;
+            v.z = e0 + 2 < n ? src.one(e0 + 2) : 0u;
+            v.w = e0 + 3 < n ? src.one(e0 + 3) : 0u;
+        }
+        packet_store(bswap4(v), pay + t);
+    }
+    for (size_t p = tid; p < np; p += gs) {
+        uint32_t fcs = h.flags_count_sw;
+        if (ovf && ovf[p]) fcs |= (uint32_t)INA_FLAG_OVERFLOW << 8;
+        const u32x4 r = nga_hdr_row(h.bitmap, fcs, h.seq0 + (uint32_t)p, h.num_slots);
+        packet_store(r, hdr + p);
+        if (desc) desc[p] = u32x2{r.y, r.z};
+    }
+}
+
+// up to kQpGroup workers' fused quantise(x_w - base) + split pack in one launch: the base
+// chunk loaded once for every worker, each worker's payload stream coalesced
+struct QPackSplit {
+    const float* x[kQpGroup];
+    u32x4* hdr[kQpGroup];
+    u32x4* pay[kQpGroup];
+    u32x2* desc[kQpGroup];          // all null or all set
+    uint32_t bitmap[kQpGroup], seq0[kQpGroup], fcs[kQpGroup];
+};
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_qpack_nga_multi_split(QPackSplit a, const float* __restrict__ base,
+                                                                  size_t n, float s, uint32_t num_slots,
+                                                                  size_t nch, size_t np) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    for (size_t t = tid; t < nch; t += gs) {
+        const size_t e0 = 4 * t;
+        if (e0 + 4 <= n) {
+            f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (base) b = *reinterpret_cast<const f32x4*>(base + e0);   // default policy: shared
+            f32x4 x[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) x[g] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.x[g] + e0));
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                f32x4 y = x[g];
+                if (base) {
+                    y.x = __fsub_rn(y.x, b.x); y.y = __fsub_rn(y.y, b.y);
+                    y.z = __fsub_rn(y.z, b.z); y.w = __fsub_rn(y.w, b.w);
+                }
+                const u32x4 q{(uint32_t)q32(y.x, s), (uint32_t)q32(y.y, s), (uint32_t)q32(y.z, s),
+                              (uint32_t)q32(y.w, s)};
+                packet_store(bswap4(q), a.pay[g] + t);
+            }
+        } else {                                       // the bucket's last chunk: zero tail
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const SrcQ32 src{a.x[g], base, s};
+                u32x4 v;
+                v.x = e0 < n ? src.one(e0) : 0u;
+                v.y = e0 + 1 < n ? src.one(e0 + 1) : 0u;
+                v.z = e0 + 2 < n ? src.one(e0 + 2) : 0u;
+                v.w = e0 + 3 < n ? src.one(e0 + 3) : 0u;
+                packet_store(bswap4(v), a.pay[g] + t);
+            }
+        }
+    }
+    for (size_t p = tid; p < np; p += gs) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const u32x4 r = nga_hdr_row(a.bitmap[g], a.fcs[g], a.seq0[g] + (uint32_t)p, num_slots);
+            packet_store(r, a.hdr[g] + p);
+            if (a.desc[g]) a.desc[g][p] = u32x2{r.y, r.z};
+        }
+    }
+}
+
+// split rows -> int32 values (payload byte-swapped back; every payload word, npk * V)
+__global__ __launch_bounds__(kBlock) void k_unpack_nga_split_vals(const u32x4* __restrict__ pay, size_t nch,
+                                                                  u32x4* __restrict__ vals) {
+    const size_t gs = (size_t)gridDim.x * kBlock;
+    for (size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x; t < nch; t += gs)
+        stream_store(bswap4(__builtin_nontemporal_load(pay + t)), vals + t);
+}
+
 // One worker's NGA-256 packets, a wave per packet (the layout of k_qpack_nga_multi_v256):
 // fp32 quantised on the fly (int32 words and the per-packet overflow flag are supported; the
 // int32 pack is faster on the flat stream, see pack_nga_launch).
@@ -2217,6 +2331,100 @@ int ina_nga_descriptors(const uint8_t* pkts, size_t npk, size_t pstride, ina_nga
     hipLaunchKernelGGL(k_nga_desc, dim3(grid_for(npk, 1)), dim3(kBlock), 0, hs(stream), pkts, npk, pstride,
                        desc);
     return check_launch("nga_descriptors");
+}
+
+// ---- split rows (include/ina.h) ----------------------------------------------------------
+static int split_geometry(int V, uint32_t num_slots) {
+    if (V <= 0 || V % 4 || V > 256 || num_slots == 0)
+        return set_error(INA_EINVAL, "split rows need V a multiple of 4 in [4, 256] and num_slots > 0%s", "");
+    return INA_OK;
+}
+
+int ina_pack_nga_split(const int32_t* vals, size_t n, const ina_nga_params_t* prm, const uint8_t* ovf,
+                       uint8_t* hdr, uint8_t* pay, ina_nga_desc_t* desc, ina_stream_t stream) {
+    if (!prm) return set_error(INA_EINVAL, "null params%s", "");
+    if (int rc = split_geometry(prm->V, prm->num_slots)) return rc;
+    const size_t V = (size_t)prm->V, npk = (n + V - 1) / V;
+    if (npk == 0) return INA_OK;
+    if (!vals || !hdr || !pay) return set_error(INA_EINVAL, "null pointer%s", "");
+    if (!aligned16(hdr) || !aligned16(pay) || (desc && ((uintptr_t)desc & 7u)))
+        return set_error(INA_EINVAL, "header / payload rows 16-byte aligned, descriptors 8%s", "");
+    NgaHdr h{prm->bitmap, prm->seq0, prm->num_slots,
+             (uint32_t)prm->count | ((uint32_t)prm->flags << 8) | ((uint32_t)prm->switch_id << 16), prm->V};
+    const size_t nch = npk * V / 4;
+    hipLaunchKernelGGL((k_pack_nga_split<SrcI32>), dim3(grid_for(std::max(nch, npk), 1, ew_grid_cap())),
+                       dim3(kBlock), 0, hs(stream), SrcI32{vals}, n, h, ovf, reinterpret_cast<u32x4*>(hdr),
+                       reinterpret_cast<u32x4*>(pay), reinterpret_cast<u32x2*>(desc), nch, npk,
+                       aligned16(vals) ? 1 : 0);
+    return check_launch("pack_nga_split");
+}
+
+int ina_quantize_pack_nga_multi_split(const float* const* x, int W, const float* base, size_t n, int k,
+                                      const ina_nga_params_t* prm, uint8_t* const* hdr, uint8_t* const* pay,
+                                      ina_nga_desc_t* const* desc, ina_stream_t stream) {
+    if (int rc = check_k(k)) return rc;
+    if (!x || !prm || !hdr || !pay || W < 1 || W > INA_MAX_WORKERS)
+        return set_error(INA_EINVAL, "x, prm, hdr, pay non-null and W in [1, %s]", "64");
+    const int V = prm[0].V;
+    if (int rc = split_geometry(V, prm[0].num_slots)) return rc;
+    const size_t npk = (n + (size_t)V - 1) / (size_t)V;
+    if (npk == 0) return INA_OK;
+    if (base && !aligned16(base)) return set_error(INA_EINVAL, "base must be 16-byte aligned%s", "");
+    for (int w = 0; w < W; ++w) {
+        if (prm[w].V != V || prm[w].num_slots != prm[0].num_slots)
+            return set_error(INA_EINVAL, "every worker needs the same V and num_slots%s", "");
+        if (!x[w] || !hdr[w] || !pay[w]) return set_error(INA_EINVAL, "null worker buffer%s", "");
+        if (!aligned16(x[w]) || !aligned16(hdr[w]) || !aligned16(pay[w]))
+            return set_error(INA_EINVAL, "worker buffers and rows must be 16-byte aligned%s", "");
+        if (desc && (!desc[w] || ((uintptr_t)desc[w] & 7u)))
+            return set_error(INA_EINVAL, "descriptors must be non-null and 8-byte aligned%s", "");
+    }
+    const float sc = ldexpf(1.0f, k);
+    const size_t nch = npk * (size_t)V / 4;
+    const dim3 grid(grid_for(std::max(nch, npk), 1, ew_grid_cap())), blk(kBlock);
+    hipStream_t s = hs(stream);
+    for (int w0 = 0; w0 < W; w0 += kQpGroup) {
+        const int G = std::min(kQpGroup, W - w0);
+        QPackSplit a{};
+        for (int g = 0; g < G; ++g) {
+            const ina_nga_params_t& q = prm[w0 + g];
+            a.x[g] = x[w0 + g];
+            a.hdr[g] = reinterpret_cast<u32x4*>(hdr[w0 + g]);
+            a.pay[g] = reinterpret_cast<u32x4*>(pay[w0 + g]);
+            a.desc[g] = desc ? reinterpret_cast<u32x2*>(desc[w0 + g]) : nullptr;
+            a.bitmap[g] = q.bitmap;
+            a.seq0[g] = q.seq0;
+            a.fcs[g] = (uint32_t)q.count | ((uint32_t)q.flags << 8) | ((uint32_t)q.switch_id << 16);
+        }
+        switch (G) {
+#define INA_QPS(g_) case g_: hipLaunchKernelGGL(k_qpack_nga_multi_split<g_>, grid, blk, 0, s, a, base, n, sc, \
+                                                prm[0].num_slots, nch, npk); break;
+            INA_QPS(1) INA_QPS(2) INA_QPS(3) INA_QPS(4) INA_QPS(5) INA_QPS(6) INA_QPS(7) INA_QPS(8)
+#undef INA_QPS
+        }
+    }
+    return check_launch("quantize_pack_nga_multi_split");
+}
+
+int ina_unpack_nga_split(const uint8_t* hdr, const uint8_t* pay, size_t npk, int V,
+                         const ina_nga_fields_t* fields, int32_t* vals, ina_stream_t stream) {
+    if (V <= 0 || V % 4 || V > 256) return set_error(INA_EINVAL, "V must be a multiple of 4 in [4, 256]%s", "");
+    if (npk == 0) return INA_OK;
+    if (!hdr || (vals && !pay)) return set_error(INA_EINVAL, "null pointer%s", "");
+    if (!aligned16(hdr) || (pay && !aligned16(pay)) || (vals && !aligned16(vals)))
+        return set_error(INA_EINVAL, "rows and values must be 16-byte aligned%s", "");
+    hipStream_t s = hs(stream);
+    if (fields) {
+        NgaFieldsDev f{fields->bitmap, fields->count, fields->flags, fields->index, fields->switch_id,
+                       fields->frag_id};
+        hipLaunchKernelGGL(k_unpack_nga_hdr, dim3(grid_for(npk, 1)), dim3(kBlock), 0, s, hdr, npk, (size_t)16, f);
+    }
+    if (vals) {
+        const size_t nch = npk * (size_t)V / 4;
+        hipLaunchKernelGGL(k_unpack_nga_split_vals, dim3(grid_for(nch, 1, ew_grid_cap())), dim3(kBlock), 0, s,
+                           reinterpret_cast<const u32x4*>(pay), nch, reinterpret_cast<u32x4*>(vals));
+    }
+    return check_launch("unpack_nga_split");
 }
 
 int ina_unpack_nga(const uint8_t* pkts, size_t npk, int V, size_t pstride,

@@ -183,6 +183,106 @@ int ina_recv_packets_fd(int fd, uint8_t* host_pkts, size_t max_pkts, size_t stri
     return (int)(got > 0x7FFFFFFFu ? 0x7FFFFFFFu : got);
 }
 
+// split rows on the socket (include/ina.h): datagram p = header row p's 15 bytes || payload
+// row p's 4V bytes, two iovecs -- the bytes ina_send_packets_fd sends from packed rows
+int ina_send_packets_split_fd(int fd, const uint8_t* host_hdr, const uint8_t* host_pay, size_t npk, int V,
+                              uint32_t dst_ip) {
+    if (npk == 0) return 0;
+    if (!host_hdr || !host_pay || V <= 0) return ina::set_error(INA_EINVAL, "bad packet buffers%s", "");
+    const size_t plen = 4u * (size_t)V;
+    sockaddr_in dst;
+    memset(&dst, 0, sizeof dst);
+    dst.sin_family = AF_INET;
+    dst.sin_addr.s_addr = htonl(dst_ip);
+    int domain = AF_INET;
+    socklen_t dl = sizeof domain;
+    if (getsockopt(fd, SOL_SOCKET, SO_DOMAIN, &domain, &dl) == 0 && domain != AF_INET) dst_ip = 0;
+    constexpr size_t kBatch = 1024;
+    std::vector<mmsghdr> msgs(kBatch);
+    std::vector<iovec> iov(2 * kBatch);
+    size_t sent = 0;
+    while (sent < npk) {
+        size_t nb = npk - sent < kBatch ? npk - sent : kBatch;
+        for (size_t i = 0; i < nb; ++i) {
+            iov[2 * i].iov_base = const_cast<uint8_t*>(host_hdr) + (sent + i) * 16;
+            iov[2 * i].iov_len = INA_NGA_HDR_BYTES;
+            iov[2 * i + 1].iov_base = const_cast<uint8_t*>(host_pay) + (sent + i) * plen;
+            iov[2 * i + 1].iov_len = plen;
+            memset(&msgs[i], 0, sizeof(mmsghdr));
+            msgs[i].msg_hdr.msg_iov = &iov[2 * i];
+            msgs[i].msg_hdr.msg_iovlen = 2;
+            if (dst_ip) {
+                msgs[i].msg_hdr.msg_name = &dst;
+                msgs[i].msg_hdr.msg_namelen = sizeof dst;
+            }
+        }
+        int r = sendmmsg(fd, msgs.data(), (unsigned)nb, 0);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return ina::set_error(INA_ESOCK, "sendmmsg: %s", strerror(errno));
+        }
+        sent += (size_t)r;
+    }
+    if (sent > 0x7FFFFFFFu) sent = 0x7FFFFFFFu;
+    return (int)sent;
+}
+
+int ina_recv_packets_split_fd(int fd, uint8_t* host_hdr, uint8_t* host_pay, size_t max_pkts, int V,
+                              size_t skip, int timeout_ms, uint32_t* lens) {
+    if (max_pkts == 0) return 0;
+    if (!host_hdr || !host_pay || V <= 0) return ina::set_error(INA_EINVAL, "bad packet buffers%s", "");
+    const size_t plen = 4u * (size_t)V;
+    constexpr size_t kBatch = 1024;
+    std::vector<mmsghdr> msgs(kBatch);
+    std::vector<iovec> iov(3 * kBatch);
+    std::vector<uint8_t> skipbuf(skip ? skip : 1);
+    size_t got = 0;
+    timespec t0{};
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    const int64_t end_ns = (int64_t)t0.tv_sec * 1000000000LL + t0.tv_nsec +
+                           (int64_t)(timeout_ms < 0 ? 0 : timeout_ms) * 1000000LL;
+    while (got < max_pkts) {
+        size_t nb = max_pkts - got < kBatch ? max_pkts - got : kBatch;
+        for (size_t i = 0; i < nb; ++i) {
+            int k = 0;
+            if (skip) {
+                iov[3 * i].iov_base = skipbuf.data();
+                iov[3 * i].iov_len = skip;
+                k = 1;
+            }
+            iov[3 * i + k].iov_base = host_hdr + (got + i) * 16;
+            iov[3 * i + k].iov_len = INA_NGA_HDR_BYTES;
+            iov[3 * i + k + 1].iov_base = host_pay + (got + i) * plen;
+            iov[3 * i + k + 1].iov_len = plen;
+            memset(&msgs[i], 0, sizeof(mmsghdr));
+            msgs[i].msg_hdr.msg_iov = &iov[3 * i];
+            msgs[i].msg_hdr.msg_iovlen = (size_t)(k + 2);
+        }
+        int r = recvmmsg(fd, msgs.data(), (unsigned)nb, MSG_DONTWAIT, nullptr);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            if (errno != EAGAIN && errno != EWOULDBLOCK)
+                return ina::set_error(INA_ESOCK, "recvmmsg: %s", strerror(errno));
+            timespec now{};
+            clock_gettime(CLOCK_MONOTONIC, &now);
+            int64_t left = end_ns - ((int64_t)now.tv_sec * 1000000000LL + now.tv_nsec);
+            if (left <= 0) break;
+            pollfd pfd{fd, POLLIN, 0};
+            int pr = poll(&pfd, 1, (int)((left + 999999) / 1000000));
+            if (pr < 0 && errno != EINTR) return ina::set_error(INA_ESOCK, "poll: %s", strerror(errno));
+            if (pr == 0) break;
+            continue;
+        }
+        for (int i = 0; i < r; ++i) {
+            size_t len = msgs[i].msg_len;
+            len = len > skip ? len - skip : 0;
+            if (lens) lens[got + i] = (uint32_t)len;
+        }
+        got += (size_t)r;
+    }
+    return (int)(got > 0x7FFFFFFFu ? 0x7FFFFFFFu : got);
+}
+
 void send_gradients(uint32_t* gradient_array, int packet_num, uint32_t dst_ip, int worker_id,
                     uint32_t aggregator_index, int tensor_index) {
     int fd = socket(AF_INET, SOCK_RAW, IPPROTO_UDP);   // communicator.cc:10

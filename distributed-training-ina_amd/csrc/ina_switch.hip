@@ -1246,9 +1246,14 @@ struct PsFuse {
 // pid_batch(q0, nb, pid) gives the packet ids of the segment's packets q0 .. q0+nb-1 (wave-
 // uniform): the sorted run reads them from its window, the structured run (a batch of
 // dense ascending runs) from its run table.
-template <bool kPs, bool kLat, typename PidFn>
+// kSplit: split rows (include/ina.h) -- pkts holds 16-byte header rows (stride 16) and pay the
+// 4V-byte payload rows: lane l loads payload chunk l (values 4l..4l+3, one byte swap each,
+// no neighbour lane), lane b < kB the header row of packet b, and a forwarded packet
+// rewrites only its payload row.
+template <bool kPs, bool kLat, bool kSplit, typename PidFn>
 __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
-                                            size_t stride, uint8_t* __restrict__ actions, const PsFuse& ps,
+                                            size_t stride, uint8_t* __restrict__ pay,
+                                            uint8_t* __restrict__ actions, const PsFuse& ps,
                                             uint32_t slot, bool ack_led, size_t q_begin, size_t q_end,
                                             PidFn&& pid_batch) {
     constexpr bool kActBatch = INA_SWITCH_ACT_BATCH;
@@ -1289,6 +1294,14 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
 #pragma unroll
         for (int b = 1; b < kB; ++b) mypid = lane == b ? pid[b] : mypid;
         uint32_t act_v = 0;                      // lane b: packet b's action (kActBatch)
+        if constexpr (kSplit) {                  // lane b: packet b's header row
+            tl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * 16);
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const u32x4s* pk = reinterpret_cast<const u32x4s*>(pay + (size_t)pid[b] * (size_t)(4 * V));
+                a[b] = sw_ld(pk + (vl ? lane : 0));
+            }
+        } else {
         if (wide) {
 #if INA_SWITCH_TAIL_NT
             tl = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride) + 64);
@@ -1301,6 +1314,7 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
             const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[b] * stride);
             a[b] = sw_ld(pk + (lane <= L ? lane : 0));
         }
+        }
         if constexpr (kLat) {
             if (!st_ready) {
                 cnt = __builtin_amdgcn_readfirstlane(cnt_ld);
@@ -1311,9 +1325,9 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
             if (b >= nb) break;
-            const uint32_t h1 = __builtin_amdgcn_readlane(a[b].y, 0),
-                           h2 = __builtin_amdgcn_readlane(a[b].z, 0),
-                           h3 = __builtin_amdgcn_readlane(a[b].w, 0);
+            const uint32_t h1 = kSplit ? __builtin_amdgcn_readlane(tl.y, b) : __builtin_amdgcn_readlane(a[b].y, 0),
+                           h2 = kSplit ? __builtin_amdgcn_readlane(tl.z, b) : __builtin_amdgcn_readlane(a[b].z, 0),
+                           h3 = kSplit ? __builtin_amdgcn_readlane(tl.w, b) : __builtin_amdgcn_readlane(a[b].w, 0);
             const uint32_t hcount = h1 & 0xFFu, flags = (h1 >> 8) & 0xFFu;
             // keep the state machine scalar (SGPRs + scalar branches)
             const uint32_t frag_in =
@@ -1327,17 +1341,22 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
                 if (frag != frag_in) {                   // collision (ngaa.p4:177-181):
                     act = INA_ACT_FWD_COLLISION;         // only the flag byte changes
                     if (lane == 0)
-                        reinterpret_cast<uint32_t*>(pkts + (size_t)pid[b] * stride)[1] =
-                            a[b].y | ((uint32_t)INA_FLAG_COLLISION << 8);
+                        reinterpret_cast<uint32_t*>(pkts + (size_t)pid[b] * (kSplit ? 16 : stride))[1] =
+                            h1 | ((uint32_t)INA_FLAG_COLLISION << 8);
                 } else {
                     cnt = (cnt + 1u) & 0xFFu;            // read_add_count (ngaa.p4:66-78)
                     if (cnt == hcount) cnt = 0;
                     cnt = __builtin_amdgcn_readfirstlane(cnt);
                     const bool first = cnt == 1u;
+                    u32x4s v;                            // values 4l..4l+3
+                    uint32_t tw = 0;                     // old byte 1039 (padding) for the tail
+                    if constexpr (kSplit) {
+                        v.x = __builtin_bswap32(a[b].x); v.y = __builtin_bswap32(a[b].y);
+                        v.z = __builtin_bswap32(a[b].z); v.w = __builtin_bswap32(a[b].w);
+                    } else {
                     u32x4s c;                            // chunk l+1
                     c.x = from_next_lane(a[b].x); c.y = from_next_lane(a[b].y);
                     c.z = from_next_lane(a[b].z); c.w = from_next_lane(a[b].w);
-                    uint32_t tw = 0;                     // old byte 1039 (padding) for the tail
                     if (wide) {
                         const uint32_t tx = __builtin_amdgcn_readlane(tl.x, b);
                         const uint32_t ty = __builtin_amdgcn_readlane(tl.y, b);
@@ -1345,11 +1364,11 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
                         tw = __builtin_amdgcn_readlane(tl.w, b);
                         if (lane == 63) c = u32x4s{tx, ty, tz, tw};
                     }
-                    u32x4s v;                            // values 4l..4l+3
                     v.x = dec_be(c.x, a[b].w);
                     v.y = dec_be(c.y, c.x);
                     v.z = dec_be(c.z, c.y);
                     v.w = dec_be(c.w, c.z);
+                    }
                     if (first) {                         // processor.p4:16-21
                         reg = v;
                     } else if (have_reg) {
@@ -1389,8 +1408,9 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
                             }
                             if (lane == 0 && ps.acks) {      // the PS ack (fragcheck.p4:26-31)
                                 u32x4s hd = a[b];
+                                if constexpr (kSplit) hd = u32x4s{(uint32_t)__builtin_amdgcn_readlane(tl.x, b), h1, h2, h3};
                                 hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
-                                hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                                if constexpr (!kSplit) hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
                                 *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
                                 // its descriptor, so the next switch batch (these acks in
                                 // front of the next step's packets) needs no gather pass
@@ -1398,7 +1418,12 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
                             }
                         }
                     }
-                    if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
+                    if (kSplit && (act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
+                        // out_value -> payload (processor.p4:22): the payload row, word for word
+                        const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
+                                       __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
+                        if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid[b] * (size_t)(4 * V)) + lane);
+                    } else if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
                         // out_value -> payload (processor.p4:22): chunk c from lane c-1
                         u32x4s p;
                         p.x = from_prev_lane(reg.x); p.y = from_prev_lane(reg.y);
@@ -1470,9 +1495,10 @@ __device__ __forceinline__ uint32_t from_prev_in_row(uint32_t x) {
 constexpr int kNarrowMaxV = 32;
 static_assert(kB == 8, "the narrow run puts a batch of 8 packets in 8 lane groups");
 
-template <bool kPs, typename PidFn>
+template <bool kPs, bool kSplit, typename PidFn>
 __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
-                                                   size_t stride, uint8_t* __restrict__ actions,
+                                                   size_t stride, uint8_t* __restrict__ pay,
+                                                   uint8_t* __restrict__ actions,
                                                    const PsFuse& ps, uint32_t slot, bool ack_led,
                                                    size_t q_begin, size_t q_end, PidFn&& pid_batch) {
     const int lane = threadIdx.x & 63;
@@ -1496,18 +1522,25 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
             mypid = g == b ? pid[b] : mypid;
             lanepid = lane == b ? pid[b] : lanepid;
         }
-        const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride);
-        const u32x4s a = sw_ld(pk + (vl ? l : 0));   // chunk l (lanes past L re-read chunk 0)
-        const u32x4s tl = *(pk + L);                  // the tail chunk (one request per group)
+        u32x4s a, tl;
+        if constexpr (kSplit) {                       // payload chunk l; the group's header row
+            a = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)mypid * (size_t)(4 * V)) + (vl ? l : 0));
+            tl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * 16);
+        } else {
+            const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride);
+            a = sw_ld(pk + (vl ? l : 0));             // chunk l (lanes past L re-read chunk 0)
+            tl = *(pk + L);                           // the tail chunk (one request per group)
+        }
+        const u32x4s hw = kSplit ? tl : a;            // header words (lane 8b: packet b's)
         // the state machine, packet by packet in arrival order (SGPRs, scalar branches)
         uint32_t m_add = 0, m_first = 0, m_fwd = 0, m_coll = 0, m_ps = 0;
         uint32_t act_v = 0, ps_slot_v = 0;
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
             if (b >= nb) break;
-            const uint32_t h1 = __builtin_amdgcn_readlane(a.y, 8 * b),
-                           h2 = __builtin_amdgcn_readlane(a.z, 8 * b),
-                           h3 = __builtin_amdgcn_readlane(a.w, 8 * b);
+            const uint32_t h1 = __builtin_amdgcn_readlane(hw.y, 8 * b),
+                           h2 = __builtin_amdgcn_readlane(hw.z, 8 * b),
+                           h3 = __builtin_amdgcn_readlane(hw.w, 8 * b);
             const uint32_t hcount = h1 & 0xFFu, flags = (h1 >> 8) & 0xFFu;
             const uint32_t frag_in =
                 __builtin_amdgcn_readfirstlane(__builtin_bswap32((h2 >> 24) | (h3 << 8)));
@@ -1541,16 +1574,22 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
         }
         if (lane < nb) actions[lanepid] = (uint8_t)act_v;   // one store for the batch
         if (((m_coll >> g) & 1u) && l == 0)                // only the flag byte changes
-            reinterpret_cast<uint32_t*>(pkts + (size_t)mypid * stride)[1] = a.y | ((uint32_t)INA_FLAG_COLLISION << 8);
+            reinterpret_cast<uint32_t*>(pkts + (size_t)mypid * (kSplit ? 16 : stride))[1] =
+                hw.y | ((uint32_t)INA_FLAG_COLLISION << 8);
         if (m_add) {
             // values 4l..4l+3 of packet g: chunk l and chunk l+1 (the neighbour lane, or the
             // tail for the group's last value lane)
-            u32x4s c;
-            c.x = from_next_in_row(a.x); c.y = from_next_in_row(a.y);
-            c.z = from_next_in_row(a.z); c.w = from_next_in_row(a.w);
-            if (l == L - 1) c = tl;
             u32x4s x;
-            x.x = dec_be(c.x, a.w); x.y = dec_be(c.y, c.x); x.z = dec_be(c.z, c.y); x.w = dec_be(c.w, c.z);
+            if constexpr (kSplit) {
+                x.x = __builtin_bswap32(a.x); x.y = __builtin_bswap32(a.y);
+                x.z = __builtin_bswap32(a.z); x.w = __builtin_bswap32(a.w);
+            } else {
+                u32x4s c;
+                c.x = from_next_in_row(a.x); c.y = from_next_in_row(a.y);
+                c.z = from_next_in_row(a.z); c.w = from_next_in_row(a.w);
+                if (l == L - 1) c = tl;
+                x.x = dec_be(c.x, a.w); x.y = dec_be(c.y, c.x); x.z = dec_be(c.z, c.y); x.w = dec_be(c.w, c.z);
+            }
             const bool add = (m_add >> g) & 1u;
             uint32_t f = (m_first >> g) & 1u;
             if (!add) x = u32x4s{0u, 0u, 0u, 0u};
@@ -1597,14 +1636,18 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
                                                    __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
                 }
                 if (l == 0 && ps.acks) {             // the PS ack (fragcheck.p4:26-31)
-                    u32x4s hd = a;
+                    u32x4s hd = hw;
                     hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
-                    hd.w = (hd.w & 0x00FFFFFFu) | (S.x & 0xFF000000u);
+                    if constexpr (!kSplit) hd.w = (hd.w & 0x00FFFFFFu) | (S.x & 0xFF000000u);
                     *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot_v * ps.ack_stride) = hd;
                     if (ps.ack_desc) ps.ack_desc[ps_slot_v] = uint2{hd.y, hd.z};
                 }
             }
-            if ((m_fwd >> g) & 1u) {                 // out_value -> payload (processor.p4:22)
+            if (kSplit && ((m_fwd >> g) & 1u)) {     // out_value -> the payload row (processor.p4:22)
+                const u32x4s e{__builtin_bswap32(S.x), __builtin_bswap32(S.y), __builtin_bswap32(S.z),
+                               __builtin_bswap32(S.w)};
+                if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)mypid * (size_t)(4 * V)) + l);
+            } else if ((m_fwd >> g) & 1u) {          // out_value -> payload (processor.p4:22)
                 u32x4s p;                            // values of lane l-1
                 p.x = from_prev_in_row(S.x); p.y = from_prev_in_row(S.y);
                 p.z = from_prev_in_row(S.z); p.w = from_prev_in_row(S.w);
@@ -1638,9 +1681,9 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
         __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
 }
 
-template <bool kPs, bool kLat = false, bool kNarrow = false>
+template <bool kPs, bool kLat = false, bool kNarrow = false, bool kSplit = false>
 __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
-                                                 size_t npk, size_t stride,
+                                                 uint8_t* __restrict__ pay, size_t npk, size_t stride,
                                                  const uint32_t* __restrict__ keys,
                                                  const uint32_t* __restrict__ ids,
                                                  uint8_t* __restrict__ actions, uint32_t win,
@@ -1709,9 +1752,11 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
             }
         };
         if constexpr (kNarrow)
-            run_segment_narrow<kPs>(st, pkts, stride, actions, ps, slot, ack_led, pos + (ack_led ? 1 : 0), end, pids);
+            run_segment_narrow<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led,
+                                            pos + (ack_led ? 1 : 0), end, pids);
         else
-            run_segment<kPs, kLat>(st, pkts, stride, actions, ps, slot, ack_led, pos + (ack_led ? 1 : 0), end, pids);
+            run_segment<kPs, kLat, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led,
+                                           pos + (ack_led ? 1 : 0), end, pids);
         }
     }
 }
@@ -1721,9 +1766,10 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
 // slots (one pass of the grid) and runs slot s's segment -- the packets start_r + s -
 // first_r of the runs that hold s, in run order = arrival order -- through run_segment.
 // A PS ack leading its segment is done without reading it, as in switch_run2_body.
-template <bool kPs, bool kNarrow>
+template <bool kPs, bool kNarrow, bool kSplit>
 __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
-                                                 size_t stride, uint8_t* __restrict__ actions,
+                                                 size_t stride, uint8_t* __restrict__ pay,
+                                                 uint8_t* __restrict__ actions,
                                                  uint32_t kmask, const PsFuse& ps,
                                                  const uint32_t* __restrict__ runs, size_t wave,
                                                  size_t nwaves) {
@@ -1785,9 +1831,9 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
             }
         };
         if constexpr (kNarrow)
-            run_segment_narrow<kPs>(st, pkts, stride, actions, ps, slot, ack_led, 0, nseg, pids);
+            run_segment_narrow<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led, 0, nseg, pids);
         else
-            run_segment<kPs, false>(st, pkts, stride, actions, ps, slot, ack_led, 0, nseg, pids);
+            run_segment<kPs, false, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led, 0, nseg, pids);
     }
 }
 
@@ -1808,9 +1854,10 @@ __device__ __forceinline__ size_t switch_block_index() {
 #endif
 }
 
-template <bool kPs, bool kNarrow>
+template <bool kPs, bool kNarrow, bool kSplit>
 __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? INA_SWITCH_WAVES : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
-                                                          uint8_t* __restrict__ pkts, size_t npk,
+                                                          uint8_t* __restrict__ pkts,
+                                                          uint8_t* __restrict__ pay, size_t npk,
                                                           size_t stride,
                                                           const uint32_t* __restrict__ keys,
                                                           const uint32_t* __restrict__ ids,
@@ -1832,23 +1879,24 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
             ids = ids_a;
         } else if (unsorted[2] == ep) {
             // a batch of dense ascending runs: the bucket pass wrote the run table, not a sort
-            switch_runs_body<kPs, kNarrow>(st, pkts, stride, actions, kmask, ps, unsorted + (kCtlRuns - kCtlEpochs),
-                                  wave, nwaves);
+            switch_runs_body<kPs, kNarrow, kSplit>(st, pkts, stride, pay, actions, kmask, ps,
+                                                   unsorted + (kCtlRuns - kCtlEpochs), wave, nwaves);
             return;
         }
     }
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
-    switch_run2_body<kPs, false, kNarrow>(st, pkts, npk, stride, keys, ids, actions, win, kmask, ps, wave, nwaves);
+    switch_run2_body<kPs, false, kNarrow, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps,
+                                                  wave, nwaves);
 }
 
 // batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
 // one 16-wave workgroup -- the bitonic (slot, packet id) sort in LDS, then the run
 // kernel's work on the same 16 waves with the sorted arrays read from LDS.
-template <bool kPs, typename T, int kIdBits>
+template <bool kPs, typename T, int kIdBits, bool kSplit>
 __global__ __launch_bounds__(kSmallBlock) void k_switch_tiny(ina_switch_state_t st, uint8_t* __restrict__ pkts,
-                                                             uint32_t npk, size_t stride,
+                                                             uint8_t* __restrict__ pay, uint32_t npk, size_t stride,
                                                              uint8_t* __restrict__ actions, uint32_t win,
                                                              PsFuse ps) {
     // the sorted (slot, packet id) arrays stay in LDS: the run loop's window loads are LDS
@@ -1856,8 +1904,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_switch_tiny(ina_switch_state_t 
     __shared__ uint32_t keys_s[INA_SWITCH_SMALL_MAX], ids_s[INA_SWITCH_SMALL_MAX];
     switch_sort_small_body<T, kIdBits>(pkts, npk, stride, st.num_slots, st.switch_id, actions, keys_s, ids_s);
     __syncthreads();
-    switch_run2_body<kPs, true>(st, pkts, npk, stride, keys_s, ids_s, actions, win, 0xFFFFFFFFu, ps,
-                                wave_in_block(), kSmallBlock / 64);
+    switch_run2_body<kPs, true, false, kSplit>(st, pkts, pay, npk, stride, keys_s, ids_s, actions, win,
+                                               0xFFFFFFFFu, ps, wave_in_block(), kSmallBlock / 64);
 }
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -2012,16 +2060,23 @@ size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots) {
 // descriptors, so it may run before or beside the kernels that fill the payload); 2 the run
 // alone over a scratch a phase-1 call filled for the same batch (paths whose sort reads the
 // packets -- the one-workgroup small-batch paths -- sort in phase 2 instead)
+// pay != NULL: split rows -- pkts are the 16-byte header rows (stride 16), pay the 4V-byte
+// payload rows (include/ina.h "split NGA rows"); only the register-resident run kernels
+// take them
 static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
                                const uint64_t* desc, uint8_t* actions, void* scratch,
-                               ina_stream_t stream, const PsFuse& ps, bool* fused_out, int phase = 0) {
+                               ina_stream_t stream, const PsFuse& ps, bool* fused_out, int phase = 0,
+                               uint8_t* pay = nullptr) {
     *fused_out = false;
+    const bool split = pay != nullptr;
+    if (split && (!st || st->V % 4 || st->V <= 0 || st->V > kMaxV || stride != 16 || ((uintptr_t)pay & 15u)))
+        return set_error(INA_EINVAL, "split rows need V a multiple of 4 <= 256 and 16-byte aligned rows%s", "");
     if (phase == 1 && !desc && npk)
         return set_error(INA_EINVAL, "the separate slot sort needs the batch's descriptors%s", "");
     const bool do_sort = phase != 2, do_run = phase != 1;
     if (!st || st->V <= 0 || st->V > kMaxV || st->num_slots == 0)
         return set_error(INA_EINVAL, "bad switch state (V in [1,256])%s", "");
-    if (stride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)st->V)
+    if (!split && stride < (size_t)INA_NGA_HDR_BYTES + 4u * (size_t)st->V)
         return set_error(INA_EINVAL, "stride must be >= 15+4V%s", "");
     if (stride > 0xFFFFFFFFu) return set_error(INA_EINVAL, "stride too large%s", "");
     if (npk == 0) return INA_OK;
@@ -2049,6 +2104,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     uint32_t *kc = k_in, *vc = v_in, *kn = k_out, *vn = v_out;
     const bool fast = stride % 16 == 0 && ((uintptr_t)pkts & 15u) == 0 && st->V % 4 == 0 &&
                       st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
+    if (split && !fast) return set_error(INA_EINVAL, "split rows need 16-byte aligned rows and registers%s", "");
     // keys carry the PS-ack bit for the run kernel when bit 31 is outside every digit
     const bool ack_hint = fast && sp.passes * sp.bits <= 31 && g_ack_fast.load();
     const bool small = npk <= (size_t)g_small_sort.load();
@@ -2064,13 +2120,16 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         uint32_t win = (uint32_t)INA_SWITCH_WIN_SMALL;
         if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
         const bool narrow = (uint64_t)st->num_slots + 1 <= (1u << 20);
+#define INA_TINY(P_, T_, B_, S_) hipLaunchKernelGGL((k_switch_tiny<P_, T_, B_, S_>), dim3(1), dim3(kSmallBlock), 0, s, \
+                                                   *st, pkts, pay, (uint32_t)npk, stride, actions, win, ps)
         if (ps.on) {
-            if (narrow) hipLaunchKernelGGL((k_switch_tiny<true, uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
-            else hipLaunchKernelGGL((k_switch_tiny<true, unsigned long long, 32>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
+            if (narrow) { if (split) INA_TINY(true, uint32_t, 12, true); else INA_TINY(true, uint32_t, 12, false); }
+            else { if (split) INA_TINY(true, unsigned long long, 32, true); else INA_TINY(true, unsigned long long, 32, false); }
         } else {
-            if (narrow) hipLaunchKernelGGL((k_switch_tiny<false, uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
-            else hipLaunchKernelGGL((k_switch_tiny<false, unsigned long long, 32>), dim3(1), dim3(kSmallBlock), 0, s, *st, pkts, (uint32_t)npk, stride, actions, win, ps);
+            if (narrow) { if (split) INA_TINY(false, uint32_t, 12, true); else INA_TINY(false, uint32_t, 12, false); }
+            else { if (split) INA_TINY(false, unsigned long long, 32, true); else INA_TINY(false, unsigned long long, 32, false); }
         }
+#undef INA_TINY
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch tiny launch%s", "");
         *fused_out = ps.on != 0;
         return INA_OK;
@@ -2188,9 +2247,11 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // V <= 32 (NGA-32, the P4 program's format): 8 packets of a segment side by side per
         // wave (run_segment_narrow); wider packets: a packet per wave instruction
         const bool narrow = st->V <= kNarrowMaxV;
-        auto* run = ps.on ? (narrow ? &k_switch_run2<true, true> : &k_switch_run2<true, false>)
-                          : (narrow ? &k_switch_run2<false, true> : &k_switch_run2<false, false>);
-        hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, npk, stride, kc, vc, actions,
+        auto* run = split ? (ps.on ? (narrow ? &k_switch_run2<true, true, true> : &k_switch_run2<true, false, true>)
+                                   : (narrow ? &k_switch_run2<false, true, true> : &k_switch_run2<false, false, true>))
+                          : (ps.on ? (narrow ? &k_switch_run2<true, true, false> : &k_switch_run2<true, false, false>)
+                                   : (narrow ? &k_switch_run2<false, true, false> : &k_switch_run2<false, false, false>));
+        hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, pay, npk, stride, kc, vc, actions,
                            win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted);
         *fused_out = ps.on != 0;
     } else {
@@ -2227,7 +2288,8 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
                              const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
                              uint32_t seq0, const float* local, int k, double weight_step,
                              float* out, size_t n, uint8_t* acks, size_t ack_stride,
-                             ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream, int phase);
+                             ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream, int phase,
+                             uint8_t* pay = nullptr);
 
 int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
                                   const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
@@ -2284,7 +2346,8 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
                              const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
                              uint32_t seq0, const float* local, int k, double weight_step,
                              float* out, size_t n, uint8_t* acks, size_t ack_stride,
-                             ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream, int phase) {
+                             ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream, int phase,
+                             uint8_t* pay) {
     if (k < -126 || k > 127) return set_error(INA_EINVAL, "k out of range [-126,127]%s", "");
     if (npk == 0) return INA_OK;
     if (!local || !out) return set_error(INA_EINVAL, "null pointer%s", "");
@@ -2306,14 +2369,33 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
               nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,
               keep_forwarded ? 1 : 0, reinterpret_cast<uint2*>(ack_desc)};
     bool fused = false;
-    if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused, phase))
+    if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused, phase, pay))
         return rc;
     if (fused) return INA_OK;
+    if (pay) return set_error(INA_EHIP, "split rows: the PS step was not fused%s", "");
     // layouts the register-resident run kernel does not take: the two steps one by one
     if (int rc = ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,
                                          n, acks, ack_stride, stream))
         return rc;
     return ack_desc ? ina_nga_descriptors(acks, nslots, ack_stride, ack_desc, stream) : INA_OK;
+}
+
+int ina_switch_process_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npk,
+                             const ina_nga_desc_t* desc, uint8_t* actions, void* scratch, ina_stream_t stream) {
+    if (npk && !pay) return set_error(INA_EINVAL, "null payload rows%s", "");
+    PsFuse off{};
+    bool fused = false;
+    return switch_process_impl(st, hdr, npk, 16, desc, actions, scratch, stream, off, &fused, 0, pay);
+}
+
+int ina_switch_process_apply_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npk,
+                                   const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                                   uint32_t seq0, const float* local, int k, double weight_step,
+                                   float* out, size_t n, uint8_t* ack_hdr, ina_nga_desc_t* ack_desc,
+                                   int keep_forwarded, ina_stream_t stream) {
+    if (npk && !pay) return set_error(INA_EINVAL, "null payload rows%s", "");
+    return switch_apply_impl(st, hdr, npk, 16, desc, actions, scratch, seq0, local, k, weight_step, out, n,
+                             ack_hdr, 16, ack_desc, keep_forwarded, stream, 0, pay);
 }
 
 int ina_switch_batch_path(const void* scratch, size_t npk, uint32_t num_slots, int* path) {

@@ -81,6 +81,14 @@ SIGNATURES = {
     "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
     "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],
+    "ina_pack_nga_split": [_vp, _sz, C.POINTER(NgaParams), _vp, _vp, _vp, _vp, _vp],
+    "ina_quantize_pack_nga_multi_split": [_vp, _i, _vp, _sz, _i, _vp, _vp, _vp, _vp, _vp],
+    "ina_unpack_nga_split": [_vp, _vp, _sz, _i, C.POINTER(NgaFields), _vp, _vp],
+    "ina_switch_process_split": [C.POINTER(SwitchState), _vp, _vp, _sz, _vp, _vp, _vp, _vp],
+    "ina_switch_process_apply_split": [C.POINTER(SwitchState), _vp, _vp, _sz, _vp, _vp, _vp, _u32, _vp, _i,
+                                       _d, _vp, _sz, _vp, _vp, _i, _vp],
+    "ina_send_packets_split_fd": [_i, _vp, _vp, _sz, _i, _u32],
+    "ina_recv_packets_split_fd": [_i, _vp, _vp, _sz, _i, _sz, _i, _vp],
     "ina_switch_scratch_bytes": [_sz, _u32],
     "ina_switch_batch_path": [_vp, _sz, _u32, C.POINTER(C.c_int)],
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],

@@ -409,6 +409,104 @@ def quantize_pack_nga_multi(xs, k: int, V: int, bitmaps, count: int, switch_id: 
     return (outs, ds) if ds is not None else outs
 
 
+# ---- split NGA rows (include/ina.h): 16-byte header rows + 4V-byte payload rows -------------
+def _split_rows(npk, V, dev, hdr=None, pay=None):
+    if V % 4 or not 4 <= V <= 256:
+        raise ValueError("split rows need V a multiple of 4 in [4, 256]")
+    hdr = torch.zeros((npk, 16), dtype=torch.uint8, device=dev) if hdr is None else hdr
+    pay = torch.empty((npk, 4 * V), dtype=torch.uint8, device=dev) if pay is None else pay
+    for t, name, row in ((hdr, "hdr", 16), (pay, "pay", 4 * V)):
+        _req(t, torch.uint8, name)
+        if t.dim() != 2 or t.shape[1] != row or t.shape[0] < npk or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous uint8 [>= {npk}, {row}] tensor")
+        if t.data_ptr() % 16:
+            raise ValueError(f"{name} rows must be 16-byte aligned")
+    return hdr, pay
+
+
+def pack_nga_split(vals: torch.Tensor, V: int, bitmap: int, count: int, switch_id: int, seq0: int,
+                   flags: int = 0, num_slots: int = NUM_REGISTER, overflow: torch.Tensor | None = None,
+                   hdr: torch.Tensor | None = None, pay: torch.Tensor | None = None, desc=None):
+    """pack_nga into split rows (ina_pack_nga_split): returns (hdr uint8 [npkts, 16], pay uint8
+    [npkts, 4V]) -- hdr[p, :15] || pay[p] is packet p's datagram, byte for byte the packed
+    row's first 15 + 4V bytes -- or (hdr, pay, desc) with desc as in pack_nga."""
+    _req(vals, torch.int32, "vals")
+    npk = (vals.numel() + V - 1) // V
+    hdr, pay = _split_rows(npk, V, vals.device, hdr, pay)
+    prm = _lib.NgaParams(bitmap & 0xFFFFFFFF, count & 0xFF, flags & 0xFF, switch_id & 0xFF, 0,
+                         seq0 & 0xFFFFFFFF, num_slots, V)
+    ovp = None
+    if overflow is not None:
+        _req(overflow, torch.uint8, "overflow")
+        _fits(overflow, npk, "overflow")
+        ovp = overflow.data_ptr()
+    d = _desc_arg(desc, npk, vals.device)
+    check(load().ina_pack_nga_split(vals.data_ptr(), vals.numel(), C.byref(prm), ovp, hdr.data_ptr(),
+                                    pay.data_ptr(), d.data_ptr() if d is not None else None, _stream(vals)),
+          "pack_nga_split")
+    return (hdr, pay, d) if d is not None else (hdr, pay)
+
+
+def quantize_pack_nga_multi_split(xs, k: int, V: int, bitmaps, count: int, switch_id: int, seq0,
+                                  base: torch.Tensor | None = None, flags: int = 0,
+                                  num_slots: int = NUM_REGISTER, hdrs=None, pays=None, descs=None):
+    """quantize_pack_nga_multi into split rows (ina_quantize_pack_nga_multi_split): W
+    workers' quantize(xs[w] - base, k) as header rows hdrs[w] + payload rows pays[w], the
+    base read once per 8 workers.  Returns (hdrs, pays) or (hdrs, pays, descs)."""
+    xs, n = _bufs(xs, torch.float32, "xs")
+    W, dev = len(xs), xs[0].device
+    if base is not None:
+        _req(base, torch.float32, "base")
+        if base.numel() != n:
+            raise ValueError("base and xs differ in length")
+        _same_device(xs[0], base)
+    bitmaps = list(bitmaps)
+    seqs = [int(seq0)] * W if isinstance(seq0, numbers.Integral) else list(seq0)
+    if len(bitmaps) != W or len(seqs) != W:
+        raise ValueError("one bitmap and one seq0 per worker")
+    npk = (n + V - 1) // V
+    hdrs = [None] * W if hdrs is None else list(hdrs)
+    pays = [None] * W if pays is None else list(pays)
+    if len(hdrs) != W or len(pays) != W:
+        raise ValueError("one header and one payload array per worker")
+    rows = [_split_rows(npk, V, dev, h, p) for h, p in zip(hdrs, pays)]
+    hdrs, pays = [r[0] for r in rows], [r[1] for r in rows]
+    ds = None
+    if descs is not None and descs is not False:
+        if descs is not True and (len(descs) != W or any(d is None for d in descs)):
+            raise ValueError("descs: True, or one int64 tensor per worker")
+        ds = [_desc_arg(True if descs is True else descs[w], npk, dev) for w in range(W)]
+    prm = (_lib.NgaParams * W)(*[_lib.NgaParams(bitmaps[w] & 0xFFFFFFFF, count & 0xFF, flags & 0xFF,
+                                                switch_id & 0xFF, 0, seqs[w] & 0xFFFFFFFF, num_slots, V)
+                                 for w in range(W)])
+    check(load().ina_quantize_pack_nga_multi_split(
+        ptr_array([x.data_ptr() for x in xs]), W, base.data_ptr() if base is not None else None, n, k,
+        prm, ptr_array([h.data_ptr() for h in hdrs]), ptr_array([p.data_ptr() for p in pays]),
+        ptr_array([d.data_ptr() for d in ds]) if ds is not None else None, _stream(xs[0])),
+        "quantize_pack_nga_multi_split")
+    return (hdrs, pays, ds) if ds is not None else (hdrs, pays)
+
+
+def unpack_nga_split(hdr: torch.Tensor, pay: torch.Tensor, V: int, with_values: bool = True):
+    """The PS parse of split rows: (fields dict of device tensors, int32 values [npkts*V] or
+    None) -- what unpack_nga returns for the packed rows."""
+    npk = hdr.shape[0]
+    hdr, pay = _split_rows(npk, V, hdr.device, hdr, pay)
+    dev = hdr.device
+    f = {"bitmap": torch.empty(npk, dtype=torch.int32, device=dev),
+         "count": torch.empty(npk, dtype=torch.uint8, device=dev),
+         "flags": torch.empty(npk, dtype=torch.uint8, device=dev),
+         "index": torch.empty(npk, dtype=torch.int32, device=dev),
+         "switch_id": torch.empty(npk, dtype=torch.uint8, device=dev),
+         "frag_id": torch.empty(npk, dtype=torch.int32, device=dev)}
+    fs = _lib.NgaFields(*[f[k].data_ptr() for k in ("bitmap", "count", "flags", "index", "switch_id", "frag_id")])
+    vals = torch.empty(npk * V, dtype=torch.int32, device=dev) if with_values else None
+    check(load().ina_unpack_nga_split(hdr.data_ptr(), pay.data_ptr(), npk, V, C.byref(fs),
+                                      vals.data_ptr() if vals is not None else None, _stream(hdr)),
+          "unpack_nga_split")
+    return f, vals
+
+
 def make_descriptors(n_packets: int, W: int, count: int, switch_id: int, seq0,
                      flags: int = 0, num_slots: int = NUM_REGISTER, outs=None,
                      device: str | torch.device = "cuda", stream: torch.cuda.Stream | None = None):
@@ -790,6 +888,64 @@ class Switch:
                                                       out.data_ptr(), local.numel(), ack_ptr, ack_stride,
                                                       ad, int(keep_forwarded), st),
               "switch_process_apply")
+        self._end(ts)
+        return actions, out
+
+
+    def process_split(self, hdr: torch.Tensor, pay: torch.Tensor, actions: torch.Tensor | None = None,
+                      desc: torch.Tensor | None = None) -> torch.Tensor:
+        """process() over split rows (ina_switch_process_split): header rows uint8 [npkts, 16]
+        and payload rows uint8 [npkts, 4V]; same actions, registers and forwarded bytes."""
+        npk = hdr.shape[0]
+        hdr, pay = _split_rows(npk, self.V, hdr.device, hdr, pay)
+        d = _desc_arg(desc, npk, hdr.device)
+        actions = torch.empty(npk, dtype=torch.uint8, device=hdr.device) if actions is None else actions
+        _req(actions, torch.uint8, "actions")
+        _fits(actions, npk, "actions")
+        _same_device(hdr, pay, actions)
+        scratch = self._scratch_for(npk, hdr.device)
+        self._sorted = None
+        ts = torch.cuda.current_stream(hdr.device)
+        st = self._begin(ts)
+        check(load().ina_switch_process_split(C.byref(self._state), hdr.data_ptr(), pay.data_ptr(), npk,
+                                              d.data_ptr() if d is not None else None, actions.data_ptr(),
+                                              scratch.data_ptr(), st), "switch_process_split")
+        self._end(ts)
+        return actions
+
+    def process_apply_split(self, hdr: torch.Tensor, pay: torch.Tensor, seq0: int, local: torch.Tensor,
+                            k: int, weight_step: float, out: torch.Tensor | None = None,
+                            ack_hdr: torch.Tensor | None = None, ack_desc: torch.Tensor | None = None,
+                            keep_forwarded: bool = True, actions: torch.Tensor | None = None,
+                            desc: torch.Tensor | None = None):
+        """process_apply() over split rows (ina_switch_process_apply_split): the PS ack rows are
+        header rows (uint8 [slots, 16]) with their descriptors in ack_desc.  Returns (actions, out)."""
+        _req(local, torch.float32, "local")
+        npk = hdr.shape[0]
+        hdr, pay = _split_rows(npk, self.V, hdr.device, hdr, pay)
+        actions = torch.empty(npk, dtype=torch.uint8, device=hdr.device) if actions is None else actions
+        _req(actions, torch.uint8, "actions")
+        _fits(actions, npk, "actions")
+        out = torch.empty_like(local) if out is None else out
+        _req(out, torch.float32, "out")
+        if out.numel() != local.numel():
+            raise ValueError("out must have local's size")
+        if ack_hdr is not None:
+            _req(ack_hdr, torch.uint8, "ack_hdr")
+            if ack_hdr.dim() != 2 or ack_hdr.shape[1] != 16 or ack_hdr.shape[0] < -(-local.numel() // self.V):
+                raise ValueError("ack_hdr must be uint8 [>= ceil(local.numel() / V), 16] header rows")
+        d = _desc_arg(desc, npk, hdr.device)
+        ad = _ack_desc_arg(ack_desc, ack_hdr)
+        _same_device(hdr, pay, actions, local, out, *([ack_hdr] if ack_hdr is not None else []))
+        scratch = self._scratch_for(npk, hdr.device)
+        self._sorted = None
+        ts = torch.cuda.current_stream(hdr.device)
+        st = self._begin(ts)
+        check(load().ina_switch_process_apply_split(
+            C.byref(self._state), hdr.data_ptr(), pay.data_ptr(), npk, d.data_ptr() if d is not None else None,
+            actions.data_ptr(), scratch.data_ptr(), seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
+            out.data_ptr(), local.numel(), ack_hdr.data_ptr() if ack_hdr is not None else None, ad,
+            int(keep_forwarded), st), "switch_process_apply_split")
         self._end(ts)
         return actions, out
 

@@ -242,6 +242,26 @@ int ina_apply_completed_nga(const uint8_t* pkts, size_t npkts, int V, size_t str
                             const uint8_t* actions, uint32_t seq0, const float* local, int k,
                             double weight_step, float* out, size_t n, uint8_t* acks,
                             size_t ack_stride, ina_stream_t stream);
+/* ---- split NGA rows -------------------------------------------------------------
+ * The same datagrams (header || payload on the wire, DataManager.py:111-165 /
+ * headers.p4:27-80) stored as two arrays: hdr = npkts rows of 16 bytes (the 15-byte
+ * header + one zero byte), pay = npkts rows of 4V bytes (the V big-endian payload words).
+ * Every payload row is 16-byte aligned and covers whole cache lines (the packed NGA-256 row
+ * of 15 + 1024 bytes straddles them), so packs, the switch and the PS move aligned 16-byte
+ * chunks with no byte shifting.  sendmmsg / recvmmsg take two iovecs per datagram
+ * (ina_send_packets_split_fd / ina_recv_packets_split_fd), so the bytes on the socket are
+ * identical.  V is a multiple of 4 in [4, 256]; hdr, pay and value buffers 16-byte aligned.
+ * Packet p's payload row is pay + p * 4V, so a bucket's payload stream is its values in
+ * order, byte-swapped, zero-padded to whole packets. */
+int ina_pack_nga_split(const int32_t* vals, size_t n, const ina_nga_params_t* prm,
+                       const uint8_t* overflow_per_slot, uint8_t* hdr, uint8_t* pay,
+                       ina_nga_desc_t* desc, ina_stream_t stream);
+int ina_quantize_pack_nga_multi_split(const float* const* x, int W, const float* base, size_t n, int k,
+                                      const ina_nga_params_t* prm, uint8_t* const* hdr,
+                                      uint8_t* const* pay, ina_nga_desc_t* const* desc,
+                                      ina_stream_t stream);
+int ina_unpack_nga_split(const uint8_t* hdr, const uint8_t* pay, size_t npkts, int V,
+                         const ina_nga_fields_t* fields, int32_t* vals, ina_stream_t stream);
 /* C-128 pack (communicator.cc:23-37): npkts x 524-byte packet_t, all words htonl. */
 int ina_pack_c128(const uint32_t* gradient, int packet_num, int worker_id,
                   uint32_t aggregator_index, int tensor_index, uint8_t* pkts,
@@ -336,6 +356,20 @@ int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* p
 #define INA_PATH_SORTED 3     /* the bucket sort */
 int ina_switch_batch_path(const void* scratch, size_t npkts, uint32_t num_slots, int* path);
 
+/* The switch over split rows (hdr: 16-byte header rows, pay: 4V-byte payload rows, see
+ * "split NGA rows"): the same semantics, actions, registers and forwarded bytes as
+ * ina_switch_process_desc on the packed rows (a collision rewrites the header row's flag
+ * byte, a forwarded packet its payload row).  The PS step's ack rows are header rows
+ * (16 bytes apart) with their descriptors in ack_desc (may be NULL). */
+int ina_switch_process_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npkts,
+                             const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                             ina_stream_t stream);
+int ina_switch_process_apply_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npkts,
+                                   const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
+                                   uint32_t seq0, const float* local, int k, double weight_step,
+                                   float* out, size_t n, uint8_t* ack_hdr, ina_nga_desc_t* ack_desc,
+                                   int keep_forwarded, ina_stream_t stream);
+
 /* ---- ipRoute (ngaa.p4:39-61, entries as bfrt/setup.py:85-95 installs them) -------
  * Every packet the ingress does not drop (actions FWD_AGG, FWD_COLLISION, FWD_ACK,
  * FWD_OTHER) leaves through ipRoute: an exact match on the IPv4 destination.
@@ -398,6 +432,15 @@ int ina_send_gradients_fd(int fd, const uint32_t* gradient_array, int packet_num
 int ina_send_packets_fd(int fd, const uint8_t* host_pkts, size_t npkts, size_t stride,
                         size_t pkt_len, uint32_t dst_ip);
 
+/* Split rows on the socket: datagram p = hdr row p's 15 bytes || pay row p's 4V bytes (two
+ * iovecs), the same bytes ina_send_packets_fd sends from packed rows.  host_hdr / host_pay:
+ * host memory, rows 16 / 4V bytes apart. */
+int ina_send_packets_split_fd(int fd, const uint8_t* host_hdr, const uint8_t* host_pay, size_t npkts,
+                              int V, uint32_t dst_ip);
+/* ... and into them: each datagram's first 15 bytes (after `skip`) land in its header row,
+ * the next 4V in its payload row (header byte 15 is left as it was).  lens as below. */
+int ina_recv_packets_split_fd(int fd, uint8_t* host_hdr, uint8_t* host_pay, size_t max_pkts, int V,
+                              size_t skip, int timeout_ms, uint32_t* lens);
 /* Batched datagram ingest, the counterpart of get_data_from_nic (utils.py:61-64,
  * one recvfrom per packet): up to max_pkts datagrams land in host_pkts at `stride`
  * apart via recvmmsg(); the first `skip` bytes of each datagram (20 for the IPv4

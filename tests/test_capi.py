@@ -159,6 +159,14 @@ def _einval_cases():
         "ina_absmax_multi_f32": (P([None, None]), 2, None, 64, None, None),
         "ina_sum_reduce_host_i32": (P([None, None]), 2, None, 64, 0, None, None),
         "ina_switch_batch_path": (None, 2048, 16384, None),
+        "ina_pack_nga_split": (None, 64, ctypes.byref(prm), None, None, None, None, None),
+        "ina_quantize_pack_nga_multi_split": (P([None, None]), 2, None, 64, 16,
+                                              (_lib.NgaParams * 2)(prm, prm), P([None, None]),
+                                              P([None, None]), None, None),
+        "ina_unpack_nga_split": (None, None, 2, 32, None, None, None),
+        "ina_switch_process_split": (ctypes.byref(st), None, None, 2, None, None, None, None),
+        "ina_switch_process_apply_split": (ctypes.byref(st), None, None, 2, None, None, None, 1, None, 16,
+                                           0.5, None, 64, None, None, 1, None),
         "ina_switch_process_apply_ackdesc": (ctypes.byref(st), None, 2, 144, None, None, None, 1, None, 16,
                                              0.5, None, 64, None, 144, None, 1, None),
         "ina_switch_run_sorted_apply_ackdesc": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
@@ -175,7 +183,8 @@ def test_every_device_entry_point_rejects_null_buffers():
     device_fns = {n for n in _lib.SIGNATURES if n.startswith("ina_")} - {
         "ina_version", "ina_last_error_string", "ina_set_tuning", "ina_switch_scratch_bytes",
         "ina_host_reduce_scratch_bytes", "ina_scale_for", "ina_send_gradients_fd",
-        "ina_send_packets_fd", "ina_recv_packets_fd"}
+        "ina_send_packets_fd", "ina_recv_packets_fd", "ina_send_packets_split_fd",
+        "ina_recv_packets_split_fd"}
     assert device_fns == set(cases)
     for name, args in cases.items():
         rc = getattr(lib, name)(*args)
@@ -189,6 +198,8 @@ def test_socket_entry_points_reject_bad_descriptors():
     assert lib.ina_send_packets_fd(-1, None, 2, 144, 144, 0) < 0
     assert lib.ina_recv_packets_fd(-1, None, 2, 144, 0, 0, None) < 0
     assert lib.ina_send_gradients_fd(-1, None, 1, 0, 1, 0, 0) < 0
+    assert lib.ina_send_packets_split_fd(-1, None, None, 2, 32, 0) < 0
+    assert lib.ina_recv_packets_split_fd(-1, None, None, 2, 32, 0, 0, None) < 0
 
 
 def test_set_tuning_rejects_unknown_keys_and_values():
