@@ -1532,9 +1532,41 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
             tl = *(pk + L);                           // the tail chunk (one request per group)
         }
         const u32x4s hw = kSplit ? tl : a;            // header words (lane 8b: packet b's)
+        // per-group outcome of the state machine: adds, overwrites, forwards, PS consumption,
+        // collisions (group g's packet, in every lane of the group)
+        bool add_g, first_g, fwd_g, ps_g, coll_g;
+        uint32_t act_v = 0, ps_slot_v = 0;
+        int lastb;                                    // the batch's last adding packet (-1: none)
+        bool before;                                  // an add before the batch's first overwrite
+        // header words of packet g in every lane of its group; lane b also packet b's
+        const uint32_t g1 = kSplit ? hw.y : from_lane(hw.y, 8 * g), g2 = kSplit ? hw.z : from_lane(hw.z, 8 * g),
+                       g3 = kSplit ? hw.w : from_lane(hw.w, 8 * g);
+        const uint32_t gfin = __builtin_bswap32((g2 >> 24) | (g3 << 8)), ghc = g1 & 0xFFu;
+        // the common batch -- no PS ack, every frag id the slot's (or the first packet's when
+        // the slot is free), one degree H with count < H -- needs no packet-by-packet walk:
+        // packet b's count is (count + b + 1) mod H (ngaa.p4:66-78), it completes the slot when
+        // that is 0 and overwrites the registers when it is 1
+        const uint32_t F = frag ? frag : (uint32_t)__builtin_amdgcn_readlane(gfin, 0);
+        const uint32_t H = (uint32_t)__builtin_amdgcn_readlane(ghc, 0);
+        const bool odd = g < nb && (((g1 >> 14) & 1u) || gfin != F || ghc != H);
+        if (__ballot(odd) == 0 && H >= 1u && cnt < H) {
+            frag = F;
+            const uint32_t cg = (cnt + (uint32_t)g + 1u) % H;
+            const uint32_t cl = (cnt + (uint32_t)lane + 1u) % H;   // lane b as packet b
+            const bool cons = kPs && F - ps.seq0 < ps.nslots;       // the PS takes this slot
+            add_g = g < nb;
+            first_g = add_g && cg == 1u;
+            ps_g = add_g && cons && cg == 0u;
+            fwd_g = add_g && (cg == 0u || st.write_dropped) && (!ps_g || ps.keep_fwd);
+            coll_g = false;
+            if (cons) ps_slot_v = F - ps.seq0;
+            act_v = cl == 0u ? INA_ACT_FWD_AGG : INA_ACT_DROP;
+            lastb = nb - 1;
+            before = !(H > 1u && cnt == 0u);          // count 0: packet 0 overwrites
+            cnt = __builtin_amdgcn_readfirstlane((cnt + (uint32_t)nb) % H);
+        } else {
         // the state machine, packet by packet in arrival order (SGPRs, scalar branches)
         uint32_t m_add = 0, m_first = 0, m_fwd = 0, m_coll = 0, m_ps = 0;
-        uint32_t act_v = 0, ps_slot_v = 0;
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
             if (b >= nb) break;
@@ -1572,11 +1604,20 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
             }
             act_v = lane == b ? act : act_v;
         }
+        add_g = (m_add >> g) & 1u;
+        first_g = (m_first >> g) & 1u;
+        fwd_g = (m_fwd >> g) & 1u;
+        ps_g = (m_ps >> g) & 1u;
+        coll_g = (m_coll >> g) & 1u;
+        lastb = m_add ? 31 - __builtin_clz(m_add) : -1;
+        // the stored registers count only before the batch's first overwrite
+        before = (m_first ? m_add & ((m_first & (0u - m_first)) - 1u) : m_add) != 0u;
+        }
         if (lane < nb) actions[lanepid] = (uint8_t)act_v;   // one store for the batch
-        if (((m_coll >> g) & 1u) && l == 0)                // only the flag byte changes
+        if (coll_g && l == 0)                              // only the flag byte changes
             reinterpret_cast<uint32_t*>(pkts + (size_t)mypid * (kSplit ? 16 : stride))[1] =
-                hw.y | ((uint32_t)INA_FLAG_COLLISION << 8);
-        if (m_add) {
+                g1 | ((uint32_t)INA_FLAG_COLLISION << 8);
+        if (lastb >= 0) {
             // values 4l..4l+3 of packet g: chunk l and chunk l+1 (the neighbour lane, or the
             // tail for the group's last value lane)
             u32x4s x;
@@ -1590,9 +1631,8 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
                 if (l == L - 1) c = tl;
                 x.x = dec_be(c.x, a.w); x.y = dec_be(c.y, c.x); x.z = dec_be(c.z, c.y); x.w = dec_be(c.w, c.z);
             }
-            const bool add = (m_add >> g) & 1u;
-            uint32_t f = (m_first >> g) & 1u;
-            if (!add) x = u32x4s{0u, 0u, 0u, 0u};
+            uint32_t f = first_g ? 1u : 0u;
+            if (!add_g) x = u32x4s{0u, 0u, 0u, 0u};
             // segmented inclusive scan over the groups (a reset at each overwrite)
 #pragma unroll
             for (int d = 1; d < kB; d <<= 1) {
@@ -1608,18 +1648,16 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
             }
             // the stored registers count only before the batch's first overwrite; load them
             // if an add comes before it and no earlier batch left them in registers
-            const uint32_t before = m_first ? m_add & ((m_first & (0u - m_first)) - 1u) : m_add;
             if (before && !have_reg)
                 reg = vl ? *reinterpret_cast<const u32x4s*>(st.regs + (size_t)slot * V + 4 * l)
                          : u32x4s{0u, 0u, 0u, 0u};
             const u32x4s S = f ? x : x + reg;        // packet g's running sum
             // the registers after the batch: the last adding packet's running sum
-            const int lastb = 31 - __builtin_clz(m_add);
             const int src = 8 * lastb + l;
             reg.x = from_lane(S.x, src); reg.y = from_lane(S.y, src);
             reg.z = from_lane(S.z, src); reg.w = from_lane(S.w, src);
             have_reg = true;
-            if (kPs && ((m_ps >> g) & 1u)) {         // launch.py:46-50 with the switch's sum
+            if (kPs && ps_g) {                       // launch.py:46-50 with the switch's sum
                 const size_t e0 = (size_t)ps_slot_v * (size_t)V + 4 * (size_t)l;
                 if (vl && e0 + 4 <= ps.n) {
                     const f32x4s lo = *reinterpret_cast<const f32x4s*>(ps.local + e0);
@@ -1643,11 +1681,11 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
                     if (ps.ack_desc) ps.ack_desc[ps_slot_v] = uint2{hd.y, hd.z};
                 }
             }
-            if (kSplit && ((m_fwd >> g) & 1u)) {     // out_value -> the payload row (processor.p4:22)
+            if (kSplit && fwd_g) {                   // out_value -> the payload row (processor.p4:22)
                 const u32x4s e{__builtin_bswap32(S.x), __builtin_bswap32(S.y), __builtin_bswap32(S.z),
                                __builtin_bswap32(S.w)};
                 if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)mypid * (size_t)(4 * V)) + l);
-            } else if ((m_fwd >> g) & 1u) {          // out_value -> payload (processor.p4:22)
+            } else if (fwd_g) {                      // out_value -> payload (processor.p4:22)
                 u32x4s p;                            // values of lane l-1
                 p.x = from_prev_in_row(S.x); p.y = from_prev_in_row(S.y);
                 p.z = from_prev_in_row(S.z); p.w = from_prev_in_row(S.w);
@@ -2240,13 +2278,16 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // at every size -- tools/lab/switch_lab.py, profiles/r01/lab/switch_lab_win.log:
         // 1,024 packets 52.9 -> 27.7 us (64 -> 8 positions), 819,200 packets 277 -> 266 us
         // (64 -> 16 positions, one pass of the grid)
-        uint32_t win = npk <= 65536 ? (uint32_t)INA_SWITCH_WIN_SMALL : (uint32_t)INA_SWITCH_WIN_LARGE;
-        if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
-        const size_t per_block = (size_t)win * (kSwBlock / 64);
-        unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         // V <= 32 (NGA-32, the P4 program's format): 8 packets of a segment side by side per
         // wave (run_segment_narrow); wider packets: a packet per wave instruction
         const bool narrow = st->V <= kNarrowMaxV;
+        uint32_t win = npk <= 65536 ? (uint32_t)INA_SWITCH_WIN_SMALL : (uint32_t)INA_SWITCH_WIN_LARGE;
+        // a narrow wave moves a whole segment per batch: a window of 64 sorted positions
+        // (about 8 segments) keeps the grid at npk / 256 workgroups
+        if (narrow && npk > 65536) win = 64;
+        if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
+        const size_t per_block = (size_t)win * (kSwBlock / 64);
+        unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         auto* run = split ? (ps.on ? (narrow ? &k_switch_run2<true, true, true> : &k_switch_run2<true, false, true>)
                                    : (narrow ? &k_switch_run2<false, true, true> : &k_switch_run2<false, false, true>))
                           : (ps.on ? (narrow ? &k_switch_run2<true, true, false> : &k_switch_run2<true, false, false>)
