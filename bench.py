@@ -794,7 +794,7 @@ def measure_e2e(dev, world=1, reps=5, warm=1, rank=0):
 
 
 # -- the whole INA packet path, steady state (SURVEY 8f-1 + 8f-2) ---------------------------
-def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
+def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1, split=False):
     """One step of the INA data path on one GPU, as a PS co-located with the switch runs it
     in steady state: 8 workers quantise their deltas (p_w - p_global, k=16) straight into
     NGA-256 packets (DataManager.py:37 + 111-165, fused), the PS's acks of the previous
@@ -805,7 +805,10 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
     26,214,400 fp32, 102,400 slots.  HIP events around `steps` back-to-back steps; the
     roofline is the path's algorithmic bytes (packs, switch + PS, acks) over the step time.
     Parity: every worker packet completes its slot once, every ack frees one, and the
-    update at a strided sample equals a numpy restatement bit for bit."""
+    update at a strided sample equals a numpy restatement bit for bit.
+    split=True: the same step over split rows (include/ina.h: 16-byte header rows + aligned
+    1 KiB payload rows, the same datagrams) -- ina_quantize_pack_nga_multi_split and
+    ina_switch_process_apply_split."""
     from ina_amd import ops
     W, n, V, k, slots = W_WORKERS, N_VALUES, V_SLOT, 16, 1 << 17
     npk = n // V
@@ -815,27 +818,43 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
     glob = torch.randn(n, device=dev, generator=g) * 1e-2
     upd = torch.empty_like(glob)
     stride = ops.nga_stride(V)
-    big = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=dev)   # [acks | workers]
-    ack_rows, rows_w = big[:npk], big[npk:].view(W, npk, stride)
+    if split:
+        hdr = torch.zeros(((W + 1) * npk, 16), dtype=torch.uint8, device=dev)      # [acks | workers]
+        pay = torch.zeros(((W + 1) * npk, 4 * V), dtype=torch.uint8, device=dev)
+        ack_rows = hdr[:npk]
+        hdrs_w, pays_w = list(hdr[npk:].view(W, npk, 16).unbind(0)), list(pay[npk:].view(W, npk, 4 * V).unbind(0))
+        big = None
+    else:
+        big = torch.zeros(((W + 1) * npk, stride), dtype=torch.uint8, device=dev)   # [acks | workers]
+        ack_rows, rows_w = big[:npk], big[npk:].view(W, npk, stride)
     desc = torch.empty((W + 1) * npk, dtype=torch.int64, device=dev)
     desc_ack, desc_w = desc[:npk], desc[npk:].view(W, npk)
     acts = torch.empty((W + 1) * npk, dtype=torch.uint8, device=dev)
     sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
     ws = 1.0 / (W + 1)
 
-    outs_w, descs_w = list(rows_w.unbind(0)), list(desc_w.unbind(0))
+    descs_w = list(desc_w.unbind(0))
+    outs_w = None if split else list(rows_w.unbind(0))
     bms = [w + 1 for w in range(W)]
 
     def pack():
         # the 8 workers' quantise + packs as ONE launch (p_global read once for all of them)
-        ops.quantize_pack_nga_multi(xs, k, V, bms, W, 1, 1, base=glob, num_slots=slots,
-                                    outs=outs_w, descs=descs_w)
+        if split:
+            ops.quantize_pack_nga_multi_split(xs, k, V, bms, W, 1, 1, base=glob, num_slots=slots,
+                                              hdrs=hdrs_w, pays=pays_w, descs=descs_w)
+        else:
+            ops.quantize_pack_nga_multi(xs, k, V, bms, W, 1, 1, base=glob, num_slots=slots,
+                                        outs=outs_w, descs=descs_w)
 
     def switch():
         # the fused run kernel writes each ack row's descriptor beside it (ack_desc), so the
         # next step's batch -- these acks in front of the packets -- needs no gather pass
-        sw.process_apply(big, 1, glob, k, ws, out=upd, acks=ack_rows, keep_forwarded=False,
-                         actions=acts, desc=desc, ack_desc=desc_ack)
+        if split:
+            sw.process_apply_split(hdr, pay, 1, glob, k, ws, out=upd, ack_hdr=ack_rows, ack_desc=desc_ack,
+                                   keep_forwarded=False, actions=acts, desc=desc)
+        else:
+            sw.process_apply(big, 1, glob, k, ws, out=upd, acks=ack_rows, keep_forwarded=False,
+                             actions=acts, desc=desc, ack_desc=desc_ack)
 
     def step(_r=0):
         pack()
@@ -868,7 +887,7 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
     want = gl + (acc.astype(np.float32) * np.float32(2.0 ** -k)) * np.float32(ws)
     ok = all_ranks_true(ok and bool(np.array_equal(upd[ti].cpu().numpy().view(np.uint32),
                                                    want.astype(np.float32).view(np.uint32))), world)
-    rb, npk_all = stride, W * npk
+    rb, npk_all = (16 + 4 * V if split else stride), W * npk
     b_pack = W * (4 * n + npk * rb) + 4 * n + W * npk * 8  # fused worker quantise + packs (one
                                                           # launch, p_global read once) + descriptors
     b_sw = (npk * 8                                       # ack descriptors (run kernel)
@@ -878,7 +897,10 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
     res = {"workload": ("INA packet path, steady state, PS fused into the switch pass: 8 workers x "
                         f"{n} fp32 -> quantise(p_w - p_global) + NGA-256 pack -> one switch batch of "
                         f"{npk} PS acks + {npk_all} worker packets -> completed slots applied to "
-                        "p_global (launch.py:46-50) + ack rows"),
+                        "p_global (launch.py:46-50) + ack rows"
+                        + (" -- split rows: 16-byte header rows + 1 KiB payload rows" if split else
+                           " -- packed rows: 15 + 1024 bytes in a 1,040-byte row")),
+           "rows": "split" if split else "packed",
            "value": round(W * n * 4 / avg / 1e9, 2), "unit": "GB/s (worker fp32 bytes aggregated)",
            "ms_per_step": round(avg * 1e3, 3), "steps": steps, "warmup": warm,
            "launches_per_step": 1 + 3,
@@ -887,7 +909,8 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
                         "unit": "GB/s", "frac": round(path / avg / 1e9 / HBM_PEAK_GBS, 4),
                         "path_bytes_per_step": int(path),
                         "measures": "the step's algorithmic bytes (all its kernels) / the step time"},
-           "phases": {"worker_packs": {"kernel": "ina::k_qpack_nga_multi_v256<8> (one launch)",
+           "phases": {"worker_packs": {"kernel": ("ina::k_qpack_nga_multi_split<8>" if split else
+                                                  "ina::k_qpack_nga_multi_v256<8>") + " (one launch)",
                                        "us": round(t_pack * 1e6, 1), "bytes": int(b_pack),
                                        "frac": round(b_pack / t_pack / 1e9 / HBM_PEAK_GBS, 4)},
                       "switch_and_ps": {"kernels": "k_sort_chunks, k_sort_buckets (finds 9 dense runs: "
@@ -900,6 +923,8 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1):
            "parity_sample": (f"every worker packet completes its slot, every ack frees one; the update at "
                              f"{idx.size} positions vs numpy quantise + wrapping sum + launch.py update")}
     del xs, glob, upd, big, desc, acts, sw
+    if split:
+        del hdr, pay, hdrs_w, pays_w
     torch.cuda.empty_cache()
     return res
 
@@ -1175,6 +1200,7 @@ def run_reduce(args, rank, world, dev, backend):
                                                               orders=("worker_major", "round_robin",
                                                                       "shuffled")))
         run_leg(line, "packet_path", lambda: measure_packet_path(dev, rank=rank, world=world))
+        run_leg(line, "packet_path_split", lambda: measure_packet_path(dev, rank=rank, world=world, split=True))
     if cpu_in is not None:
         run_leg(line, "cpu_baseline", lambda: cpu_baseline(args, *cpu_in))
     return line

@@ -642,7 +642,12 @@ constexpr int kRunsStart = 1, kRunsKey = 2 + kRunsMax;
 constexpr int kCtlWords = kCtlRuns + kRunsKey + kRunsMax;
 static_assert(kCtlWords * 4 <= 1024, "control block fits its 1 KiB");
 
-template <int R, bool kDesc, int BINS>
+// kMode: 0 the chunk pass (keys, detection, digits, scatter); for keys of 19-22 bits, whose
+// 2,048-bin chunk pass holds one block per CU (136 KiB of LDS), the pass is split in two so a
+// structured batch never pays it: 1 = detection only (the arrival-order keys into kout, the
+// descent flag, the breaks; no digits, a small LDS footprint), then k_runs_decide, then 2 =
+// digits + scatter only, leaving at once when the batch is in slot order or dense runs.
+template <int R, bool kDesc, int BINS, int kMode = 0>
 __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restrict__ pkts,
                                                         const uint2* __restrict__ desc, size_t npk,
                                                         size_t stride, uint32_t num_slots, int switch_id,
@@ -659,8 +664,11 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     __shared__ uint32_t wbrk[kBkWaves];               // per-wave break counts
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
+    if constexpr (kMode == 2)                         // in slot order or dense runs: no sort
+        if (unsorted[0] != epoch || unsorted[2] == epoch) return;
     const uint32_t nb = 1u << hbits;
-    for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
+    if constexpr (kMode != 1)
+        for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
     const size_t i0 = c * (size_t)(kBkThr * R) + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t idx[R], sid[R], ack[R], k[R], v[R];
     load_key_fields<R, kDesc>(pkts, desc, npk, stride, i0, idx, sid, ack);
@@ -683,8 +691,10 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         // bit 31 carries "PS ack" through the sort (no digit reads it)
         k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
         v[r] = (uint32_t)p;
-        if (p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
-        lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
+        if (kMode != 2 && p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
+        if constexpr (kMode != 1) lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
+        if constexpr (kMode == 1)
+            if (p < npk) kout[p] = k[r];              // arrival-order keys (the in-order run's)
         // predecessor: lane l-1 of this round (DPP wave_shr:1), lane 0 the previous round's
         // lane 63 (or, in round 0, the key loaded above)
         const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp((int)prev, (int)key, 0x138, 0xF, 0xF, false);
@@ -697,14 +707,16 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     }
     // the batch is not in slot order: B sorts (else B only copies A's output, which is then
     // the identity permutation).  Tagged with the call's epoch, so nothing needs clearing.
-    if (__ballot(down) && lane == 0) unsorted[0] = epoch;
-    if (c == 0 && threadIdx.x == 0) unsorted[1] = epoch;     // this call's epoch, for the run kernel
+    if constexpr (kMode != 2) {
+        if (__ballot(down) && lane == 0) unsorted[0] = epoch;
+        if (c == 0 && threadIdx.x == 0) unsorted[1] = epoch;     // this call's epoch, for the run kernel
+    }
     uint32_t nbw = 0;                                         // this wave's breaks
 #pragma unroll
     for (int r = 0; r < R; ++r) nbw += (uint32_t)__builtin_popcountll(bm[r]);
     if (lane == 0) wbrk[wv] = nbw;
     __syncthreads();
-    if (brk_cnt) {                                            // the chunk's breaks, in order
+    if (kMode != 2 && brk_cnt) {                              // the chunk's breaks, in order
         uint32_t tot = 0, pre = 0;
 #pragma unroll
         for (int w = 0; w < kBkWaves; ++w) {
@@ -724,6 +736,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
             }
         }
     }
+    if constexpr (kMode == 1) return;
     // thread t owns digits t*DPT .. t*DPT+DPT-1: the chunk's counts, their chunk-local run
     // starts (block scan)
     constexpr int DPT = kDigitsPerThread<BINS>;
@@ -762,6 +775,54 @@ __device__ unsigned long long g_bk_t[kRsBins][6];
 #define BK_STAMP(q) do { } while (0)
 #endif
 
+// the run table from the chunks' break records (a structured batch, total <= kRunsMax breaks),
+// by one block of kBkThr threads: thread t takes chunks 2t and 2t+1 (nch <= 2 x kBkThr), so the
+// entries land in chunk order = position order
+__device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk_cnt, const uint2* __restrict__ brk_ent,
+                                                uint32_t nch, uint32_t total, uint32_t npk,
+                                                uint32_t* __restrict__ unsorted, uint32_t epoch, uint32_t* wtot) {
+    const uint32_t c0 = 2u * threadIdx.x;
+    const uint32_t n0 = c0 < nch ? brk_cnt[c0] : 0u, n1 = c0 + 1 < nch ? brk_cnt[c0 + 1] : 0u;
+    const uint32_t ex = block_digit_scan(n0 + n1, wtot, 0u);
+    uint32_t* runs = unsorted + (kCtlRuns - kCtlEpochs);
+    for (uint32_t j = 0; j < n0; ++j) {
+        const uint2 e = brk_ent[(size_t)c0 * kRunsMax + j];
+        runs[kRunsStart + ex + j] = e.x;
+        runs[kRunsKey + ex + j] = e.y;
+    }
+    for (uint32_t j = 0; j < n1; ++j) {
+        const uint2 e = brk_ent[(size_t)(c0 + 1) * kRunsMax + j];
+        runs[kRunsStart + ex + n0 + j] = e.x;
+        runs[kRunsKey + ex + n0 + j] = e.y;
+    }
+    if (threadIdx.x == 0) {
+        runs[0] = total;
+        runs[kRunsStart + total] = npk;
+        unsorted[2] = epoch;                          // the run table is this call's
+    }
+}
+
+// the split chunk pass of 19-22-bit keys (k_sort_chunks modes 1 / 2): one block decides between
+// the detection and the sort -- a batch not in slot order with at most kRunsMax breaks gets its
+// run table, and the digit pass and the bucket pass then leave at once
+__global__ __launch_bounds__(kBkThr) void k_runs_decide(const uint32_t* __restrict__ brk_cnt,
+                                                        const uint2* __restrict__ brk_ent, uint32_t nch,
+                                                        uint32_t npk, uint32_t* __restrict__ unsorted,
+                                                        uint32_t epoch) {
+    __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
+    if (unsorted[0] != epoch) return;                 // in slot order: the run reads the keys
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    uint32_t part = 0;
+    for (uint32_t c = threadIdx.x; c < nch; c += kBkThr) part += brk_cnt[c];
+    const uint32_t inc = wave_incl_scan(part);
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    uint32_t total = 0;
+#pragma unroll
+    for (int w = 0; w < kBkWaves; ++w) total += red[w];
+    if (total <= (uint32_t)kRunsMax) build_run_table(brk_cnt, brk_ent, nch, total, npk, unsorted, epoch, red2);
+}
+
 // positions of bucket items i[r] (0 <= i < the bucket's size) in A's output: the run of the
 // last chunk whose bucket offset is <= i (s_dst: exclusive prefix of the run lengths over the
 // nch chunks, then the bucket's size).  A branch-free binary search with a uniform step
@@ -795,7 +856,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
                                                          uint32_t skip, uint32_t* __restrict__ unsorted,
                                                          uint32_t epoch, int sorted_copy,
                                                          const uint32_t* __restrict__ brk_cnt,
-                                                         const uint2* __restrict__ brk_ent, uint32_t npk) {
+                                                         const uint2* __restrict__ brk_ent, uint32_t npk,
+                                                         int pre) {
     __shared__ uint32_t s_dst[kBkMaxChunks + 1], s_src[kBkMaxChunks];
     __shared__ uint32_t base[kBkWaves][BINS];
     __shared__ uint32_t gst[BINS];                    // bucket digit counts, then output positions
@@ -805,6 +867,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
     // keys already in slot order: A's output is the sorted order and the register-resident
     // run kernel reads it there (sorted_copy = 0), so only the foreign bucket's size is needed
     const bool in_order = unsorted[0] != epoch;
+    // after the split chunk pass (pre): structured batches were decided, nothing to gather
+    if (pre && (in_order || unsorted[2] == epoch)) return;
     if (in_order && !sorted_copy && b != skip) return;
     if (!in_order && brk_cnt) {
         // dense ascending runs (brk_cnt != NULL only for the register-resident run kernel):
@@ -819,27 +883,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
 #pragma unroll
         for (int w = 0; w < kBkWaves; ++w) total += red[w];
         if (total <= (uint32_t)kRunsMax) {
-            if (b != 0) return;
-            // thread t: chunks 2t and 2t+1 (nch <= 2 x kBkThr), entries in chunk order
-            const uint32_t c0 = 2u * threadIdx.x;
-            const uint32_t n0 = c0 < nch ? brk_cnt[c0] : 0u, n1 = c0 + 1 < nch ? brk_cnt[c0 + 1] : 0u;
-            const uint32_t ex = block_digit_scan(n0 + n1, red2, 0u);
-            uint32_t* runs = unsorted + (kCtlRuns - kCtlEpochs);
-            for (uint32_t j = 0; j < n0; ++j) {
-                const uint2 e = brk_ent[(size_t)c0 * kRunsMax + j];
-                runs[kRunsStart + ex + j] = e.x;
-                runs[kRunsKey + ex + j] = e.y;
-            }
-            for (uint32_t j = 0; j < n1; ++j) {
-                const uint2 e = brk_ent[(size_t)(c0 + 1) * kRunsMax + j];
-                runs[kRunsStart + ex + n0 + j] = e.x;
-                runs[kRunsKey + ex + n0 + j] = e.y;
-            }
-            if (threadIdx.x == 0) {
-                runs[0] = total;
-                runs[kRunsStart + total] = npk;
-                unsorted[2] = epoch;                  // the run table is this call's
-            }
+            if (b == 0) build_run_table(brk_cnt, brk_ent, nch, total, npk, unsorted, epoch, red2);
             return;
         }
         __syncthreads();                              // red[] is reused below
@@ -1735,7 +1779,8 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
         const size_t i = w0 + (size_t)lane;
         const uint32_t kr = i < npk ? keys[i] : NS;
         const uint32_t ki = kr & kmask;                   // slot (bit 31: PS-ack hint)
-        const uint32_t idw = i < npk ? ids[i] : 0u;     // packet ids of the window, one load
+        // packet ids of the window, one load (no ids: a batch in slot order read in place)
+        const uint32_t idw = i < npk ? (ids ? ids[i] : (uint32_t)i) : 0u;
         const uint32_t kp = (i > 0 && i <= npk) ? (keys[i - 1] & kmask) : 0xFFFFFFFFu;
         const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
         // a PS ack only clears the slot's frag register and is forwarded unchanged
@@ -1784,7 +1829,7 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                 for (int b = 0; b < kB; ++b)
                     pid[b] = b < nb ? __builtin_amdgcn_readlane(idw, o + b < 64 ? o + b : 63) : 0u;
             } else {
-                const uint32_t my = lane < nb ? ids[q0 + (size_t)lane] : 0u;
+                const uint32_t my = lane < nb ? (ids ? ids[q0 + (size_t)lane] : (uint32_t)(q0 + (size_t)lane)) : 0u;
 #pragma unroll
                 for (int b = 0; b < kB; ++b) pid[b] = __builtin_amdgcn_readlane(my, b);
             }
@@ -1913,8 +1958,11 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
         const uint32_t ep = unsorted[1];
         if (unsorted[0] != ep) {
             // a batch already in slot order: the chunk sort's own output is the sorted order
+            // (after the split chunk pass of wide keys: the arrival-order keys, ids_a NULL --
+            // the packets in place, the foreign ones last with key num_slots, never a head)
             keys = keys_a;
             ids = ids_a;
+            if (!ids_a) nforeign = nullptr;
         } else if (unsorted[2] == ep) {
             // a batch of dense ascending runs: the bucket pass wrote the run table, not a sort
             switch_runs_body<kPs, kNarrow, kSplit>(st, pkts, stride, pay, actions, kmask, ps,
@@ -2192,9 +2240,35 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const bool runs_on = fast && g_runs.load() != 0;
         // never 0 (fresh scratch reads as "unsorted": the safe side); a stale epoch equal to
         // this one (2^32 calls later) also only costs the full sort
+        // keys of 19-22 bits (2,048-bin digits) with the register-resident run kernel: the
+        // chunk pass split in two around k_runs_decide, so structured batches skip the digits
+        const bool pre = sp.wide && fast;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
+        if (pre) {
+#define INA_A_DETECT(RR)                                                                              \
+            hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true, 64, 1> : &k_sort_chunks<RR, false, 64, 1>),      \
+                               dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
+                               st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kc, vc, ah, \
+                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
+            if (ri == 2) INA_A_DETECT(kR2 / 4);
+            else if (ri == 1) INA_A_DETECT(kR1 / 4);
+            else INA_A_DETECT(kR0 / 4);
+#undef INA_A_DETECT
+            if (runs_on)
+                hipLaunchKernelGGL(k_runs_decide, dim3(1), dim3(kBkThr), 0, s, ax.brk_cnt, ax.brk_ent,
+                                   (uint32_t)sp.nch, (uint32_t)npk, ax.unsorted, epoch);
+#define INA_A_SORT(RR)                                                                                \
+            hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true, kBinsBig, 2> : &k_sort_chunks<RR, false, kBinsBig, 2>), \
+                               dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
+                               st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
+                               ax.unsorted, epoch, nullptr, ax.brk_ent)
+            if (ri == 2) INA_A_SORT(kR2 / 4);
+            else if (ri == 1) INA_A_SORT(kR1 / 4);
+            else INA_A_SORT(kR0 / 4);
+#undef INA_A_SORT
+        } else {
 #define INA_A_LAUNCH(RR)                                                                              \
         hipLaunchKernelGGL((sp.wide ? (desc ? &k_sort_chunks<RR, true, kBinsBig> : &k_sort_chunks<RR, false, kBinsBig>) \
                                     : (desc ? &k_sort_chunks<RR, true, kRsBins> : &k_sort_chunks<RR, false, kRsBins>)), \
@@ -2205,6 +2279,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
         else INA_A_LAUNCH(kR0 / 4);
 #undef INA_A_LAUNCH
+        }
         }
         // the bucket of foreign packets only (a pool of a multiple of 2^lb slots) is left out
         // when the register-resident run kernel takes the batch (it stops before them); the
@@ -2226,7 +2301,11 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                dim3(gb),
                                dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
                                ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1,
-                               runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, (uint32_t)npk);
+                               (runs_on && !pre) ? ax.brk_cnt : nullptr, ax.brk_ent, (uint32_t)npk, pre ? 1 : 0);
+        if (pre) {                                 // the in-order run reads the arrival-order keys
+            kn = kc;
+            vn = nullptr;
+        }
         if (fast) unsorted = ax.unsorted;
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch sort launch%s", "");
     } else {

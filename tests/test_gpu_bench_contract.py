@@ -100,9 +100,12 @@ def test_bench_json_line_contract():
     assert pp["parity_spot_check"] is True and pp["value"] > 0 and pp["ms_per_step"] > 0
     assert pp["roofline"]["bound"] == "hbm" and 0 < pp["roofline"]["frac"] < 1
     assert abs(pp["roofline"]["frac"] - pp["roofline"]["achieved"] / pp["roofline"]["peak"]) < 1e-3
-    ph = pp["phases"]                            # the packs and the switch + PS pass apart
-    assert 0 < ph["worker_packs"]["frac"] < 1 and 0 < ph["switch_and_ps"]["frac"] < 1
-    assert ph["worker_packs"]["bytes"] + ph["switch_and_ps"]["bytes"] == pp["roofline"]["path_bytes_per_step"]
+    for leg in (pp, d["packet_path_split"]):     # packed rows, and split rows (same datagrams)
+        assert leg["parity_spot_check"] is True and leg["value"] > 0 and leg["switch_batch_path"] == "runs"
+        ph = leg["phases"]                       # the packs and the switch + PS pass apart
+        assert 0 < ph["worker_packs"]["frac"] < 1 and 0 < ph["switch_and_ps"]["frac"] < 1
+        assert ph["worker_packs"]["bytes"] + ph["switch_and_ps"]["bytes"] == leg["roofline"]["path_bytes_per_step"]
+    assert pp["rows"] == "packed" and d["packet_path_split"]["rows"] == "split"
     assert not any(isinstance(v, dict) and "error" in v for v in d.values())   # no leg raised
 
 
