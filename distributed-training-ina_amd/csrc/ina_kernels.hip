@@ -1967,6 +1967,7 @@ int ina_set_tuning(int key, int value) {
         case 16: return set_zero_copy(value);
         case 17: return set_bucket_tile(value);
         case 18: return set_runs(value);
+        case 19: return set_pre_all(value);
         default: return INA_EINVAL;
     }
 }

@@ -287,6 +287,16 @@ int set_runs(int v) {
     g_runs = v ? 1 : 0;
     return INA_OK;
 }
+// ina_set_tuning key 19: the split chunk pass (detection, decision, then digits) for keys of
+// 19-22 bits only (0, default) or for every key width (1)
+#ifndef INA_SWITCH_PRE_ALL
+#define INA_SWITCH_PRE_ALL 0
+#endif
+static std::atomic<int> g_pre_all{INA_SWITCH_PRE_ALL};
+int set_pre_all(int v) {
+    g_pre_all = v ? 1 : 0;
+    return INA_OK;
+}
 int set_sort_mode(int v) {
     if (v != 0 && v != 3) return INA_EINVAL;
     g_sort_mode = v;
@@ -2242,7 +2252,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // this one (2^32 calls later) also only costs the full sort
         // keys of 19-22 bits (2,048-bin digits) with the register-resident run kernel: the
         // chunk pass split in two around k_runs_decide, so structured batches skip the digits
-        const bool pre = sp.wide && fast;
+        const bool pre = (sp.wide || g_pre_all.load()) && fast;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
@@ -2260,7 +2270,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                 hipLaunchKernelGGL(k_runs_decide, dim3(1), dim3(kBkThr), 0, s, ax.brk_cnt, ax.brk_ent,
                                    (uint32_t)sp.nch, (uint32_t)npk, ax.unsorted, epoch);
 #define INA_A_SORT(RR)                                                                                \
-            hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true, kBinsBig, 2> : &k_sort_chunks<RR, false, kBinsBig, 2>), \
+            hipLaunchKernelGGL((sp.wide ? (desc ? &k_sort_chunks<RR, true, kBinsBig, 2> : &k_sort_chunks<RR, false, kBinsBig, 2>) \
+                                        : (desc ? &k_sort_chunks<RR, true, kRsBins, 2> : &k_sort_chunks<RR, false, kRsBins, 2>)), \
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
                                ax.unsorted, epoch, nullptr, ax.brk_ent)

@@ -986,7 +986,7 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                switch_sort: int | None = None, switch_sort_rounds: int | None = None,
                ew_blocks: int | None = None, switch_tiny_max: int | None = None,
                host_zero_copy: bool | None = None, switch_bucket_tile: int | None = None,
-               switch_runs: bool | None = None):
+               switch_runs: bool | None = None, switch_pre_all: bool | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -1010,7 +1010,9 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     sort's bucket tile in 64-item rounds per wave (0 = auto: 8 when the average bucket
     exceeds 3,584 packets, else 4; or 4, 8); switch_runs lets batches of at most 64 runs of
     consecutive slots (worker-major arrival, PS acks in front) skip the slot sort (True, the
-    default; False always sorts); unroll is the
+    default; False always sorts); switch_pre_all splits the sort's first pass into detection,
+    decision and digits for every key width (False, the default: keys of 19-22 bits only);
+    unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()
     if reduce_blocks is not None:
@@ -1045,6 +1047,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(17, int(switch_bucket_tile)), "set_tuning")
     if switch_runs is not None:
         check(lib.ina_set_tuning(18, int(bool(switch_runs))), "set_tuning")
+    if switch_pre_all is not None:
+        check(lib.ina_set_tuning(19, int(bool(switch_pre_all))), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

@@ -79,7 +79,9 @@ const char* ina_last_error_string(void);
  * pipeline (0), 17 the slot sort's bucket tile in 64-item rounds per wave (0 auto: 8 when
  * the average bucket exceeds 3,584 packets, else 4; or 4, 8), 18 switch batches made of at
  * most 64 runs of consecutive slots (worker-major arrival, PS acks in front) skip the slot
- * sort and run from a table of the runs (1, default; 0 = always sort).
+ * sort and run from a table of the runs (1, default; 0 = always sort), 19 the slot sort's
+ * first pass split into detection + decision + digits for every key width (1) or only for
+ * keys of 19-22 bits (0, default).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 
