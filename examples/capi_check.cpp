@@ -156,9 +156,36 @@ int main() {
     for (uint8_t a : act) done += a == INA_ACT_FWD_AGG;
     if (done != npk) ++bad;
     for (size_t i = 0; i < n; ++i) bad += std::memcmp(&out[i], &f[i], 4) != 0;
+
+    // the same step over split rows (16-byte headers + 4V-byte payloads): fresh switch
+    // state, same dequantised sum, same actions
+    {
+        uint8_t *d_hdr, *d_pay;
+        HK(hipMalloc(&d_hdr, (size_t)W * npk * 16));
+        HK(hipMalloc(&d_pay, (size_t)W * npk * 4 * V));
+        for (int w = 0; w < W; ++w) {
+            prm.bitmap = 1u << w;
+            CK(ina_pack_nga_split(d_q[w], n, &prm, nullptr, d_hdr + (size_t)w * npk * 16,
+                                  d_pay + (size_t)w * npk * 4 * V, nullptr, s));
+        }
+        HK(hipMemsetAsync(d_count, 0, slots, s));
+        HK(hipMemsetAsync(d_frag, 0, slots * 4, s));
+        HK(hipMemsetAsync(d_regs, 0, (size_t)slots * V * 4, s));
+        HK(hipMemsetAsync(d_out, 0xff, n * 4, s));
+        CK(ina_switch_process_apply_split(&st, d_hdr, d_pay, (size_t)W * npk, nullptr, d_act, d_scratch, 1,
+                                          d_zero, k, 1.0, d_out, n, nullptr, nullptr, 0, s));
+        HK(hipStreamSynchronize(s));
+        std::vector<uint8_t> act2(act.size());
+        HK(hipMemcpy(out.data(), d_out, n * 4, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(act2.data(), d_act, act2.size(), hipMemcpyDeviceToHost));
+        if (act2 != act) ++bad;
+        for (size_t i = 0; i < n; ++i) bad += std::memcmp(&out[i], &f[i], 4) != 0;
+        HK(hipFree(d_hdr));
+        HK(hipFree(d_pay));
+    }
     // the error path: a bad argument returns a code, sets a message, never exits
     const int rc = ina_sum_reduce_i32((const int32_t* const*)d_q, 0, d_sum, n, s);
     if (rc != INA_EINVAL || std::strlen(ina_last_error_string()) == 0) ++bad;
-    std::printf("capi_check: %zu values x %d workers (bulk reduce, NGA-256 pack/unpack, one-launch worker packs, switch + fused PS step), %zu mismatches\n", n, W, bad);
+    std::printf("capi_check: %zu values x %d workers (bulk reduce, NGA-256 pack/unpack, one-launch worker packs, switch + fused PS step, packed and split rows), %zu mismatches\n", n, W, bad);
     return bad ? 1 : 0;
 }

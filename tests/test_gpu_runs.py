@@ -435,3 +435,16 @@ def test_nga32_config3_full_size(order):
     slot = (ts + 1) % ns                                   # packet p of a worker: slot (seq0 + p) % pool
     assert torch.equal(sw.regs[slot], want)
     assert int(sw.count.max()) == 0
+
+
+def test_numpy_integer_seq0_broadcasts():
+    """seq0 given as a numpy integer scalar is one seq0 for every worker (numbers.Integral),
+    as a Python int is -- make_descriptors and the one-launch worker pack alike."""
+    o = ops()
+    a = o.make_descriptors(100, 3, 3, 1, np.int64(5), num_slots=1 << 13, device=DEV)
+    b = o.make_descriptors(100, 3, 3, 1, 5, num_slots=1 << 13, device=DEV)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    xs = [torch.zeros(320, device=DEV) for _ in range(3)]
+    p1 = o.quantize_pack_nga_multi(xs, 16, 32, [1, 2, 3], 3, 1, np.uint32(9))
+    p2 = o.quantize_pack_nga_multi(xs, 16, 32, [1, 2, 3], 3, 1, 9)
+    assert all(torch.equal(x, y) for x, y in zip(p1, p2))
