@@ -1195,6 +1195,11 @@ constexpr int kB = INA_SWITCH_BATCH;         // packets of a segment loaded at o
 #ifndef INA_SWITCH_GRID
 #define INA_SWITCH_GRID (1 << 20)
 #endif
+// the narrow (V <= 32) run over a run table loads slot s+1 while it runs slot s (0: one slot
+// at a time; a lab build's A/B switch)
+#ifndef INA_SWITCH_NARROW_PRE
+#define INA_SWITCH_NARROW_PRE 1
+#endif
 static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWITCH_WIN_LARGE >= 1 &&
               INA_SWITCH_WIN_LARGE <= 64, "a window is at most one wave of keys");
 // occupancy target of k_switch_run2 without the PS step (72 VGPRs -> 7 waves per SIMD)
@@ -1549,19 +1554,50 @@ __device__ __forceinline__ uint32_t from_prev_in_row(uint32_t x) {
 constexpr int kNarrowMaxV = 32;
 static_assert(kB == 8, "the narrow run puts a batch of 8 packets in 8 lane groups");
 
-template <bool kPs, bool kSplit, typename PidFn>
+// a narrow segment's first batch and slot state, loaded ahead (the runs path issues slot s+1's
+// loads before it runs slot s, so a wave has two slots' round trips in flight)
+struct NarrowPre {
+    u32x4s a, tl;              // chunk l of packet g (split: payload chunk l), the tail / header row
+    uint32_t cnt, frag;        // the slot's count and frag registers
+};
+// packet group g's row loads (lanes past L re-read chunk 0; the tail chunk is one request per
+// group); the caller's mypid is packet g's id
+template <bool kSplit>
+__device__ __forceinline__ void narrow_load(const uint8_t* __restrict__ pkts, size_t stride,
+                                            const uint8_t* __restrict__ pay, int V, uint32_t mypid,
+                                            u32x4s& a, u32x4s& tl) {
+    const int l = threadIdx.x & 7, L = V >> 2;
+    const bool vl = l < L;
+    if constexpr (kSplit) {                           // payload chunk l; the group's header row
+        a = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)mypid * (size_t)(4 * V)) + (vl ? l : 0));
+        tl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * 16);
+    } else {
+        const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride);
+        a = sw_ld(pk + (vl ? l : 0));
+        tl = *(pk + L);
+    }
+}
+
+template <bool kPs, bool kSplit, bool kPre = false, typename PidFn>
 __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                    size_t stride, uint8_t* __restrict__ pay,
                                                    uint8_t* __restrict__ actions,
                                                    const PsFuse& ps, uint32_t slot, bool ack_led,
-                                                   size_t q_begin, size_t q_end, PidFn&& pid_batch) {
+                                                   size_t q_begin, size_t q_end, PidFn&& pid_batch,
+                                                   const NarrowPre* pre = nullptr) {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, l = lane & 7;      // packet group, value lane
     const int V = st.V;
     const int L = V >> 2;                       // value lanes per group (<= 8)
     const bool vl = l < L;
-    uint32_t cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
-    uint32_t frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
+    uint32_t cnt, frag;
+    if constexpr (kPre) {
+        cnt = __builtin_amdgcn_readfirstlane(pre->cnt);
+        frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(pre->frag);
+    } else {
+        cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
+        frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
+    }
     u32x4s reg = {0u, 0u, 0u, 0u};              // the slot's running registers, in every group
     bool have_reg = false;
     for (size_t q0 = q_begin; q0 < q_end; q0 += kB) {
@@ -1577,13 +1613,11 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
             lanepid = lane == b ? pid[b] : lanepid;
         }
         u32x4s a, tl;
-        if constexpr (kSplit) {                       // payload chunk l; the group's header row
-            a = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)mypid * (size_t)(4 * V)) + (vl ? l : 0));
-            tl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * 16);
+        if (kPre && q0 == q_begin) {
+            a = pre->a;
+            tl = pre->tl;
         } else {
-            const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)mypid * stride);
-            a = sw_ld(pk + (vl ? l : 0));             // chunk l (lanes past L re-read chunk 0)
-            tl = *(pk + L);                           // the tail chunk (one request per group)
+            narrow_load<kSplit>(pkts, stride, pay, V, mypid, a, tl);
         }
         const u32x4s hw = kSplit ? tl : a;            // header words (lane 8b: packet b's)
         // per-group outcome of the state machine: adds, overwrites, forwards, PS consumption,
@@ -1892,6 +1926,95 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
     const size_t per = ((size_t)(hi - lo) + nwaves - 1) / nwaves;
     const size_t s_begin = (size_t)lo + wave * per;
     const size_t s_end = s_begin + per < (size_t)hi ? s_begin + per : (size_t)hi;
+#if INA_SWITCH_NARROW_PRE
+    if constexpr (kNarrow) {
+        // NGA-32: a slot's 8 packets are one 144-byte row each, a single load per lane, so one
+        // slot's round trips leave the memory system idle.  Slot s+1's state and first batch
+        // are loaded before slot s runs (slots are independent, ngaa.p4:87-168; no wave
+        // touches another's slots), two slots' loads in flight per wave.
+        struct SlotInfo {
+            unsigned long long m;                     // the runs holding the slot (ack removed)
+            bool ack_led;
+            uint32_t p_ack;                           // the leading ack's packet
+        };
+        auto info = [&](size_t s) {
+            SlotInfo si{0ull, false, 0u};
+            const uint32_t off = (uint32_t)s - rslot;
+            const bool in = off < rlen;
+            si.m = __ballot(in);
+            if (si.m) {
+                const int l0 = __builtin_ctzll(si.m);
+                si.ack_led = (__ballot(in && rack) >> l0) & 1ull;
+                if (si.ack_led) {
+                    si.p_ack = __builtin_amdgcn_readlane(rpos + off, l0);
+                    si.m &= si.m - 1;
+                }
+            }
+            return si;
+        };
+        const int g = lane >> 3;
+        auto preload = [&](size_t s, const SlotInfo& si, NarrowPre& p) {
+            const uint32_t pidv = rpos + ((uint32_t)s - rslot);
+            unsigned long long mm = si.m;
+            uint32_t first = 0u, mypid = 0u;
+            bool set = false;
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                if (mm) {
+                    const uint32_t v = __builtin_amdgcn_readlane(pidv, __builtin_ctzll(mm));
+                    mm &= mm - 1;
+                    first = b == 0 ? v : first;
+                    if (g == b) { mypid = v; set = true; }
+                }
+            }
+            if (!set) mypid = first;                  // groups past the segment repeat packet 0
+            p.cnt = st.count[s];
+            p.frag = st.frag[s];
+            narrow_load<kSplit>(pkts, stride, pay, st.V, mypid, p.a, p.tl);
+        };
+        // run slot s from (ci, cp) after issuing slot s+1's loads into (ni, np)
+        auto step = [&](size_t s, const SlotInfo& ci, const NarrowPre& cp, SlotInfo& ni, NarrowPre& np) {
+            ni = SlotInfo{0ull, false, 0u};
+            if (s + 1 < s_end) {
+                ni = info(s + 1);
+                if (ni.m) preload(s + 1, ni, np);
+            }
+            const uint32_t slot = (uint32_t)s;
+            if (ci.ack_led && lane == 0) {            // reset_id (fragcheck.p4:26-31), unread
+                actions[ci.p_ack] = INA_ACT_FWD_ACK;
+                if (!ci.m) st.frag[slot] = 0u;        // a lone ack
+            }
+            if (ci.m) {
+                unsigned long long m = ci.m;
+                const uint32_t pidv = rpos + (slot - rslot);
+                auto pids = [&](size_t, int nb, uint32_t (&pid)[kB]) {
+#pragma unroll
+                    for (int b = 0; b < kB; ++b) {
+                        if (b < nb) {
+                            const int l = __builtin_ctzll(m);
+                            m &= m - 1;
+                            pid[b] = __builtin_amdgcn_readlane(pidv, l);
+                        } else {
+                            pid[b] = 0u;
+                        }
+                    }
+                };
+                run_segment_narrow<kPs, kSplit, true>(st, pkts, stride, pay, actions, ps, slot, ci.ack_led, 0,
+                                                      (size_t)__builtin_popcountll(ci.m), pids, &cp);
+            }
+        };
+        // two register sets used in turn (no copy of a set whose loads are still in flight)
+        SlotInfo ia = s_begin < s_end ? info(s_begin) : SlotInfo{0ull, false, 0u}, ib;
+        NarrowPre pa{}, pb{};
+        if (ia.m) preload(s_begin, ia, pa);
+        for (size_t s = s_begin; s < s_end; s += 2) {
+            step(s, ia, pa, ib, pb);
+            if (s + 1 >= s_end) break;
+            step(s + 1, ib, pb, ia, pa);
+        }
+        return;
+    }
+#endif
     for (size_t s = s_begin; s < s_end; ++s) {
         const uint32_t slot = (uint32_t)s;
         const uint32_t off = slot - rslot;

@@ -121,6 +121,19 @@ _lib = None
 _lock = threading.Lock()
 
 
+def open_library(path: str) -> C.CDLL:
+    """A libina.so build at `path` with the ABI's signatures set (the A/B labs load a second
+    build beside the in-tree one and swap it in as `_lib._lib`)."""
+    if not os.path.exists(path):
+        raise InaError(f"libina.so not built at {path}; run `make -C {CSRC}` or __graft_entry__.build()")
+    lib = C.CDLL(path)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, C.c_int)
+    return lib
+
+
 def load() -> C.CDLL:
     """Load libina.so (raises InaError if it is not built)."""
     global _lib
@@ -128,15 +141,7 @@ def load() -> C.CDLL:
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
-                raise InaError(f"libina.so not built at {LIB_PATH}; run "
-                               f"`make -C {CSRC}` or __graft_entry__.build()")
-            lib = C.CDLL(LIB_PATH)
-            for name, args in SIGNATURES.items():
-                fn = getattr(lib, name)
-                fn.argtypes = args
-                fn.restype = _RESTYPE.get(name, C.c_int)
-            _lib = lib
+            _lib = open_library(LIB_PATH)
     return _lib
 
 
