@@ -65,6 +65,18 @@ for st in $STAGES; do
       ( export ${envs//,/ }; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$OUT/swtrace_$tag" -o run -- python3 tools/prof_switch.py > "$OUT/swtrace_$tag.log" 2>&1 )
       rc=$?; tail -2 "$OUT/swtrace_$tag.log"; [ $rc -ne 0 ] && fatal "$st" $rc ;;
+    swpmc:*|pathtrace:*|pathpmc:*)
+      # swpmc:K=V,..  FETCH/WRITE PMC passes of tools/prof_switch.py with env overrides;
+      # pathtrace:K=V,.. / pathpmc:K=V,..  kernel trace / PMC passes of tools/prof_path.py
+      kind=${st%%:*}; envs=${st#*:}; tag=$(echo "$envs" | tr ',=' '__')
+      case $kind in swpmc|pathpmc) cs="FETCH_SIZE WRITE_SIZE" ;; *) cs="TRACE" ;; esac
+      case $kind in swpmc) tgt=tools/prof_switch.py ;; *) tgt=tools/prof_path.py ;; esac
+      for c in $cs; do
+        if [ "$c" = TRACE ]; then args="--kernel-trace --stats"; else args="--pmc $c"; fi
+        ( export ${envs//,/ }; timeout -k 10 300 rocprofv3 $args --output-format csv \
+            -d "$OUT/${kind}_${tag}_$c" -o run -- python3 $tgt > "$OUT/${kind}_${tag}_$c.log" 2>&1 )
+        rc=$?; tail -2 "$OUT/${kind}_${tag}_$c.log"; [ $rc -ne 0 ] && fatal "$st $c" $rc
+      done ;;
     swprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/swprof" -o run -- \
         python3 tools/prof_switch.py > "$OUT/swprof.log" 2>&1

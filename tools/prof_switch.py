@@ -1,6 +1,7 @@
 """Profile target: the device packet-stream switch on 8 workers x NGA-256 packets of
 a config-3 bucket (run under rocprofv3 --kernel-trace --stats); the slot sort reads the
-pack kernels' packet descriptors (DESC=0: the packet headers)."""
+pack kernels' packet descriptors (DESC=0: the packet headers).  Env: V, SLOTS, ORDER (wm,
+rr, random), RUNS (tuning key 18), SPLIT=1 (split rows: 16-byte headers + 4V-byte payloads)."""
 import os
 import sys
 
@@ -30,10 +31,18 @@ if order != "wm":
 sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
 acts = torch.empty(stream.shape[0], dtype=torch.uint8, device=dev)
 use_desc = os.environ.get("DESC", "1") == "1"
+split = os.environ.get("SPLIT", "0") == "1"
+if split:
+    hdr = torch.zeros((stream.shape[0], 16), dtype=torch.uint8, device=dev)
+    hdr[:, :15] = stream[:, :15]
+    pay = stream[:, 15:15 + 4 * V].contiguous()
 for i in range(int(os.environ.get("REPS", 5))):
     sw.count.zero_()
     sw.frag.zero_()
-    sw.process(stream, acts, desc=desc if use_desc else None)
+    if split:
+        sw.process_split(hdr, pay, acts, desc=desc if use_desc else None)
+    else:
+        sw.process(stream, acts, desc=desc if use_desc else None)
 torch.cuda.synchronize()
 ok = torch.equal(stream.view(W, -1, stream.shape[1])[-1, :, 15:15 + 4 * V].contiguous().view(-1).view(torch.uint8)[:8], stream[stream.shape[0] // W * (W - 1), 15:23])
 print("done", stream.shape, int((acts == 1).sum()))
