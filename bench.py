@@ -974,20 +974,35 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
     # arrival order (the sort, unavoidably)
     gperm = torch.Generator(device=dev)
     gperm.manual_seed(77 + rank)
+    # worker_major_split: the worker-major batch in split rows (16-byte header rows + aligned
+    # 4V-byte payload rows: the same datagrams, include/ina.h), the run table path
     order = {"worker_major": None,
+             "worker_major_split": None,
              "round_robin": torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1),
              "worker_major_sorted": None,
              "shuffled": torch.randperm(npk_all, device=dev, generator=gperm)}
     for name in list(order):
         if orders is not None and name not in orders:
             del order[name]
-    def parity(perm):
+    def split_rows(rows):
+        h = torch.zeros((rows.shape[0], 16), dtype=torch.uint8, device=dev)
+        h[:, :15] = rows[:, :15]
+        return h, rows[:, 15:15 + 4 * V].contiguous()
+
+    def parity(perm, split=False):
         """A fresh switch over a pristine copy of the batch in this arrival order: every slot
         completes exactly once, and each sampled slot's completing packet carries the
-        wrapping int32 sum of the 8 workers' values (big-endian payload at byte 15)."""
+        wrapping int32 sum of the 8 workers' values (big-endian payload at byte 15, or the
+        payload row)."""
         cp = pristine.clone() if perm is None else pristine[perm]
         chk = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
-        a = chk.process(cp, desc=desc if perm is None else desc[perm])
+        if split:
+            hp, pp = split_rows(cp)
+            a = chk.process_split(hp, pp, desc=desc if perm is None else desc[perm])
+            cp[:, 15:15 + 4 * V] = pp
+            del hp, pp
+        else:
+            a = chk.process(cp, desc=desc if perm is None else desc[perm])
         pos = torch.arange(npk_all, device=dev) if perm is None else torch.argsort(perm)
         ts = torch.from_numpy(samp).to(dev)
         cand = torch.stack([pos[w * npk + ts] for w in range(W)])          # [W, samples]
@@ -1002,9 +1017,15 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
 
     for name, perm in order.items():
         st, ds = (stream, desc) if perm is None else (stream[perm], desc[perm])
+        split = name.endswith("_split")
+        if split:
+            hp, pp = split_rows(st)
+            call = lambda: sw.process_split(hp, pp, acts, desc=ds)   # noqa: E731
+        else:
+            call = lambda: sw.process(st, acts, desc=ds)             # noqa: E731
         ops.set_tuning(switch_runs=name != "worker_major_sorted")
         for _ in range(warm):
-            sw.process(st, acts, desc=ds)
+            call()
         barrier(world)
         # like the headline's avg_launch_us: one event pair around `reps` back-to-back calls
         # (a pair per call adds ~7 us of event overhead, tools/lab/event_overhead_lab.py;
@@ -1014,7 +1035,7 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(reps):
-                sw.process(st, acts, desc=ds)
+                call()
             e1.record(s)
             torch.cuda.synchronize()
             per_rep.append(e0.elapsed_time(e1) * 1e3 / reps)
@@ -1022,7 +1043,7 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            sw.process(st, acts, desc=ds)
+            call()
             e1.record(s)
             evs.append((e0, e1))
         torch.cuda.synchronize()
@@ -1033,8 +1054,11 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
                      "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
                      "ok": all_ranks_true(done == npk, world), "us_event_pair_per_call": round(us_pair, 2),
                      "batch_path": sw.batch_path(npk_all)}
-        del st, ds
-        res[name]["parity_spot_check"] = all_ranks_true(parity(perm), world)
+        if split:
+            res[name]["rows"] = "split: 16-byte header rows + 4V-byte payload rows"
+            del hp, pp
+        del st, ds, call
+        res[name]["parity_spot_check"] = all_ranks_true(parity(perm, split), world)
         ops.set_tuning(switch_runs=True)
         if world > 1:
             res[name]["aggregate_GBps"] = round(world * algo / us / 1e3, 1)
@@ -1199,8 +1223,10 @@ def run_reduce(args, rank, world, dev, backend):
         run_leg(line, "switch_c3_v32", lambda: measure_switch(dev, rank=rank, world=world, V=32, slots=1 << 20,
                                                               orders=("worker_major", "round_robin",
                                                                       "shuffled")))
-        run_leg(line, "packet_path", lambda: measure_packet_path(dev, rank=rank, world=world))
-        run_leg(line, "packet_path_split", lambda: measure_packet_path(dev, rank=rank, world=world, split=True))
+        # the INA step in the split-row layout (the device format: same datagrams on the wire,
+        # aligned payload rows), and in packed 1,040-byte rows beside it
+        run_leg(line, "packet_path", lambda: measure_packet_path(dev, rank=rank, world=world, split=True))
+        run_leg(line, "packet_path_packed", lambda: measure_packet_path(dev, rank=rank, world=world))
     if cpu_in is not None:
         run_leg(line, "cpu_baseline", lambda: cpu_baseline(args, *cpu_in))
     return line

@@ -83,8 +83,8 @@ def test_bench_json_line_contract():
         assert all(p["frac"] > 0 for p in r["hbm_phases"].values())   # 16 MiB: may replay from MALL
     sw = d["switch_c3"]                          # the packet-stream switch, measured live
     assert sw["algorithmic_bytes"] == 819_200 * 1040 + 102_400 * (1040 + 1029) + 819_200
-    paths = {"worker_major": "runs", "round_robin": "in_order", "worker_major_sorted": "sorted",
-             "shuffled": "sorted"}
+    paths = {"worker_major": "runs", "worker_major_split": "runs", "round_robin": "in_order",
+             "worker_major_sorted": "sorted", "shuffled": "sorted"}
     for order, path in paths.items():
         assert sw[order]["ok"] is True and sw[order]["slots_completed"] == 102_400
         assert 0 < sw[order]["frac"] < 1 and sw[order]["batch_path"] == path, order
@@ -100,12 +100,12 @@ def test_bench_json_line_contract():
     assert pp["parity_spot_check"] is True and pp["value"] > 0 and pp["ms_per_step"] > 0
     assert pp["roofline"]["bound"] == "hbm" and 0 < pp["roofline"]["frac"] < 1
     assert abs(pp["roofline"]["frac"] - pp["roofline"]["achieved"] / pp["roofline"]["peak"]) < 1e-3
-    for leg in (pp, d["packet_path_split"]):     # packed rows, and split rows (same datagrams)
+    for leg in (pp, d["packet_path_packed"]):    # split rows, and packed rows (same datagrams)
         assert leg["parity_spot_check"] is True and leg["value"] > 0 and leg["switch_batch_path"] == "runs"
         ph = leg["phases"]                       # the packs and the switch + PS pass apart
         assert 0 < ph["worker_packs"]["frac"] < 1 and 0 < ph["switch_and_ps"]["frac"] < 1
         assert ph["worker_packs"]["bytes"] + ph["switch_and_ps"]["bytes"] == leg["roofline"]["path_bytes_per_step"]
-    assert pp["rows"] == "packed" and d["packet_path_split"]["rows"] == "split"
+    assert pp["rows"] == "split" and d["packet_path_packed"]["rows"] == "packed"
     assert not any(isinstance(v, dict) and "error" in v for v in d.values())   # no leg raised
 
 

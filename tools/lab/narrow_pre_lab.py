@@ -58,7 +58,7 @@ def timed(fn):
 
 # parity: a fresh switch per library over pristine copies, two batches (the second finds the
 # first's count/frag/registers), everything compared
-state = {}
+state, paths = {}, {}
 for name in libs:
     use(name)
     sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
@@ -68,7 +68,8 @@ for name in libs:
         a1 = sw.process(st, desc=desc)
         a2 = ops.Switch(V, num_slots=slots, switch_id=1, device=dev).process_split(h, p, desc=desc)
         out += [a1, st, a2, h, p]
-    out += [sw.count.clone(), sw.frag.clone(), sw.regs.clone(), torch.tensor([sw.batch_path(W * npk)])]
+    out += [sw.count.clone(), sw.frag.clone(), sw.regs.clone()]
+    paths[name] = sw.batch_path(W * npk)
     state[name] = out
     del sw
 same = all(torch.equal(x, y) for x, y in zip(state["pre"], state["nopre"]))
@@ -87,5 +88,6 @@ use("pre")
 sw = sws["pre"]
 out = {k: round(statistics.median(v), 2) for k, v in res.items()}
 out["bytes_equal"] = same
+out["parity_batch_path"] = paths
 out["batch_path"] = sw.batch_path(W * npk)
 print(json.dumps(out, indent=1))
