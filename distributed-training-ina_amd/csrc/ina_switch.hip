@@ -287,10 +287,13 @@ int set_runs(int v) {
     g_runs = v ? 1 : 0;
     return INA_OK;
 }
-// ina_set_tuning key 19: the split chunk pass (detection, decision, then digits) for keys of
-// 19-22 bits only (0, default) or for every key width (1)
+// ina_set_tuning key 19: the split chunk pass (detection, decision, then digits) for every key
+// width (1, default) or for keys of 19-22 bits only (0).  Interleaved over packed and split
+// rows at 819,200 NGA-256 packets (tools/lab/switch_pre_lab.py, profiles/r04/lab): worker-
+// major -3.8 / -3.2 us, round-robin -6.1 / -5.4 us, a shuffled batch +5.6 / +4.9 us (it pays
+// the detection pass and one launch more); NIC arrival is structured, so split by default
 #ifndef INA_SWITCH_PRE_ALL
-#define INA_SWITCH_PRE_ALL 0
+#define INA_SWITCH_PRE_ALL 1
 #endif
 static std::atomic<int> g_pre_all{INA_SWITCH_PRE_ALL};
 int set_pre_all(int v) {

@@ -1011,7 +1011,7 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     exceeds 3,584 packets, else 4; or 4, 8); switch_runs lets batches of at most 64 runs of
     consecutive slots (worker-major arrival, PS acks in front) skip the slot sort (True, the
     default; False always sorts); switch_pre_all splits the sort's first pass into detection,
-    decision and digits for every key width (False, the default: keys of 19-22 bits only);
+    decision and digits for every key width (True, the default; False: keys of 19-22 bits only);
     unroll is the
     sum-reduce's 16-byte chunks per worker per thread."""
     lib = load()

@@ -80,8 +80,8 @@ const char* ina_last_error_string(void);
  * the average bucket exceeds 3,584 packets, else 4; or 4, 8), 18 switch batches made of at
  * most 64 runs of consecutive slots (worker-major arrival, PS acks in front) skip the slot
  * sort and run from a table of the runs (1, default; 0 = always sort), 19 the slot sort's
- * first pass split into detection + decision + digits for every key width (1) or only for
- * keys of 19-22 bits (0, default).
+ * first pass split into detection + decision + digits for every key width (1, default:
+ * structured batches then skip the digits) or only for keys of 19-22 bits (0).
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 

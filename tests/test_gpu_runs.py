@@ -200,6 +200,36 @@ def test_runs_tuning_off_takes_the_sort():
     check_batches(o, V, batches, "runs", use_desc=False, write_dropped=False)
 
 
+@pytest.mark.parametrize("pre_all", [False, True])
+@pytest.mark.parametrize("case", ["runs", "in_order", "sorted", "acks_behind"])
+def test_first_pass_whole_or_split(case, pre_all):
+    """ina_set_tuning key 19: the slot sort's first pass whole (keys of <= 18 bits, 0) or split
+    into detection + one-block decision + digits (1, the default) -- the same results on every
+    path (the run table, in slot order, the bucket sort), with and without descriptors."""
+    o = ops()
+    rng = np.random.default_rng(19 + len(case) + int(pre_all))
+    V, W, per = 64, 8, 600
+    stride = o.nga_stride(V)
+    specs = worker_major(W, per, seq0=3, acks=case != "acks_behind")
+    if case == "acks_behind":
+        specs = worker_major(W, per, seq0=3) + [(3, per, "ack")]
+    batches = []
+    for _ in range(2):
+        b = runs_batch(rng, V, specs, W, stride)
+        if case == "in_order":          # the workers' packets interleaved, slot by slot
+            b = b[np.argsort(np.arange(len(b)) % per, kind="stable")]
+        elif case == "sorted":
+            b = b[rng.permutation(len(b))]
+        batches.append(b)
+    path = {"runs": "runs", "in_order": None, "sorted": "sorted", "acks_behind": "runs"}[case]
+    o.set_tuning(switch_pre_all=pre_all)
+    try:
+        check_batches(o, V, batches, path)
+        check_batches(o, V, batches, path, use_desc=False)
+    finally:
+        o.set_tuning(switch_pre_all=True)
+
+
 @pytest.mark.parametrize("V,W,per", [(256, 8, 700), (32, 4, 3000)])
 def test_runs_fused_ps_and_two_phase_equal_sorted(V, W, per):
     """The packet path's steady state through the run table -- the fused PS apply (one call

@@ -77,6 +77,13 @@ for st in $STAGES; do
             -d "$OUT/${kind}_${tag}_$c" -o run -- python3 $tgt > "$OUT/${kind}_${tag}_$c.log" 2>&1 )
         rc=$?; tail -2 "$OUT/${kind}_${tag}_$c.log"; [ $rc -ne 0 ] && fatal "$st $c" $rc
       done ;;
+    swsq:*)
+      # swsq:K=V,..  one PMC pass of SQ issue / wait counters over tools/prof_switch.py
+      envs=${st#swsq:}; tag=$(echo "$envs" | tr ',=' '__')
+      ( export ${envs//,/ }; timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY \
+          SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv \
+          -d "$OUT/swsq_$tag" -o run -- python3 tools/prof_switch.py > "$OUT/swsq_$tag.log" 2>&1 )
+      rc=$?; tail -2 "$OUT/swsq_$tag.log"; [ $rc -ne 0 ] && fatal "$st" $rc ;;
     swprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/swprof" -o run -- \
         python3 tools/prof_switch.py > "$OUT/swprof.log" 2>&1
