@@ -1198,10 +1198,10 @@ constexpr int kB = INA_SWITCH_BATCH;         // packets of a segment loaded at o
 #ifndef INA_SWITCH_GRID
 #define INA_SWITCH_GRID (1 << 20)
 #endif
-// the narrow (V <= 32) run over a run table loads slot s+1 while it runs slot s (0: one slot
-// at a time; a lab build's A/B switch)
-#ifndef INA_SWITCH_NARROW_PRE
-#define INA_SWITCH_NARROW_PRE 1
+// the narrow (V <= 32) run over a run table: 8 slots side by side per wave, the runs walked in
+// order (1), or one slot's 8 packets side by side (0; a lab build's A/B switch)
+#ifndef INA_SWITCH_NARROW_SLOTS
+#define INA_SWITCH_NARROW_SLOTS 1
 #endif
 static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWITCH_WIN_LARGE >= 1 &&
               INA_SWITCH_WIN_LARGE <= 64, "a window is at most one wave of keys");
@@ -1557,12 +1557,6 @@ __device__ __forceinline__ uint32_t from_prev_in_row(uint32_t x) {
 constexpr int kNarrowMaxV = 32;
 static_assert(kB == 8, "the narrow run puts a batch of 8 packets in 8 lane groups");
 
-// a narrow segment's first batch and slot state, loaded ahead (the runs path issues slot s+1's
-// loads before it runs slot s, so a wave has two slots' round trips in flight)
-struct NarrowPre {
-    u32x4s a, tl;              // chunk l of packet g (split: payload chunk l), the tail / header row
-    uint32_t cnt, frag;        // the slot's count and frag registers
-};
 // packet group g's row loads (lanes past L re-read chunk 0; the tail chunk is one request per
 // group); the caller's mypid is packet g's id
 template <bool kSplit>
@@ -1581,26 +1575,19 @@ __device__ __forceinline__ void narrow_load(const uint8_t* __restrict__ pkts, si
     }
 }
 
-template <bool kPs, bool kSplit, bool kPre = false, typename PidFn>
+template <bool kPs, bool kSplit, typename PidFn>
 __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                    size_t stride, uint8_t* __restrict__ pay,
                                                    uint8_t* __restrict__ actions,
                                                    const PsFuse& ps, uint32_t slot, bool ack_led,
-                                                   size_t q_begin, size_t q_end, PidFn&& pid_batch,
-                                                   const NarrowPre* pre = nullptr) {
+                                                   size_t q_begin, size_t q_end, PidFn&& pid_batch) {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, l = lane & 7;      // packet group, value lane
     const int V = st.V;
     const int L = V >> 2;                       // value lanes per group (<= 8)
     const bool vl = l < L;
-    uint32_t cnt, frag;
-    if constexpr (kPre) {
-        cnt = __builtin_amdgcn_readfirstlane(pre->cnt);
-        frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(pre->frag);
-    } else {
-        cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
-        frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
-    }
+    uint32_t cnt = __builtin_amdgcn_readfirstlane((uint32_t)st.count[slot]);
+    uint32_t frag = ack_led ? 0u : __builtin_amdgcn_readfirstlane(st.frag[slot]);
     u32x4s reg = {0u, 0u, 0u, 0u};              // the slot's running registers, in every group
     bool have_reg = false;
     for (size_t q0 = q_begin; q0 < q_end; q0 += kB) {
@@ -1616,12 +1603,7 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
             lanepid = lane == b ? pid[b] : lanepid;
         }
         u32x4s a, tl;
-        if (kPre && q0 == q_begin) {
-            a = pre->a;
-            tl = pre->tl;
-        } else {
-            narrow_load<kSplit>(pkts, stride, pay, V, mypid, a, tl);
-        }
+        narrow_load<kSplit>(pkts, stride, pay, V, mypid, a, tl);
         const u32x4s hw = kSplit ? tl : a;            // header words (lane 8b: packet b's)
         // per-group outcome of the state machine: adds, overwrites, forwards, PS consumption,
         // collisions (group g's packet, in every lane of the group)
@@ -1891,6 +1873,184 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
     }
 }
 
+// Narrow packets (V <= 32) over a run table, slot-parallel: lane group g = lane / 8 owns slot
+// s0 + g of the wave's range, and the wave walks the runs in order (= each slot's arrival
+// order, ngaa.p4:120-196): run r's packets for slots s0 .. s0+7 are neighbouring rows, so one
+// wave instruction reads them contiguously (lane l: payload chunk l; packed rows: row chunk
+// l + 1, the header chunk 0 for every lane of the group).  The count / frag state machine
+// (ngaa.p4:64-82, fragcheck.p4:14-57) and the Processor add (processor.p4:14-24) run in every
+// group at once on group-uniform VGPRs -- no per-packet scalar walk and no cross-group scan,
+// about a tenth of run_segment_narrow's instructions per packet.  kP runs' loads are in
+// flight together.  Same results as the per-slot walk, packet for packet.
+constexpr int kSlotRunsInFlight = 4;
+template <bool kPs, bool kSplit>
+__device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                                  size_t stride, uint8_t* __restrict__ pay,
+                                                  uint8_t* __restrict__ actions, const PsFuse& ps,
+                                                  uint32_t R, uint32_t rpos, uint32_t rlen, uint32_t rslot,
+                                                  bool rack, uint32_t lo, uint32_t hi, size_t wave,
+                                                  size_t nwaves) {
+    constexpr int kP = kSlotRunsInFlight;
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 3, l = lane & 7;
+    const int V = st.V, L = V >> 2;
+    const bool vl = l < L;
+    // whole groups of 8 slots per wave
+    size_t per = ((size_t)(hi - lo) + nwaves - 1) / nwaves;
+    per = (per + 7) & ~(size_t)7;
+    const size_t s_begin = (size_t)lo + wave * per;
+    const size_t s_end = s_begin + per < (size_t)hi ? s_begin + per : (size_t)hi;
+    const uint32_t rack_u = rack ? 1u : 0u;
+    for (size_t s8 = s_begin; s8 < s_end; s8 += 8) {
+        const uint32_t slot = (uint32_t)(s8 + (size_t)g);
+        const bool sv = s8 + (size_t)g < s_end;
+        uint32_t cnt = 0, frag = 0;
+        if (sv) {
+            cnt = st.count[slot];
+            frag = st.frag[slot];
+        }
+        u32x4s reg = {0u, 0u, 0u, 0u};
+        bool have_reg = false, touched = false;
+        for (uint32_t r0 = 0; r0 < R; r0 += kP) {
+            // issue kP runs' loads: the group's packet of run r (if the run holds the slot)
+            u32x4s m[kP], h[kP];
+            uint32_t pid[kP];
+            bool in[kP], ackr[kP];
+#pragma unroll
+            for (int j = 0; j < kP; ++j) {
+                const uint32_t r = r0 + (uint32_t)j;
+                const uint32_t rr = r < R ? r : 0u;
+                const uint32_t rs = __builtin_amdgcn_readlane(rslot, rr);
+                const uint32_t rl = r < R ? __builtin_amdgcn_readlane(rlen, rr) : 0u;
+                const uint32_t rp = __builtin_amdgcn_readlane(rpos, rr);
+                ackr[j] = __builtin_amdgcn_readlane(rack_u, rr) != 0u;
+                const uint32_t off = slot - rs;
+                in[j] = sv && off < rl;
+                pid[j] = rp + off;
+                if (in[j] && !ackr[j]) {                  // a run of PS acks needs no read
+                    if constexpr (kSplit) {
+                        m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
+                                     (vl ? l : 0));
+                        h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+                    } else {
+                        const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
+                        m[j] = sw_ld(pk + (vl ? l + 1 : 1));
+                        h[j] = *pk;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kP; ++j) {
+                if (!__ballot(in[j])) continue;          // no slot of this wave in run r0 + j
+                if (!in[j]) continue;
+                touched = true;
+                const uint32_t h1 = h[j].y, h2 = h[j].z, h3 = h[j].w;
+                const bool is_ack = ackr[j] || ((h1 >> 14) & 1u);
+                uint8_t act;
+                if (is_ack) {                            // reset_id (fragcheck.p4:26-31)
+                    frag = 0;
+                    act = INA_ACT_FWD_ACK;
+                } else {
+                    const uint32_t hcount = h1 & 0xFFu;
+                    const uint32_t frag_in = __builtin_bswap32((h2 >> 24) | (h3 << 8));
+                    if (frag == 0) frag = frag_in;       // write_read_id (fragcheck.p4:14-24)
+                    if (frag != frag_in) {               // collision (ngaa.p4:177-181): the flag byte
+                        act = INA_ACT_FWD_COLLISION;
+                        if (l == 0)
+                            reinterpret_cast<uint32_t*>(pkts + (size_t)pid[j] * (kSplit ? 16 : stride))[1] =
+                                h1 | ((uint32_t)INA_FLAG_COLLISION << 8);
+                    } else {
+                        cnt = (cnt + 1u) & 0xFFu;        // read_add_count (ngaa.p4:66-78)
+                        if (cnt == hcount) cnt = 0;
+                        const bool first = cnt == 1u;
+                        u32x4s v;                        // values 4l..4l+3
+                        if constexpr (kSplit) {
+                            v.x = __builtin_bswap32(m[j].x); v.y = __builtin_bswap32(m[j].y);
+                            v.z = __builtin_bswap32(m[j].z); v.w = __builtin_bswap32(m[j].w);
+                        } else {
+                            // value 4l starts at the last byte of chunk l: the previous lane's
+                            // chunk, or the header chunk for the group's lane 0
+                            const uint32_t pw = l == 0 ? h3 : from_prev_in_row(m[j].w);
+                            v.x = dec_be(m[j].x, pw);
+                            v.y = dec_be(m[j].y, m[j].x);
+                            v.z = dec_be(m[j].z, m[j].y);
+                            v.w = dec_be(m[j].w, m[j].z);
+                        }
+                        if (first) {                     // processor.p4:16-21
+                            reg = v;
+                        } else {
+                            if (!have_reg)               // adds to a stored register: load it now
+                                reg = vl ? *reinterpret_cast<const u32x4s*>(st.regs + (size_t)slot * V + 4 * l)
+                                         : u32x4s{0u, 0u, 0u, 0u};
+                            reg += v;
+                        }
+                        have_reg = true;
+                        act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
+                        const uint32_t ps_slot = frag_in - ps.seq0;
+                        const bool consumed = kPs && act == INA_ACT_FWD_AGG && ps_slot < ps.nslots;
+                        if (kPs && consumed) {           // launch.py:46-50 with the switch's sum
+                            const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)l;
+                            if (vl && e0 + 4 <= ps.n) {
+                                const f32x4s lc = *reinterpret_cast<const f32x4s*>(ps.local + e0);
+                                f32x4s o;
+                                o.x = __fadd_rn(lc.x, __fmul_rn(__fmul_rn((float)(int32_t)reg.x, ps.inv), ps.ws));
+                                o.y = __fadd_rn(lc.y, __fmul_rn(__fmul_rn((float)(int32_t)reg.y, ps.inv), ps.ws));
+                                o.z = __fadd_rn(lc.z, __fmul_rn(__fmul_rn((float)(int32_t)reg.z, ps.inv), ps.ws));
+                                o.w = __fadd_rn(lc.w, __fmul_rn(__fmul_rn((float)(int32_t)reg.w, ps.inv), ps.ws));
+                                __builtin_nontemporal_store(o, reinterpret_cast<f32x4s*>(ps.out + e0));
+                            } else if (vl) {
+                                const uint32_t rv[4] = {reg.x, reg.y, reg.z, reg.w};
+                                for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
+                                    ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
+                                                               __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
+                            }
+                            if (l == 0 && ps.acks) {     // the PS ack (fragcheck.p4:26-31)
+                                u32x4s hd = h[j];
+                                hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+                                if constexpr (!kSplit) hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                                *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
+                                if (ps.ack_desc) ps.ack_desc[ps_slot] = uint2{hd.y, hd.z};
+                            }
+                        }
+                        if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
+                            // out_value -> the packet (processor.p4:22)
+                            if constexpr (kSplit) {
+                                const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
+                                               __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
+                                if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) + l);
+                            } else {
+                                // chunk l + 1: bytes 1..3 of values 4l..4l+3, then byte 0 of value
+                                // 4l + 4 (the next lane's; the group's last value lane keeps the
+                                // padding byte); lane 0 also rewrites the header chunk's byte 15
+                                u32x4s* dst = reinterpret_cast<u32x4s*>(pkts + (size_t)pid[j] * stride);
+                                const uint32_t nx = from_next_in_row(reg.x);
+                                u32x4s e;
+                                e.x = enc_lo(reg.x, reg.y);
+                                e.y = enc_lo(reg.y, reg.z);
+                                e.z = enc_lo(reg.z, reg.w);
+                                e.w = enc_lo(reg.w, l < L - 1 ? nx : m[j].w);
+                                if (vl) sw_st(e, dst + l + 1);
+                                if (l == 0) {
+                                    u32x4s c0 = h[j];
+                                    c0.w = (c0.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                                    sw_st(c0, dst);
+                                }
+                            }
+                        }
+                    }
+                }
+                if (l == 0) actions[pid[j]] = act;
+            }
+        }
+        if (touched && l == 0) {
+            st.count[slot] = (uint8_t)cnt;
+            st.frag[slot] = frag;
+        }
+        if (have_reg && vl)
+            __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
+    }
+}
+
 // The run kernel's work over a batch of dense ascending runs (the run table the bucket
 // pass wrote, see kRunsMax): lane r holds run r; each wave takes one contiguous range of
 // slots (one pass of the grid) and runs slot s's segment -- the packets start_r + s -
@@ -1929,92 +2089,10 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
     const size_t per = ((size_t)(hi - lo) + nwaves - 1) / nwaves;
     const size_t s_begin = (size_t)lo + wave * per;
     const size_t s_end = s_begin + per < (size_t)hi ? s_begin + per : (size_t)hi;
-#if INA_SWITCH_NARROW_PRE
+#if INA_SWITCH_NARROW_SLOTS
     if constexpr (kNarrow) {
-        // NGA-32: a slot's 8 packets are one 144-byte row each, a single load per lane, so one
-        // slot's round trips leave the memory system idle.  Slot s+1's state and first batch
-        // are loaded before slot s runs (slots are independent, ngaa.p4:87-168; no wave
-        // touches another's slots), two slots' loads in flight per wave.
-        struct SlotInfo {
-            unsigned long long m;                     // the runs holding the slot (ack removed)
-            bool ack_led;
-            uint32_t p_ack;                           // the leading ack's packet
-        };
-        auto info = [&](size_t s) {
-            SlotInfo si{0ull, false, 0u};
-            const uint32_t off = (uint32_t)s - rslot;
-            const bool in = off < rlen;
-            si.m = __ballot(in);
-            if (si.m) {
-                const int l0 = __builtin_ctzll(si.m);
-                si.ack_led = (__ballot(in && rack) >> l0) & 1ull;
-                if (si.ack_led) {
-                    si.p_ack = __builtin_amdgcn_readlane(rpos + off, l0);
-                    si.m &= si.m - 1;
-                }
-            }
-            return si;
-        };
-        const int g = lane >> 3;
-        auto preload = [&](size_t s, const SlotInfo& si, NarrowPre& p) {
-            const uint32_t pidv = rpos + ((uint32_t)s - rslot);
-            unsigned long long mm = si.m;
-            uint32_t first = 0u, mypid = 0u;
-            bool set = false;
-#pragma unroll
-            for (int b = 0; b < kB; ++b) {
-                if (mm) {
-                    const uint32_t v = __builtin_amdgcn_readlane(pidv, __builtin_ctzll(mm));
-                    mm &= mm - 1;
-                    first = b == 0 ? v : first;
-                    if (g == b) { mypid = v; set = true; }
-                }
-            }
-            if (!set) mypid = first;                  // groups past the segment repeat packet 0
-            p.cnt = st.count[s];
-            p.frag = st.frag[s];
-            narrow_load<kSplit>(pkts, stride, pay, st.V, mypid, p.a, p.tl);
-        };
-        // run slot s from (ci, cp) after issuing slot s+1's loads into (ni, np)
-        auto step = [&](size_t s, const SlotInfo& ci, const NarrowPre& cp, SlotInfo& ni, NarrowPre& np) {
-            ni = SlotInfo{0ull, false, 0u};
-            if (s + 1 < s_end) {
-                ni = info(s + 1);
-                if (ni.m) preload(s + 1, ni, np);
-            }
-            const uint32_t slot = (uint32_t)s;
-            if (ci.ack_led && lane == 0) {            // reset_id (fragcheck.p4:26-31), unread
-                actions[ci.p_ack] = INA_ACT_FWD_ACK;
-                if (!ci.m) st.frag[slot] = 0u;        // a lone ack
-            }
-            if (ci.m) {
-                unsigned long long m = ci.m;
-                const uint32_t pidv = rpos + (slot - rslot);
-                auto pids = [&](size_t, int nb, uint32_t (&pid)[kB]) {
-#pragma unroll
-                    for (int b = 0; b < kB; ++b) {
-                        if (b < nb) {
-                            const int l = __builtin_ctzll(m);
-                            m &= m - 1;
-                            pid[b] = __builtin_amdgcn_readlane(pidv, l);
-                        } else {
-                            pid[b] = 0u;
-                        }
-                    }
-                };
-                run_segment_narrow<kPs, kSplit, true>(st, pkts, stride, pay, actions, ps, slot, ci.ack_led, 0,
-                                                      (size_t)__builtin_popcountll(ci.m), pids, &cp);
-            }
-        };
-        // two register sets used in turn (no copy of a set whose loads are still in flight)
-        SlotInfo ia = s_begin < s_end ? info(s_begin) : SlotInfo{0ull, false, 0u}, ib;
-        NarrowPre pa{}, pb{};
-        if (ia.m) preload(s_begin, ia, pa);
-        for (size_t s = s_begin; s < s_end; s += 2) {
-            step(s, ia, pa, ib, pb);
-            if (s + 1 >= s_end) break;
-            step(s + 1, ib, pb, ia, pa);
-        }
+        runs_slots_narrow<kPs, kSplit>(st, pkts, stride, pay, actions, ps, R, rpos, rlen, rslot, rack, lo, hi,
+                                       wave, nwaves);
         return;
     }
 #endif

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Narrow-run lab (experiment only): the NGA-32 run over a run table with slot s+1's loads
-issued before slot s runs (INA_SWITCH_NARROW_PRE=1, the in-tree libina.so) against one slot at
-a time (tools/lab/libina_nopre.so: make -C distributed-training-ina_amd/csrc
-OUT=../../tools/lab/libina_nopre.so BUILD=build_nopre EXTRA=-DINA_SWITCH_NARROW_PRE=0).
+"""Narrow-run lab (experiment only): the NGA-32 run over a run table slot-parallel (8 slots per
+wave, the runs walked in order: INA_SWITCH_NARROW_SLOTS=1, the in-tree libina.so) against one
+slot's 8 packets side by side (tools/lab/libina_noslots.so: make -C
+distributed-training-ina_amd/csrc OUT=../../tools/lab/libina_noslots.so BUILD=build_noslots
+EXTRA=-DINA_SWITCH_NARROW_SLOTS=0).  (Round 4's first try, slot s+1's loads issued before slot
+s runs, measured 541.8 vs 547.8 us packed, 488.2 vs 491.3 split: profiles/r04/lab/narrow_pre_lab.log.)
 Config 3 as NGA-32 packets (8 workers x 819,200, 2^20-slot pool, descriptors) in worker-major
 arrival, packed and split rows, and the same batch with the previous step's PS acks in front;
 HIP events around K back-to-back process() calls, interleaved over rounds, medians in us.
@@ -19,7 +21,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
 from ina_amd import _lib, ops  # noqa: E402
 
-libs = {"pre": _lib.load(), "nopre": _lib.open_library(os.path.join(HERE, "libina_nopre.so"))}
+libs = {"slots": _lib.load(), "segments": _lib.open_library(os.path.join(HERE, "libina_noslots.so"))}
 dev = torch.device("cuda")
 W, n, V, slots = 8, 26_214_400, 32, 1 << 20
 npk = n // V
@@ -72,7 +74,7 @@ for name in libs:
     paths[name] = sw.batch_path(W * npk)
     state[name] = out
     del sw
-same = all(torch.equal(x, y) for x, y in zip(state["pre"], state["nopre"]))
+same = all(torch.equal(x, y) for x, y in zip(state["slots"], state["segments"]))
 del state
 
 # one switch (and sort scratch) per library: each library keeps its own call epochs
@@ -84,8 +86,8 @@ for r in range(ROUNDS):
         sw = sws[name]
         res.setdefault(f"packed/{name}", []).append(timed(lambda: sw.process(stream, acts, desc=desc)))
         res.setdefault(f"split/{name}", []).append(timed(lambda: sw.process_split(hdr, pay, acts, desc=desc)))
-use("pre")
-sw = sws["pre"]
+use("slots")
+sw = sws["slots"]
 out = {k: round(statistics.median(v), 2) for k, v in res.items()}
 out["bytes_equal"] = same
 out["parity_batch_path"] = paths
