@@ -1792,6 +1792,255 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
         __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
 }
 
+constexpr int kSlotRunsInFlight = 4;
+// one packet of a lane group's slot (group-uniform: every lane of the group runs it with the
+// same header): ack / collision / count / Processor add, the PS step, the rewritten packet
+// and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
+// header chunk / header row; ack_known: a PS ack by its sort key (then m and h are unread)
+template <bool kPs, bool kSplit>
+__device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                             size_t stride, uint8_t* __restrict__ pay,
+                                             uint8_t* __restrict__ actions, const PsFuse& ps, uint32_t slot,
+                                             uint32_t pid, const u32x4s& m, const u32x4s& h, bool ack_known,
+                                             uint32_t& cnt, uint32_t& frag, u32x4s& reg, bool& have_reg) {
+    // neighbour lanes' words go through LDS, not DPP: a DPP move whose source lane is disabled
+    // returns its fallback, and the compiler may narrow EXEC around a DPP that feeds a per-lane
+    // select (it did: l == 0 ? h3 : row_shr(m.w) became a branch on l != 0).  Every lane of the
+    // group stores, then reads its neighbour's word (LDS executes one wave's ops in order)
+    __shared__ uint32_t s_xch[kSwBlock];
+    const int l = threadIdx.x & 7;
+    const int V = st.V, L = V >> 2;
+    const bool vl = l < L;
+    const uint32_t h1 = h.y, h2 = h.z, h3 = h.w;
+    const bool is_ack = ack_known || ((h1 >> 14) & 1u);
+    uint8_t act;
+    if (is_ack) {                            // reset_id (fragcheck.p4:26-31)
+        frag = 0;
+        act = INA_ACT_FWD_ACK;
+    } else {
+        const uint32_t hcount = h1 & 0xFFu;
+        const uint32_t frag_in = __builtin_bswap32((h2 >> 24) | (h3 << 8));
+        if (frag == 0) frag = frag_in;       // write_read_id (fragcheck.p4:14-24)
+        if (frag != frag_in) {               // collision (ngaa.p4:177-181): the flag byte
+            act = INA_ACT_FWD_COLLISION;
+            if (l == 0)
+                reinterpret_cast<uint32_t*>(pkts + (size_t)pid * (kSplit ? 16 : stride))[1] =
+                    h1 | ((uint32_t)INA_FLAG_COLLISION << 8);
+        } else {
+            cnt = (cnt + 1u) & 0xFFu;        // read_add_count (ngaa.p4:66-78)
+            if (cnt == hcount) cnt = 0;
+            const bool first = cnt == 1u;
+            u32x4s v;                        // values 4l..4l+3
+            if constexpr (kSplit) {
+                v.x = __builtin_bswap32(m.x); v.y = __builtin_bswap32(m.y);
+                v.z = __builtin_bswap32(m.z); v.w = __builtin_bswap32(m.w);
+            } else {
+                // value 4l starts at the last byte of chunk l: the previous lane's
+                // chunk, or the header chunk for the group's lane 0
+                s_xch[threadIdx.x] = m.w;
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t pw = l == 0 ? h3 : s_xch[threadIdx.x - 1];
+                __builtin_amdgcn_wave_barrier();
+                v.x = dec_be(m.x, pw);
+                v.y = dec_be(m.y, m.x);
+                v.z = dec_be(m.z, m.y);
+                v.w = dec_be(m.w, m.z);
+            }
+            if (first) {                     // processor.p4:16-21
+                reg = v;
+            } else {
+                if (!have_reg)               // adds to a stored register: load it now
+                    reg = vl ? *reinterpret_cast<const u32x4s*>(st.regs + (size_t)slot * V + 4 * l)
+                             : u32x4s{0u, 0u, 0u, 0u};
+                reg += v;
+            }
+            have_reg = true;
+            act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
+            const uint32_t ps_slot = frag_in - ps.seq0;
+            const bool consumed = kPs && act == INA_ACT_FWD_AGG && ps_slot < ps.nslots;
+            if (kPs && consumed) {           // launch.py:46-50 with the switch's sum
+                const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)l;
+                if (vl && e0 + 4 <= ps.n) {
+                    const f32x4s lc = *reinterpret_cast<const f32x4s*>(ps.local + e0);
+                    f32x4s o;
+                    o.x = __fadd_rn(lc.x, __fmul_rn(__fmul_rn((float)(int32_t)reg.x, ps.inv), ps.ws));
+                    o.y = __fadd_rn(lc.y, __fmul_rn(__fmul_rn((float)(int32_t)reg.y, ps.inv), ps.ws));
+                    o.z = __fadd_rn(lc.z, __fmul_rn(__fmul_rn((float)(int32_t)reg.z, ps.inv), ps.ws));
+                    o.w = __fadd_rn(lc.w, __fmul_rn(__fmul_rn((float)(int32_t)reg.w, ps.inv), ps.ws));
+                    __builtin_nontemporal_store(o, reinterpret_cast<f32x4s*>(ps.out + e0));
+                } else if (vl) {
+                    const uint32_t rv[4] = {reg.x, reg.y, reg.z, reg.w};
+                    for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
+                        ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
+                                                   __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
+                }
+                if (l == 0 && ps.acks) {     // the PS ack (fragcheck.p4:26-31)
+                    u32x4s hd = h;
+                    hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+                    if constexpr (!kSplit) hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                    *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
+                    if (ps.ack_desc) ps.ack_desc[ps_slot] = uint2{hd.y, hd.z};
+                }
+            }
+            if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
+                // out_value -> the packet (processor.p4:22)
+                if constexpr (kSplit) {
+                    const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
+                                   __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
+                    if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid * (size_t)(4 * V)) + l);
+                } else {
+                    // chunk l + 1: bytes 1..3 of values 4l..4l+3, then byte 0 of value
+                    // 4l + 4 (the next lane's; the group's last value lane keeps the
+                    // padding byte); lane 0 also rewrites the header chunk's byte 15
+                    u32x4s* dst = reinterpret_cast<u32x4s*>(pkts + (size_t)pid * stride);
+                    s_xch[threadIdx.x] = reg.x;
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t nx = l < L - 1 ? s_xch[threadIdx.x + 1] : m.w;
+                    __builtin_amdgcn_wave_barrier();
+                    u32x4s e;
+                    e.x = enc_lo(reg.x, reg.y);
+                    e.y = enc_lo(reg.y, reg.z);
+                    e.z = enc_lo(reg.z, reg.w);
+                    e.w = enc_lo(reg.w, nx);
+                    if (vl) sw_st(e, dst + l + 1);
+                    if (l == 0) {
+                        u32x4s c0 = h;
+                        c0.w = (c0.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
+                        sw_st(c0, dst);
+                    }
+                }
+            }
+        }
+    }
+    if (l == 0) actions[pid] = act;
+}
+
+// Narrow packets (V <= 32) in sorted order (the bucket sort's arrays, or a batch already in
+// slot order read in place), segment-parallel: each wave takes windows of `win` sorted
+// positions, and its 8 lane groups take the segments that START in the window, 8 at a time
+// (group g: the g-th head), walking each segment's packets in position order (= arrival
+// order inside the slot, ngaa.p4:120-196) with kP positions' loads in flight.  Per packet the
+// same group_packet as the run-table path; a segment may run past the window's end.
+template <bool kPs, bool kSplit>
+__device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                                    uint8_t* __restrict__ pay, size_t npk, size_t stride,
+                                                    const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ ids,
+                                                    uint8_t* __restrict__ actions, uint32_t win, uint32_t kmask,
+                                                    const PsFuse& ps, size_t wave, size_t nwaves) {
+    constexpr int kP = kSlotRunsInFlight;
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 3, l = lane & 7;
+    const int V = st.V, L = V >> 2;
+    const bool vl = l < L;
+    const uint32_t NS = st.num_slots;
+    // the window's packet ids and ack hints, for the lane groups to pick from (through LDS,
+    // written by every lane of the wave: see group_packet on DPP / permutes and EXEC)
+    __shared__ uint32_t s_wid[kSwBlock], s_wack[kSwBlock];
+    const int wb = (int)threadIdx.x & ~63;
+    for (size_t w0 = wave * win; w0 < npk; w0 += nwaves * win) {
+        const size_t i = w0 + (size_t)lane;
+        const uint32_t kr = i < npk ? keys[i] : NS;
+        const uint32_t ki = kr & kmask;                   // slot (bit 31: PS-ack hint)
+        const uint32_t idw = i < npk ? (ids ? ids[i] : (uint32_t)i) : 0u;
+        const uint32_t kp = (i > 0 && i <= npk) ? (keys[i - 1] & kmask) : 0xFFFFFFFFu;
+        const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
+        __builtin_amdgcn_wave_barrier();
+        s_wid[threadIdx.x] = idw;
+        s_wack[threadIdx.x] = (kr & ~kmask) != 0u ? 1u : 0u;   // a PS ack by its key (with the hint)
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long hm = __ballot(head);
+        while (hm) {
+            // up to 8 segments: group g takes the g-th head's [start, end)
+            uint32_t hslot = 0, hst = 0, hlen = 0, maxlen = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                if (!hm) break;
+                const int hl = __builtin_ctzll(hm);
+                hm &= hm - 1;
+                const uint32_t slot_b = __builtin_amdgcn_readlane(ki, hl);
+                size_t end;
+                const unsigned long long dm = __ballot(ki != slot_b) & ~((2ull << hl) - 1ull);
+                if (dm) {
+                    end = w0 + (size_t)__builtin_ctzll(dm);
+                } else {
+                    size_t j0 = w0 + 64;
+                    for (;;) {
+                        const size_t j = j0 + (size_t)lane;
+                        const bool diff = j >= npk || (keys[j] & kmask) != slot_b;
+                        const unsigned long long mm = __ballot(diff);
+                        if (mm) { end = j0 + (size_t)__builtin_ctzll(mm); break; }
+                        j0 += 64;
+                    }
+                }
+                const uint32_t len_b = (uint32_t)(end - (w0 + (size_t)hl));
+                maxlen = len_b > maxlen ? len_b : maxlen;
+                if (g == b) {
+                    hslot = slot_b;
+                    hst = (uint32_t)hl;                   // window-relative start
+                    hlen = len_b;
+                }
+            }
+            const bool has = hlen != 0;
+            uint32_t cnt = 0, frag = 0;
+            if (has) {
+                cnt = st.count[hslot];
+                frag = st.frag[hslot];
+            }
+            u32x4s reg = {0u, 0u, 0u, 0u};
+            bool have_reg = false;
+            for (uint32_t k0 = 0; k0 < maxlen; k0 += kP) {
+                u32x4s m[kP], h[kP];
+                uint32_t pid[kP];
+                bool in[kP], acq[kP];
+#pragma unroll
+                for (int j = 0; j < kP; ++j) {
+                    const uint32_t k = k0 + (uint32_t)j;
+                    const uint32_t q = hst + k;           // window-relative position
+                    in[j] = has && k < hlen;
+                    // id and ack hint: the window's (LDS), past the window from memory
+                    pid[j] = 0u;
+                    acq[j] = false;
+                    if (in[j]) {
+                        if (q < 64u) {
+                            pid[j] = s_wid[wb + (int)q];
+                            acq[j] = s_wack[wb + (int)q] != 0u;
+                        } else {
+                            const size_t qa = w0 + (size_t)q;
+                            pid[j] = ids ? ids[qa] : (uint32_t)qa;
+                            acq[j] = (keys[qa] & ~kmask) != 0u;
+                        }
+                    }
+                    if (in[j] && !acq[j]) {
+                        if constexpr (kSplit) {
+                            m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
+                                         (vl ? l : 0));
+                            h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+                        } else {
+                            const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
+                            m[j] = sw_ld(pk + (vl ? l + 1 : 1));
+                            h[j] = *pk;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < kP; ++j) {
+                    if (!__ballot(in[j])) continue;
+                    if (!in[j]) continue;
+                    group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, hslot, pid[j], m[j], h[j], acq[j],
+                                              cnt, frag, reg, have_reg);
+                }
+            }
+            if (has && l == 0) {
+                st.count[hslot] = (uint8_t)cnt;
+                st.frag[hslot] = frag;
+            }
+            if (have_reg && vl)
+                __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)hslot * V + 4 * l));
+        }
+    }
+}
+
 template <bool kPs, bool kLat = false, bool kNarrow = false, bool kSplit = false>
 __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                  uint8_t* __restrict__ pay, size_t npk, size_t stride,
@@ -1800,6 +2049,13 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                                  uint8_t* __restrict__ actions, uint32_t win,
                                                  uint32_t kmask, const PsFuse& ps, size_t wave,
                                                  size_t nwaves) {
+#if INA_SWITCH_NARROW_SLOTS
+    if constexpr (kNarrow) {
+        window_slots_narrow<kPs, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps, wave,
+                                         nwaves);
+        return;
+    }
+#endif
     const int lane = threadIdx.x & 63;
     const uint32_t NS = st.num_slots;
     // each wave takes windows of 64 sorted positions and processes the segments that
@@ -1882,7 +2138,6 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
 // group at once on group-uniform VGPRs -- no per-packet scalar walk and no cross-group scan,
 // about a tenth of run_segment_narrow's instructions per packet.  kP runs' loads are in
 // flight together.  Same results as the per-slot walk, packet for packet.
-constexpr int kSlotRunsInFlight = 4;
 template <bool kPs, bool kSplit>
 __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                   size_t stride, uint8_t* __restrict__ pay,
@@ -1944,102 +2199,8 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                 if (!__ballot(in[j])) continue;          // no slot of this wave in run r0 + j
                 if (!in[j]) continue;
                 touched = true;
-                const uint32_t h1 = h[j].y, h2 = h[j].z, h3 = h[j].w;
-                const bool is_ack = ackr[j] || ((h1 >> 14) & 1u);
-                uint8_t act;
-                if (is_ack) {                            // reset_id (fragcheck.p4:26-31)
-                    frag = 0;
-                    act = INA_ACT_FWD_ACK;
-                } else {
-                    const uint32_t hcount = h1 & 0xFFu;
-                    const uint32_t frag_in = __builtin_bswap32((h2 >> 24) | (h3 << 8));
-                    if (frag == 0) frag = frag_in;       // write_read_id (fragcheck.p4:14-24)
-                    if (frag != frag_in) {               // collision (ngaa.p4:177-181): the flag byte
-                        act = INA_ACT_FWD_COLLISION;
-                        if (l == 0)
-                            reinterpret_cast<uint32_t*>(pkts + (size_t)pid[j] * (kSplit ? 16 : stride))[1] =
-                                h1 | ((uint32_t)INA_FLAG_COLLISION << 8);
-                    } else {
-                        cnt = (cnt + 1u) & 0xFFu;        // read_add_count (ngaa.p4:66-78)
-                        if (cnt == hcount) cnt = 0;
-                        const bool first = cnt == 1u;
-                        u32x4s v;                        // values 4l..4l+3
-                        if constexpr (kSplit) {
-                            v.x = __builtin_bswap32(m[j].x); v.y = __builtin_bswap32(m[j].y);
-                            v.z = __builtin_bswap32(m[j].z); v.w = __builtin_bswap32(m[j].w);
-                        } else {
-                            // value 4l starts at the last byte of chunk l: the previous lane's
-                            // chunk, or the header chunk for the group's lane 0
-                            const uint32_t pw = l == 0 ? h3 : from_prev_in_row(m[j].w);
-                            v.x = dec_be(m[j].x, pw);
-                            v.y = dec_be(m[j].y, m[j].x);
-                            v.z = dec_be(m[j].z, m[j].y);
-                            v.w = dec_be(m[j].w, m[j].z);
-                        }
-                        if (first) {                     // processor.p4:16-21
-                            reg = v;
-                        } else {
-                            if (!have_reg)               // adds to a stored register: load it now
-                                reg = vl ? *reinterpret_cast<const u32x4s*>(st.regs + (size_t)slot * V + 4 * l)
-                                         : u32x4s{0u, 0u, 0u, 0u};
-                            reg += v;
-                        }
-                        have_reg = true;
-                        act = cnt == 0 ? INA_ACT_FWD_AGG : INA_ACT_DROP;   // ngaa.p4:170-175
-                        const uint32_t ps_slot = frag_in - ps.seq0;
-                        const bool consumed = kPs && act == INA_ACT_FWD_AGG && ps_slot < ps.nslots;
-                        if (kPs && consumed) {           // launch.py:46-50 with the switch's sum
-                            const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)l;
-                            if (vl && e0 + 4 <= ps.n) {
-                                const f32x4s lc = *reinterpret_cast<const f32x4s*>(ps.local + e0);
-                                f32x4s o;
-                                o.x = __fadd_rn(lc.x, __fmul_rn(__fmul_rn((float)(int32_t)reg.x, ps.inv), ps.ws));
-                                o.y = __fadd_rn(lc.y, __fmul_rn(__fmul_rn((float)(int32_t)reg.y, ps.inv), ps.ws));
-                                o.z = __fadd_rn(lc.z, __fmul_rn(__fmul_rn((float)(int32_t)reg.z, ps.inv), ps.ws));
-                                o.w = __fadd_rn(lc.w, __fmul_rn(__fmul_rn((float)(int32_t)reg.w, ps.inv), ps.ws));
-                                __builtin_nontemporal_store(o, reinterpret_cast<f32x4s*>(ps.out + e0));
-                            } else if (vl) {
-                                const uint32_t rv[4] = {reg.x, reg.y, reg.z, reg.w};
-                                for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
-                                    ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
-                                                               __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
-                            }
-                            if (l == 0 && ps.acks) {     // the PS ack (fragcheck.p4:26-31)
-                                u32x4s hd = h[j];
-                                hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
-                                if constexpr (!kSplit) hd.w = (hd.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
-                                *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
-                                if (ps.ack_desc) ps.ack_desc[ps_slot] = uint2{hd.y, hd.z};
-                            }
-                        }
-                        if ((act != INA_ACT_DROP || st.write_dropped) && (!consumed || ps.keep_fwd)) {
-                            // out_value -> the packet (processor.p4:22)
-                            if constexpr (kSplit) {
-                                const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
-                                               __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
-                                if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) + l);
-                            } else {
-                                // chunk l + 1: bytes 1..3 of values 4l..4l+3, then byte 0 of value
-                                // 4l + 4 (the next lane's; the group's last value lane keeps the
-                                // padding byte); lane 0 also rewrites the header chunk's byte 15
-                                u32x4s* dst = reinterpret_cast<u32x4s*>(pkts + (size_t)pid[j] * stride);
-                                const uint32_t nx = from_next_in_row(reg.x);
-                                u32x4s e;
-                                e.x = enc_lo(reg.x, reg.y);
-                                e.y = enc_lo(reg.y, reg.z);
-                                e.z = enc_lo(reg.z, reg.w);
-                                e.w = enc_lo(reg.w, l < L - 1 ? nx : m[j].w);
-                                if (vl) sw_st(e, dst + l + 1);
-                                if (l == 0) {
-                                    u32x4s c0 = h[j];
-                                    c0.w = (c0.w & 0x00FFFFFFu) | (reg.x & 0xFF000000u);
-                                    sw_st(c0, dst);
-                                }
-                            }
-                        }
-                    }
-                }
-                if (l == 0) actions[pid[j]] = act;
+                group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, pid[j], m[j], h[j], ackr[j],
+                                          cnt, frag, reg, have_reg);
             }
         }
         if (touched && l == 0) {
@@ -2578,7 +2739,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         uint32_t win = npk <= 65536 ? (uint32_t)INA_SWITCH_WIN_SMALL : (uint32_t)INA_SWITCH_WIN_LARGE;
         // a narrow wave moves a whole segment per batch: a window of 64 sorted positions
         // (about 8 segments) keeps the grid at npk / 256 workgroups
-        if (narrow && npk > 65536) win = 64;
+        if (narrow && (INA_SWITCH_NARROW_SLOTS || npk > 65536)) win = 64;   // 8 lane groups: ~8 segments
         if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
         const size_t per_block = (size_t)win * (kSwBlock / 64);
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);

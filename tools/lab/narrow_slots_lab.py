@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
-"""Narrow-run lab (experiment only): the NGA-32 run over a run table slot-parallel (8 slots per
-wave, the runs walked in order: INA_SWITCH_NARROW_SLOTS=1, the in-tree libina.so) against one
-slot's 8 packets side by side (tools/lab/libina_noslots.so: make -C
-distributed-training-ina_amd/csrc OUT=../../tools/lab/libina_noslots.so BUILD=build_noslots
-EXTRA=-DINA_SWITCH_NARROW_SLOTS=0).  (Round 4's first try, slot s+1's loads issued before slot
-s runs, measured 541.8 vs 547.8 us packed, 488.2 vs 491.3 split: profiles/r04/lab/narrow_pre_lab.log.)
+"""Narrow-run lab (experiment only): the NGA-32 run kernel with lane groups taking 8 slots /
+segments side by side (INA_SWITCH_NARROW_SLOTS=1, the in-tree libina.so: the run table walked
+run by run, sorted windows segment by segment) against one slot's 8 packets side by side
+(tools/lab/libina_noslots.so: make -C distributed-training-ina_amd/csrc
+OUT=../../tools/lab/libina_noslots.so BUILD=build_noslots EXTRA=-DINA_SWITCH_NARROW_SLOTS=0).
+(Round 4's first try, slot s+1's loads issued before slot s runs, measured 541.8 vs 547.8 us
+packed, 488.2 vs 491.3 split: profiles/r04/lab/narrow_pre_lab.log.)
 Config 3 as NGA-32 packets (8 workers x 819,200, 2^20-slot pool, descriptors) in worker-major
-arrival, packed and split rows, and the same batch with the previous step's PS acks in front;
-HIP events around K back-to-back process() calls, interleaved over rounds, medians in us.
-Every library's actions, registers, count/frag and rewritten rows are compared byte for byte."""
+(run table), round-robin (in slot order) and shuffled (bucket sort) arrival, packed and split
+rows; HIP events around K back-to-back process() calls, interleaved over rounds, medians in
+us.  Each library's actions, registers, count/frag and rewritten rows are compared byte for
+byte (two batches on a fresh switch, the second finding the first's state)."""
 import json
 import os
 import statistics
@@ -33,17 +35,23 @@ for w in range(W):
     rows.append(p)
     descs.append(d)
     del b
-stream, desc = torch.cat(rows), torch.cat(descs)
+base, base_desc = torch.cat(rows), torch.cat(descs)
 del rows, descs
-hdr = torch.zeros((W * npk, 16), dtype=torch.uint8, device=dev)
-hdr[:, :15] = stream[:, :15]
-pay = stream[:, 15:15 + 4 * V].contiguous()
 acts = torch.empty(W * npk, dtype=torch.uint8, device=dev)
-K, ROUNDS = int(os.environ.get("K", 10)), int(os.environ.get("ROUNDS", 5))
+K, ROUNDS = int(os.environ.get("K", 10)), int(os.environ.get("ROUNDS", 4))
+perms = {"worker_major": None,
+         "round_robin": torch.arange(W * npk, device=dev).view(W, npk).t().reshape(-1),
+         "shuffled": torch.randperm(W * npk, device=dev, generator=g)}
 
 
 def use(name):
     _lib._lib = libs[name]
+
+
+def split_rows(st):
+    h = torch.zeros((st.shape[0], 16), dtype=torch.uint8, device=dev)
+    h[:, :15] = st[:, :15]
+    return h, st[:, 15:15 + 4 * V].contiguous()
 
 
 def timed(fn):
@@ -58,38 +66,41 @@ def timed(fn):
     return a.elapsed_time(b) * 1e3 / K
 
 
-# parity: a fresh switch per library over pristine copies, two batches (the second finds the
-# first's count/frag/registers), everything compared
-state, paths = {}, {}
-for name in libs:
-    use(name)
-    sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
-    out = []
-    for rep in range(2):
-        st, h, p = stream.clone(), hdr.clone(), pay.clone()
-        a1 = sw.process(st, desc=desc)
-        a2 = ops.Switch(V, num_slots=slots, switch_id=1, device=dev).process_split(h, p, desc=desc)
-        out += [a1, st, a2, h, p]
-    out += [sw.count.clone(), sw.frag.clone(), sw.regs.clone()]
-    paths[name] = sw.batch_path(W * npk)
-    state[name] = out
-    del sw
-same = all(torch.equal(x, y) for x, y in zip(state["slots"], state["segments"]))
-del state
-
-# one switch (and sort scratch) per library: each library keeps its own call epochs
-sws = {name: ops.Switch(V, num_slots=slots, switch_id=1, device=dev) for name in libs}
-res = {}
-for r in range(ROUNDS):
+out = {}
+for order, perm in perms.items():
+    stream, desc = (base, base_desc) if perm is None else (base[perm], base_desc[perm])
+    hdr, pay = split_rows(stream)
+    # parity: per library a fresh switch, two batches, packed and split rows
+    state, paths = {}, {}
     for name in libs:
         use(name)
-        sw = sws[name]
-        res.setdefault(f"packed/{name}", []).append(timed(lambda: sw.process(stream, acts, desc=desc)))
-        res.setdefault(f"split/{name}", []).append(timed(lambda: sw.process_split(hdr, pay, acts, desc=desc)))
+        sw, sws = (ops.Switch(V, num_slots=slots, switch_id=1, device=dev) for _ in range(2))
+        res = []
+        for rep in range(2):
+            st = stream.clone()
+            h, p = hdr.clone(), pay.clone()
+            res += [sw.process(st, desc=desc), st, sws.process_split(h, p, desc=desc), h, p]
+            del st, h, p
+        res += [sw.count.clone(), sw.frag.clone(), sw.regs.clone(), sws.regs.clone()]
+        paths[name] = sw.batch_path(W * npk)
+        state[name] = [x.cpu() for x in res]
+        del sw, sws, res
+        torch.cuda.empty_cache()
+    out[f"{order}/bytes_equal"] = all(torch.equal(x, y) for x, y in zip(state["slots"], state["segments"]))
+    out[f"{order}/batch_path"] = paths
+    del state
+    # timing: one switch (and sort scratch) per library, interleaved rounds
+    sws = {name: ops.Switch(V, num_slots=slots, switch_id=1, device=dev) for name in libs}
+    res = {}
+    for r in range(ROUNDS):
+        for name in libs:
+            use(name)
+            sw = sws[name]
+            res.setdefault(f"{order}/packed/{name}", []).append(timed(lambda: sw.process(stream, acts, desc=desc)))
+            res.setdefault(f"{order}/split/{name}", []).append(
+                timed(lambda: sw.process_split(hdr, pay, acts, desc=desc)))
+    out.update({k: round(statistics.median(v), 2) for k, v in res.items()})
+    del sws, stream, desc, hdr, pay
+    torch.cuda.empty_cache()
 use("slots")
-sw = sws["slots"]
-out = {k: round(statistics.median(v), 2) for k, v in res.items()}
-out["bytes_equal"] = same
-out["parity_batch_path"] = paths
-out["batch_path"] = sw.batch_path(W * npk)
 print(json.dumps(out, indent=1))
