@@ -976,11 +976,15 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
     gperm.manual_seed(77 + rank)
     # worker_major_split: the worker-major batch in split rows (16-byte header rows + aligned
     # 4V-byte payload rows: the same datagrams, include/ina.h), the run table path
+    rr = torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1)
     order = {"worker_major": None,
              "worker_major_split": None,
-             "round_robin": torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1),
+             "round_robin": rr,
+             "round_robin_split": rr,
              "worker_major_sorted": None,
              "shuffled": torch.randperm(npk_all, device=dev, generator=gperm)}
+    if orders is None:                         # NGA-256 defaults: the split row layout once
+        orders = ("worker_major", "worker_major_split", "round_robin", "worker_major_sorted", "shuffled")
     for name in list(order):
         if orders is not None and name not in orders:
             del order[name]
@@ -1221,7 +1225,8 @@ def run_reduce(args, rank, world, dev, backend):
         # behind the 15-byte header) at config-3 size: 6,553,600 packets, a 2^20-slot pool
         # (keys of 21 bits: the 2,048-bin chunk + bucket sort, and its run / in-order paths)
         run_leg(line, "switch_c3_v32", lambda: measure_switch(dev, rank=rank, world=world, V=32, slots=1 << 20,
-                                                              orders=("worker_major", "round_robin",
+                                                              orders=("worker_major", "worker_major_split",
+                                                                      "round_robin", "round_robin_split",
                                                                       "shuffled")))
         # the INA step in the split-row layout (the device format: same datagrams on the wire,
         # aligned payload rows), and in packed 1,040-byte rows beside it

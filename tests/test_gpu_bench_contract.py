@@ -92,7 +92,8 @@ def test_bench_json_line_contract():
     v32 = d["switch_c3_v32"]                     # the P4's own NGA-32 at config-3 size
     assert v32["V"] == 32 and v32["stride"] == 144
     assert v32["algorithmic_bytes"] == 6_553_600 * 144 + 819_200 * (144 + 133) + 6_553_600
-    for order, path in (("worker_major", "runs"), ("round_robin", "in_order"), ("shuffled", "sorted")):
+    for order, path in (("worker_major", "runs"), ("worker_major_split", "runs"), ("round_robin", "in_order"),
+                        ("round_robin_split", "in_order"), ("shuffled", "sorted")):
         assert v32[order]["ok"] is True and v32[order]["slots_completed"] == 819_200, order
         assert v32[order]["parity_spot_check"] is True and v32[order]["batch_path"] == path, order
         assert 0 < v32[order]["frac"] < 1, order
