@@ -655,11 +655,39 @@ constexpr int kRunsStart = 1, kRunsKey = 2 + kRunsMax;
 constexpr int kCtlWords = kCtlRuns + kRunsKey + kRunsMax;
 static_assert(kCtlWords * 4 <= 1024, "control block fits its 1 KiB");
 
-// kMode: 0 the chunk pass (keys, detection, digits, scatter); for keys of 19-22 bits, whose
-// 2,048-bin chunk pass holds one block per CU (136 KiB of LDS), the pass is split in two so a
-// structured batch never pays it: 1 = detection only (the arrival-order keys into kout, the
-// descent flag, the breaks; no digits, a small LDS footprint), then k_runs_decide, then 2 =
-// digits + scatter only, leaving at once when the batch is in slot order or dense runs.
+// the run table from the chunks' break records (a structured batch, total <= kRunsMax breaks),
+// by one block of kBkThr threads: thread t takes chunks 2t and 2t+1 (nch <= 2 x kBkThr), so the
+// entries land in chunk order = position order
+__device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk_cnt, const uint2* __restrict__ brk_ent,
+                                                uint32_t nch, uint32_t total, uint32_t npk,
+                                                uint32_t* __restrict__ unsorted, uint32_t epoch, uint32_t* wtot) {
+    const uint32_t c0 = 2u * threadIdx.x;
+    const uint32_t n0 = c0 < nch ? brk_cnt[c0] : 0u, n1 = c0 + 1 < nch ? brk_cnt[c0 + 1] : 0u;
+    const uint32_t ex = block_digit_scan(n0 + n1, wtot, 0u);
+    uint32_t* runs = unsorted + (kCtlRuns - kCtlEpochs);
+    for (uint32_t j = 0; j < n0; ++j) {
+        const uint2 e = brk_ent[(size_t)c0 * kRunsMax + j];
+        runs[kRunsStart + ex + j] = e.x;
+        runs[kRunsKey + ex + j] = e.y;
+    }
+    for (uint32_t j = 0; j < n1; ++j) {
+        const uint2 e = brk_ent[(size_t)(c0 + 1) * kRunsMax + j];
+        runs[kRunsStart + ex + n0 + j] = e.x;
+        runs[kRunsKey + ex + n0 + j] = e.y;
+    }
+    if (threadIdx.x == 0) {
+        runs[0] = total;
+        runs[kRunsStart + total] = npk;
+        unsorted[2] = epoch;                          // the run table is this call's
+    }
+}
+
+// kMode: 0 the chunk pass (keys, detection, digits, scatter); split in two (tuning key 19, the
+// default; always for keys of 19-22 bits, whose 2,048-bin chunk pass holds one block per CU)
+// so a structured batch never pays the digits: 1 = detection only (the arrival-order keys into
+// kout, the descent flag, the breaks; no digits, a small LDS footprint), then 2 = the decision
+// (every block sums the break counts; dense runs: block 0 writes the run table) and, for a
+// batch neither in slot order nor dense runs, the digits + scatter.
 template <int R, bool kDesc, int BINS, int kMode = 0>
 __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restrict__ pkts,
                                                         const uint2* __restrict__ desc, size_t npk,
@@ -677,8 +705,27 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     __shared__ uint32_t wbrk[kBkWaves];               // per-wave break counts
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
-    if constexpr (kMode == 2)                         // in slot order or dense runs: no sort
-        if (unsorted[0] != epoch || unsorted[2] == epoch) return;
+    if constexpr (kMode == 2) {
+        if (unsorted[0] != epoch) return;             // in slot order: no sort
+        if (brk_cnt) {
+            // the decision after the detection pass: every block sums the chunks' break counts
+            // (the same answer everywhere); a batch of at most kRunsMax dense runs gets its run
+            // table from block 0 and nobody sorts
+            uint32_t part = 0;
+            for (uint32_t cc = threadIdx.x; cc < (uint32_t)nch; cc += kBkThr) part += brk_cnt[cc];
+            const uint32_t inc = wave_incl_scan(part);
+            if (lane == 63) wtot[wv] = inc;
+            __syncthreads();
+            uint32_t total = 0;
+#pragma unroll
+            for (int w = 0; w < kBkWaves; ++w) total += wtot[w];
+            __syncthreads();                          // wtot is reused below
+            if (total <= (uint32_t)kRunsMax) {
+                if (c == 0) build_run_table(brk_cnt, brk_ent, (uint32_t)nch, total, (uint32_t)npk, unsorted, epoch, wtot);
+                return;
+            }
+        }
+    }
     const uint32_t nb = 1u << hbits;
     if constexpr (kMode != 1)
         for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
@@ -787,54 +834,6 @@ __device__ unsigned long long g_bk_t[kRsBins][6];
 #else
 #define BK_STAMP(q) do { } while (0)
 #endif
-
-// the run table from the chunks' break records (a structured batch, total <= kRunsMax breaks),
-// by one block of kBkThr threads: thread t takes chunks 2t and 2t+1 (nch <= 2 x kBkThr), so the
-// entries land in chunk order = position order
-__device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk_cnt, const uint2* __restrict__ brk_ent,
-                                                uint32_t nch, uint32_t total, uint32_t npk,
-                                                uint32_t* __restrict__ unsorted, uint32_t epoch, uint32_t* wtot) {
-    const uint32_t c0 = 2u * threadIdx.x;
-    const uint32_t n0 = c0 < nch ? brk_cnt[c0] : 0u, n1 = c0 + 1 < nch ? brk_cnt[c0 + 1] : 0u;
-    const uint32_t ex = block_digit_scan(n0 + n1, wtot, 0u);
-    uint32_t* runs = unsorted + (kCtlRuns - kCtlEpochs);
-    for (uint32_t j = 0; j < n0; ++j) {
-        const uint2 e = brk_ent[(size_t)c0 * kRunsMax + j];
-        runs[kRunsStart + ex + j] = e.x;
-        runs[kRunsKey + ex + j] = e.y;
-    }
-    for (uint32_t j = 0; j < n1; ++j) {
-        const uint2 e = brk_ent[(size_t)(c0 + 1) * kRunsMax + j];
-        runs[kRunsStart + ex + n0 + j] = e.x;
-        runs[kRunsKey + ex + n0 + j] = e.y;
-    }
-    if (threadIdx.x == 0) {
-        runs[0] = total;
-        runs[kRunsStart + total] = npk;
-        unsorted[2] = epoch;                          // the run table is this call's
-    }
-}
-
-// the split chunk pass of 19-22-bit keys (k_sort_chunks modes 1 / 2): one block decides between
-// the detection and the sort -- a batch not in slot order with at most kRunsMax breaks gets its
-// run table, and the digit pass and the bucket pass then leave at once
-__global__ __launch_bounds__(kBkThr) void k_runs_decide(const uint32_t* __restrict__ brk_cnt,
-                                                        const uint2* __restrict__ brk_ent, uint32_t nch,
-                                                        uint32_t npk, uint32_t* __restrict__ unsorted,
-                                                        uint32_t epoch) {
-    __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
-    if (unsorted[0] != epoch) return;                 // in slot order: the run reads the keys
-    const int lane = threadIdx.x & 63, wv = wave_in_block();
-    uint32_t part = 0;
-    for (uint32_t c = threadIdx.x; c < nch; c += kBkThr) part += brk_cnt[c];
-    const uint32_t inc = wave_incl_scan(part);
-    if (lane == 63) red[wv] = inc;
-    __syncthreads();
-    uint32_t total = 0;
-#pragma unroll
-    for (int w = 0; w < kBkWaves; ++w) total += red[w];
-    if (total <= (uint32_t)kRunsMax) build_run_table(brk_cnt, brk_ent, nch, total, npk, unsorted, epoch, red2);
-}
 
 // positions of bucket items i[r] (0 <= i < the bucket's size) in A's output: the run of the
 // last chunk whose bucket offset is <= i (s_dst: exclusive prefix of the run lengths over the
@@ -2616,7 +2615,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // never 0 (fresh scratch reads as "unsorted": the safe side); a stale epoch equal to
         // this one (2^32 calls later) also only costs the full sort
         // keys of 19-22 bits (2,048-bin digits) with the register-resident run kernel: the
-        // chunk pass split in two around k_runs_decide, so structured batches skip the digits
+        // chunk pass split in two (detection, then decision + digits), so structured batches skip the digits
         const bool pre = (sp.wide || g_pre_all.load()) && fast;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
@@ -2631,15 +2630,12 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             else if (ri == 1) INA_A_DETECT(kR1 / 4);
             else INA_A_DETECT(kR0 / 4);
 #undef INA_A_DETECT
-            if (runs_on)
-                hipLaunchKernelGGL(k_runs_decide, dim3(1), dim3(kBkThr), 0, s, ax.brk_cnt, ax.brk_ent,
-                                   (uint32_t)sp.nch, (uint32_t)npk, ax.unsorted, epoch);
 #define INA_A_SORT(RR)                                                                                \
             hipLaunchKernelGGL((sp.wide ? (desc ? &k_sort_chunks<RR, true, kBinsBig, 2> : &k_sort_chunks<RR, false, kBinsBig, 2>) \
                                         : (desc ? &k_sort_chunks<RR, true, kRsBins, 2> : &k_sort_chunks<RR, false, kRsBins, 2>)), \
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
-                               ax.unsorted, epoch, nullptr, ax.brk_ent)
+                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
             if (ri == 2) INA_A_SORT(kR2 / 4);
             else if (ri == 1) INA_A_SORT(kR1 / 4);
             else INA_A_SORT(kR0 / 4);
