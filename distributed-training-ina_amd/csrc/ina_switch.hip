@@ -194,8 +194,16 @@ __global__ __launch_bounds__(NW * 64) void k_switch_keys(const uint8_t* __restri
                                                           uint32_t* __restrict__ keys,
                                                           uint8_t* __restrict__ actions, int bits,
                                                           int shift, uint32_t* __restrict__ hist,
-                                                          size_t nch, int ack_hint) {
+                                                          size_t nch, int ack_hint,
+                                                          uint32_t* __restrict__ ctl, uint32_t epoch) {
     __shared__ uint32_t h[kRsBins];
+    // the control block's epochs say "sorted" for ina_switch_batch_path (the run kernel of the
+    // digit passes never reads them)
+    if (ctl && blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl[0] = epoch;
+        ctl[1] = epoch;
+        ctl[2] = 0u;
+    }
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
     const uint32_t nb = 1u << bits;
@@ -2694,9 +2702,12 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                     : ri == 1 ? &k_rs_scatter<true, kR1> : &k_rs_scatter<true, kR2>;
         const unsigned gd = (nb + kRsWaves - 1) / kRsWaves;
         if (do_sort) {
+        uint32_t lsd_epoch = g_sort_epoch.fetch_add(1u) + 1u;
+        if (lsd_epoch == 0u) lsd_epoch = g_sort_epoch.fetch_add(1u) + 1u;
         hipLaunchKernelGGL(k_keys, dim3(gc), dim3(kRsBlock), 0, s, pkts,
                            reinterpret_cast<const uint2*>(desc), npk, stride, st->num_slots,
-                           st->switch_id, k_in, actions, sp.bits, 0, ax.hist, sp.nch, ack_hint ? 1 : 0);
+                           st->switch_id, k_in, actions, sp.bits, 0, ax.hist, sp.nch, ack_hint ? 1 : 0,
+                           ax.unsorted, lsd_epoch);
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch keys launch%s", "");
         // (k_in, ids) -> (k_out, v_out) -> (k_in, v_in) -> ...
         for (int pass = 0; pass < sp.passes; ++pass) {

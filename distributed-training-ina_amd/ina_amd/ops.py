@@ -740,8 +740,9 @@ class Switch:
 
     def batch_path(self, npk: int) -> str:
         """Which slot-sort path the last call over this switch's scratch took for its batch of
-        npk packets (chunk + bucket sort batches only): "in_order" (no sort), "runs" (dense
-        ascending runs, no sort) or "sorted".  Synchronises the device (a diagnostic)."""
+        npk packets (batches past the one-workgroup small-batch paths): "in_order" (no sort),
+        "runs" (dense ascending runs, no sort) or "sorted" (the bucket sort or the LSD digit
+        passes).  Synchronises the device (a diagnostic)."""
         if self._scratch is None:
             raise ValueError("no batch has run on this switch")
         torch.cuda.synchronize(self._scratch.device)

@@ -350,12 +350,12 @@ int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* p
                                         size_t n, uint8_t* acks, size_t ack_stride,
                                         ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream);
 
-/* Diagnostic: which slot-sort path the last chunk + bucket sort over `scratch` took (a batch
- * of npkts packets, pools of < 2^18 slots, more than 768 packets; the small-batch paths and
- * the digit passes do not record one).  Synchronous (reads 12 bytes of the scratch). */
+/* Diagnostic: which slot-sort path the last call over `scratch` took (a batch of npkts
+ * packets, more than 768 of them; the one-workgroup small-batch paths do not record one; the
+ * LSD digit passes report INA_PATH_SORTED).  Synchronous (reads 12 bytes of the scratch). */
 #define INA_PATH_IN_ORDER 1   /* already in slot order: no sort */
 #define INA_PATH_RUNS 2       /* at most 64 runs of consecutive slots: a run table, no sort */
-#define INA_PATH_SORTED 3     /* the bucket sort */
+#define INA_PATH_SORTED 3     /* the bucket sort (or the LSD digit passes) */
 int ina_switch_batch_path(const void* scratch, size_t npkts, uint32_t num_slots, int* path);
 
 /* The switch over split rows (hdr: 16-byte header rows, pay: 4V-byte payload rows, see

@@ -200,6 +200,22 @@ def test_runs_tuning_off_takes_the_sort():
     check_batches(o, V, batches, "runs", use_desc=False, write_dropped=False)
 
 
+def test_digit_passes_report_sorted():
+    """Tuning key 12 = 3 (the LSD digit passes for every batch): a worker-major batch, which
+    the default would run from its run table, is sorted -- same results, and the diagnostic
+    says so."""
+    o = ops()
+    rng = np.random.default_rng(12)
+    V = 64
+    batches = [runs_batch(rng, V, worker_major(8, 300, acks=True), 8, o.nga_stride(V)) for _ in range(2)]
+    o.set_tuning(switch_sort=3)
+    try:
+        check_batches(o, V, batches, "sorted")
+    finally:
+        o.set_tuning(switch_sort=0)
+    check_batches(o, V, batches, "runs")
+
+
 @pytest.mark.parametrize("pre_all", [False, True])
 @pytest.mark.parametrize("case", ["runs", "in_order", "sorted", "acks_behind"])
 def test_first_pass_whole_or_split(case, pre_all):
