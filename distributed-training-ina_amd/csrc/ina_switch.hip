@@ -690,6 +690,69 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
     }
 }
 
+// The 2,048-bin chunk pass keeps two waves' per-digit counts in one LDS word (16 bits each:
+// a wave counts at most 64 x R <= 512 items of a digit, and the offsets below stay inside
+// the chunk, < 4,096): 64 KiB instead of 128 KiB of counts, so two blocks share a CU.
+// lds_count with the count shifted into the wave's half (the partner wave adds to the other
+// half of the same word, hence atomics)
+__device__ __forceinline__ void lds_count_half(uint32_t* h, uint32_t d, bool valid, int sh) {
+    const unsigned long long act = __ballot(valid);
+    if (!act) return;
+    const int first = __builtin_ctzll(act);
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, first);
+    const unsigned long long same = __ballot(valid && d == d0);
+    if (same == act) {
+        if ((int)(threadIdx.x & 63) == first) atomicAdd(&h[d0], (uint32_t)__builtin_popcountll(act) << sh);
+    } else if (valid) {
+        atomicAdd(&h[d], 1u << sh);
+    }
+}
+
+// rs_tile_scatter over the packed counts: each wave's offset of digit d inside the digit's
+// run in this chunk (16-bit halves), the run's first output position in gst[d]
+template <int R, int BINS>
+__device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], const uint32_t (&v)[R],
+                                                     size_t i0, size_t n, int shift, int bits,
+                                                     uint32_t (*base)[BINS], const uint32_t* gst,
+                                                     uint32_t* __restrict__ kout,
+                                                     uint32_t* __restrict__ vout) {
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const int sh = (wv & 1) * 16;
+    uint32_t* row = base[wv >> 1];
+    const uint32_t nb = 1u << bits;
+    constexpr int kDPT = (BINS + kBkThr - 1) / kBkThr;
+#pragma unroll
+    for (int j = 0; j < kDPT; ++j) {
+        const uint32_t d = threadIdx.x + (uint32_t)j * kBkThr;
+        if (d >= nb) continue;
+        uint32_t b = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kBkWaves / 2; ++w2) {
+            const uint32_t word = base[w2][d];
+            const uint32_t lo = word & 0xFFFFu, hi = word >> 16;
+            base[w2][d] = b | ((b + lo) << 16);
+            b += lo + hi;
+        }
+    }
+    __syncthreads();
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (i0 - (size_t)lane + (size_t)r * 64 >= n) break;    // wave-uniform
+        const bool valid = i0 + (size_t)r * 64 < n;
+        const uint32_t d = (k[r] >> shift) & (nb - 1);
+        const unsigned long long pm = lanes_with_digit(d, bits, valid);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(pm & below);
+        const uint32_t b0 = (row[d] >> sh) & 0xFFFFu;
+        if (valid) {
+            const uint32_t pos = gst[d] + b0 + rank;
+            kout[pos] = k[r];
+            vout[pos] = v[r];
+            if (rank == 0) atomicAdd(&row[d], (uint32_t)__builtin_popcountll(pm) << sh);
+        }
+    }
+}
+
 // kMode: 0 the chunk pass (keys, detection, digits, scatter); split in two (tuning key 19, the
 // default; always for keys of 19-22 bits, whose 2,048-bin chunk pass holds one block per CU)
 // so a structured batch never pays the digits: 1 = detection only (the arrival-order keys into
@@ -707,7 +770,9 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                                                         uint32_t* __restrict__ unsorted, uint32_t epoch,
                                                         uint32_t* __restrict__ brk_cnt,
                                                         uint2* __restrict__ brk_ent) {
-    __shared__ uint32_t base[kBkWaves][BINS];        // per-wave digit counts, then bases
+    // per-wave digit counts, then bases (2,048 bins: two waves' 16-bit halves per word)
+    constexpr bool kHalf = BINS > kBkThr;
+    __shared__ uint32_t base[kHalf ? kBkWaves / 2 : kBkWaves][BINS];
     __shared__ uint32_t gst[BINS];                    // the chunk's run starts (output positions)
     __shared__ uint32_t wtot[kBkWaves];
     __shared__ uint32_t wbrk[kBkWaves];               // per-wave break counts
@@ -736,7 +801,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     }
     const uint32_t nb = 1u << hbits;
     if constexpr (kMode != 1)
-        for (uint32_t d = lane; d < nb; d += 64) base[wv][d] = 0;
+        for (uint32_t d = lane; d < nb; d += 64) base[kHalf ? wv >> 1 : wv][d] = 0;
     const size_t i0 = c * (size_t)(kBkThr * R) + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t idx[R], sid[R], ack[R], k[R], v[R];
     load_key_fields<R, kDesc>(pkts, desc, npk, stride, i0, idx, sid, ack);
@@ -760,7 +825,10 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
         v[r] = (uint32_t)p;
         if (kMode != 2 && p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
-        if constexpr (kMode != 1) lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
+        if constexpr (kMode != 1) {
+            if constexpr (kHalf) lds_count_half(base[wv >> 1], (key >> lb) & (nb - 1), p < npk, (wv & 1) * 16);
+            else lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
+        }
         if constexpr (kMode == 1)
             if (p < npk) kout[p] = k[r];              // arrival-order keys (the in-order run's)
         // predecessor: lane l-1 of this round (DPP wave_shr:1), lane 0 the previous round's
@@ -814,8 +882,16 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
         tc[j] = 0;
         if (d < nb) {
+            if constexpr (kHalf) {
 #pragma unroll
-            for (int w = 0; w < kBkWaves; ++w) tc[j] += base[w][d];
+                for (int w2 = 0; w2 < kBkWaves / 2; ++w2) {
+                    const uint32_t word = base[w2][d];
+                    tc[j] += (word & 0xFFFFu) + (word >> 16);
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < kBkWaves; ++w) tc[j] += base[w][d];
+            }
         }
     }
     block_digit_scan_n<DPT>(tc, ex, wtot, 0u);
@@ -829,7 +905,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         }
     }
     __syncthreads();
-    rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
+    if constexpr (kHalf) rs_tile_scatter_half<R, BINS>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
+    else rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
 }
 
 #ifndef INA_BK_TIMING
