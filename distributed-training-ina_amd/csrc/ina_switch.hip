@@ -690,9 +690,10 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
     }
 }
 
-// The 2,048-bin chunk pass keeps two waves' per-digit counts in one LDS word (16 bits each:
-// a wave counts at most 64 x R <= 512 items of a digit, and the offsets below stay inside
-// the chunk, < 4,096): 64 KiB instead of 128 KiB of counts, so two blocks share a CU.
+// The 2,048-bin chunk pass and the 1,024- / 2,048-bin bucket pass keep two waves' per-digit
+// counts in one LDS word (16 bits each: a wave counts at most 64 x 8 items of a digit, and
+// the offsets below stay inside one chunk or tile, <= 8,192): half the count array, so two
+// chunk blocks or three bucket blocks (1,024 bins) share a CU instead of one.
 // lds_count with the count shifted into the wave's half (the partner wave adds to the other
 // half of the same word, hence atomics)
 __device__ __forceinline__ void lds_count_half(uint32_t* h, uint32_t d, bool valid, int sh) {
@@ -715,7 +716,7 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
                                                      size_t i0, size_t n, int shift, int bits,
                                                      uint32_t (*base)[BINS], const uint32_t* gst,
                                                      uint32_t* __restrict__ kout,
-                                                     uint32_t* __restrict__ vout) {
+                                                     uint32_t* __restrict__ vout, int rw = R) {
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const int sh = (wv & 1) * 16;
     uint32_t* row = base[wv >> 1];
@@ -738,7 +739,7 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
     const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (i0 - (size_t)lane + (size_t)r * 64 >= n) break;    // wave-uniform
+        if (r >= rw || i0 - (size_t)lane + (size_t)r * 64 >= n) break;   // wave-uniform
         const bool valid = i0 + (size_t)r * 64 < n;
         const uint32_t d = (k[r] >> shift) & (nb - 1);
         const unsigned long long pm = lanes_with_digit(d, bits, valid);
@@ -956,7 +957,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
                                                          const uint2* __restrict__ brk_ent, uint32_t npk,
                                                          int pre) {
     __shared__ uint32_t s_dst[kBkMaxChunks + 1], s_src[kBkMaxChunks];
-    __shared__ uint32_t base[kBkWaves][BINS];
+    constexpr bool kHalf = BINS >= 1024;              // two waves' 16-bit counts per word
+    __shared__ uint32_t base[kHalf ? kBkWaves / 2 : kBkWaves][BINS];
     __shared__ uint32_t gst[BINS];                    // bucket digit counts, then output positions
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
@@ -1105,11 +1107,16 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
             k[r] = ok ? kin[src[r]] : 0u;
             v[r] = ok ? vin[src[r]] : 0u;
         }
-        for (uint32_t dd = lane; dd < nb; dd += 64) base[wv][dd] = 0;
+        for (uint32_t dd = lane; dd < nb; dd += 64) base[kHalf ? wv >> 1 : wv][dd] = 0;
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if (r < rw) lds_count(base[wv], k[r] & (nb - 1), i0 + (uint32_t)r * 64u < t_end);
+            if (r < rw) {
+                if constexpr (kHalf)
+                    lds_count_half(base[wv >> 1], k[r] & (nb - 1), i0 + (uint32_t)r * 64u < t_end, (wv & 1) * 16);
+                else
+                    lds_count(base[wv], k[r] & (nb - 1), i0 + (uint32_t)r * 64u < t_end);
+            }
         __syncthreads();
         BK_STAMP(2);
         uint32_t tc[DPT];                             // this tile's counts of the thread's digits
@@ -1118,8 +1125,16 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
             const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
             tc[j] = 0;
             if (d < nb) {
+                if constexpr (kHalf) {
 #pragma unroll
-                for (int w = 0; w < kBkWaves; ++w) tc[j] += base[w][d];
+                    for (int w2 = 0; w2 < kBkWaves / 2; ++w2) {
+                        const uint32_t word = base[w2][d];
+                        tc[j] += (word & 0xFFFFu) + (word >> 16);
+                    }
+                } else {
+#pragma unroll
+                    for (int w = 0; w < kBkWaves; ++w) tc[j] += base[w][d];
+                }
             }
         }
         if (ntile == 1) {                             // one tile: positions from its own counts
@@ -1136,7 +1151,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restr
         // (staging a one-tile bucket's output in LDS to leave as one contiguous run measured
         // no faster: 244.5 -> 244.1 us worker-major, 228.3 -> 229.9 round-robin,
         // profiles/r03/lab/bucket_stage_lab.log)
-        rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
+        if constexpr (kHalf) rs_tile_scatter_half<R, BINS>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
+        else rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
         __syncthreads();
         BK_STAMP(4);
 #pragma unroll
@@ -2753,7 +2769,10 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const int tile = g_bucket_tile.load();
         const bool big = tile == kLcRoundsBig || (tile == 0 && npk > (size_t)gb * kBigTileAvg);
         if (do_sort)
-            hipLaunchKernelGGL((sp.wide ? (big ? &k_sort_buckets<kLcRoundsBig, kBinsBig> : &k_sort_buckets<kLcRounds, kBinsBig>)
+            // the bucket pass's bins follow the low digit: 1,024 for keys of 19-21 bits (three
+            // blocks per CU with the packed counts), 2,048 for 22 bits
+            hipLaunchKernelGGL((sp.wide ? (lb <= 10 ? (big ? &k_sort_buckets<kLcRoundsBig, 1024> : &k_sort_buckets<kLcRounds, 1024>)
+                                                    : (big ? &k_sort_buckets<kLcRoundsBig, kBinsBig> : &k_sort_buckets<kLcRounds, kBinsBig>))
                                         : (big ? &k_sort_buckets<kLcRoundsBig, kRsBins> : &k_sort_buckets<kLcRounds, kRsBins>)),
                                dim3(gb),
                                dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
