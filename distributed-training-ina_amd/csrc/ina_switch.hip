@@ -1897,7 +1897,10 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
         __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
 }
 
-constexpr int kSlotRunsInFlight = 4;
+#ifndef INA_SWITCH_SLOT_INFLIGHT
+#define INA_SWITCH_SLOT_INFLIGHT 4
+#endif
+constexpr int kSlotRunsInFlight = INA_SWITCH_SLOT_INFLIGHT;   // packets' loads in flight per lane group
 // one packet of a lane group's slot (group-uniform: every lane of the group runs it with the
 // same header): ack / collision / count / Processor add, the PS step, the rewritten packet
 // and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
