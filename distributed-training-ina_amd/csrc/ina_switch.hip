@@ -555,15 +555,10 @@ constexpr int kBkMaxChunks = 2048;                  // B's LDS rows: up to 2048 
 // so the launch picks R = 8 only when the average bucket exceeds 7/8 of the smaller tile
 constexpr int kLcRounds = 4;
 constexpr int kLcRoundsBig = 8;
-// 16,384-item tiles for the 1,024-bin (wide-key) bucket pass when the average bucket exceeds
-// 7/8 of the 8,192-item tile (NGA-32 at C3 size: 12,800 per bucket): a bucket in one tile
-// skips the counting sweep (a binary search + a dependent load per item) before the tiles
-constexpr int kLcRoundsHuge = 16;
-constexpr size_t kHugeTileAvg = (size_t)16 * 64 * kLcRoundsBig * 7 / 8;    // 7,168 items
 constexpr size_t kBigTileAvg = (size_t)kBkWaves * 64 * kLcRounds * 7 / 8;   // 3,584 items
 static std::atomic<int> g_bucket_tile{0};   // ina_set_tuning key 17: 0 auto, 4 or 8 rounds
 int set_bucket_tile(int v) {
-    if (v != 0 && v != kLcRounds && v != kLcRoundsBig && v != kLcRoundsHuge) return INA_EINVAL;
+    if (v != 0 && v != kLcRounds && v != kLcRoundsBig) return INA_EINVAL;
     g_bucket_tile = v;
     return INA_OK;
 }
@@ -2775,14 +2770,11 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // so at 2^17 slots 257 blocks (one per CU, one generation) instead of 512
         const unsigned gb = std::min<unsigned>(1u << sp.hbits, (st->num_slots >> lb) + 1u);
         const int tile = g_bucket_tile.load();
-        const bool huge = sp.wide && lb <= 10 &&
-                          (tile == kLcRoundsHuge || (tile == 0 && npk > (size_t)gb * kHugeTileAvg));
-        const bool big = tile == kLcRoundsBig || tile == kLcRoundsHuge || (tile == 0 && npk > (size_t)gb * kBigTileAvg);
+        const bool big = tile == kLcRoundsBig || (tile == 0 && npk > (size_t)gb * kBigTileAvg);
         if (do_sort)
             // the bucket pass's bins follow the low digit: 1,024 for keys of 19-21 bits (three
             // blocks per CU with the packed counts), 2,048 for 22 bits
-            hipLaunchKernelGGL((sp.wide ? (lb <= 10 ? (huge ? &k_sort_buckets<kLcRoundsHuge, 1024>
-                                                           : big ? &k_sort_buckets<kLcRoundsBig, 1024> : &k_sort_buckets<kLcRounds, 1024>)
+            hipLaunchKernelGGL((sp.wide ? (lb <= 10 ? (big ? &k_sort_buckets<kLcRoundsBig, 1024> : &k_sort_buckets<kLcRounds, 1024>)
                                                     : (big ? &k_sort_buckets<kLcRoundsBig, kBinsBig> : &k_sort_buckets<kLcRounds, kBinsBig>))
                                         : (big ? &k_sort_buckets<kLcRoundsBig, kRsBins> : &k_sort_buckets<kLcRounds, kRsBins>)),
                                dim3(gb),

@@ -1008,9 +1008,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     reach it, so it is capped by switch_small_sort's threshold; host_zero_copy lets
     sum_reduce_host reduce pinned, device-mapped host buffers in place over PCIe (True,
     the default) instead of through the chunked copy pipeline; switch_bucket_tile the slot
-    sort's bucket tile in 64-item rounds per wave (0 = auto: 16 for 1,024-bin buckets
-    averaging over 7,168 packets, 8 when the average bucket exceeds 3,584, else 4; or 4, 8,
-    16); switch_runs lets batches of at most 64 runs of
+    sort's bucket tile in 64-item rounds per wave (0 = auto: 8 when the average bucket
+    exceeds 3,584 packets, else 4; or 4, 8); switch_runs lets batches of at most 64 runs of
     consecutive slots (worker-major arrival, PS acks in front) skip the slot sort (True, the
     default; False always sorts); switch_pre_all splits the sort's first pass into detection,
     decision and digits for every key width (True, the default; False: keys of 19-22 bits only);

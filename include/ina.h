@@ -76,9 +76,8 @@ const char* ina_last_error_string(void);
  * workgroup (0 = off, <= 2048; it applies only to batches that also take key 9's
  * one-workgroup path, so it is capped by key 9's threshold), 16 host reduce on pinned
  * device-mapped buffers in place over PCIe (1, default) or through the chunked copy
- * pipeline (0), 17 the slot sort's bucket tile in 64-item rounds per wave (0 auto: 16 for
- * 1,024-bin buckets averaging over 7,168 packets, 8 when the average bucket exceeds 3,584
- * packets, else 4; or 4, 8, 16), 18 switch batches made of at
+ * pipeline (0), 17 the slot sort's bucket tile in 64-item rounds per wave (0 auto: 8 when
+ * the average bucket exceeds 3,584 packets, else 4; or 4, 8), 18 switch batches made of at
  * most 64 runs of consecutive slots (worker-major arrival, PS acks in front) skip the slot
  * sort and run from a table of the runs (1, default; 0 = always sort), 19 the slot sort's
  * first pass split into detection + decision + digits for every key width (1, default:
