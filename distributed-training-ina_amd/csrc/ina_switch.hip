@@ -1892,10 +1892,14 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
         __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
 }
 
+// packets' loads in flight per lane group: 2 (the VGPRs buy occupancy); interleaved A/B at
+// NGA-32 C3 size against 4: worker-major split 274.6 -> 260.7 us, round-robin packed 390.8 ->
+// 374.7, shuffled 757.9 -> 734.8 / split 660.2 -> 646.0, the rest equal; 8 spills (2-3x
+// slower).  profiles/r04/lab/slot_inflight_ab_v32_*.log
 #ifndef INA_SWITCH_SLOT_INFLIGHT
-#define INA_SWITCH_SLOT_INFLIGHT 4
+#define INA_SWITCH_SLOT_INFLIGHT 2
 #endif
-constexpr int kSlotRunsInFlight = INA_SWITCH_SLOT_INFLIGHT;   // packets' loads in flight per lane group
+constexpr int kSlotRunsInFlight = INA_SWITCH_SLOT_INFLIGHT;
 // one packet of a lane group's slot (group-uniform: every lane of the group runs it with the
 // same header): ack / collision / count / Processor add, the PS step, the rewritten packet
 // and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
