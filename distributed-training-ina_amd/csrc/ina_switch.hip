@@ -1892,14 +1892,20 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
         __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
 }
 
-// packets' loads in flight per lane group: 2 (the VGPRs buy occupancy); interleaved A/B at
-// NGA-32 C3 size against 4: worker-major split 274.6 -> 260.7 us, round-robin packed 390.8 ->
-// 374.7, shuffled 757.9 -> 734.8 / split 660.2 -> 646.0, the rest equal; 8 spills (2-3x
-// slower).  profiles/r04/lab/slot_inflight_ab_v32_*.log
+// packets' loads in flight per lane group (the VGPRs buy occupancy): 2 for packed rows, 1 for
+// split rows.  Interleaved A/Bs at NGA-32 C3 size (profiles/r04/lab/slot_inflight_ab_v32_*.log):
+// 2 against 4 -- worker-major split 274.6 -> 260.7 us, round-robin packed 390.8 -> 374.7,
+// shuffled 757.9 -> 734.8, the rest equal (8 spills: 2-3x slower); 1 against 2 -- split rows
+// worker-major 258.6 -> 220.8, round-robin 285.9 -> 252.1, shuffled 646 -> 642, packed rows
+// 4-7 % slower (3: no better than 2)
 #ifndef INA_SWITCH_SLOT_INFLIGHT
 #define INA_SWITCH_SLOT_INFLIGHT 2
 #endif
-constexpr int kSlotRunsInFlight = INA_SWITCH_SLOT_INFLIGHT;
+#ifndef INA_SWITCH_SLOT_INFLIGHT_SPLIT
+#define INA_SWITCH_SLOT_INFLIGHT_SPLIT 1
+#endif
+template <bool kSplit>
+constexpr int kSlotInFlight = kSplit ? INA_SWITCH_SLOT_INFLIGHT_SPLIT : INA_SWITCH_SLOT_INFLIGHT;
 // one packet of a lane group's slot (group-uniform: every lane of the group runs it with the
 // same header): ack / collision / count / Processor add, the PS step, the rewritten packet
 // and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
@@ -2035,7 +2041,7 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                                                     const uint32_t* __restrict__ ids,
                                                     uint8_t* __restrict__ actions, uint32_t win, uint32_t kmask,
                                                     const PsFuse& ps, size_t wave, size_t nwaves) {
-    constexpr int kP = kSlotRunsInFlight;
+    constexpr int kP = kSlotInFlight<kSplit>;
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, l = lane & 7;
     const int V = st.V, L = V >> 2;
@@ -2252,7 +2258,7 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                                                   uint32_t R, uint32_t rpos, uint32_t rlen, uint32_t rslot,
                                                   bool rack, uint32_t lo, uint32_t hi, size_t wave,
                                                   size_t nwaves) {
-    constexpr int kP = kSlotRunsInFlight;
+    constexpr int kP = kSlotInFlight<kSplit>;
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, l = lane & 7;
     const int V = st.V, L = V >> 2;
