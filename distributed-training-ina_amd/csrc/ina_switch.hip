@@ -2269,6 +2269,15 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
     const size_t s_begin = (size_t)lo + wave * per;
     const size_t s_end = s_begin + per < (size_t)hi ? s_begin + per : (size_t)hi;
     const uint32_t rack_u = rack ? 1u : 0u;
+    // packed rows: run r's rows for the wave's 8 slots are neighbours, 8 x (L + 1) chunks of 16
+    // bytes; lane c loads chunk c (and chunk 64 + c) of that stretch, so each wave instruction
+    // reads contiguous lines, and the chunks reach their group's lanes through LDS (each
+    // group reading its own row straight from memory issued ~24 line requests per 8 rows
+    // instead of ~10)
+    const int cpr = L + 1;                            // chunks per packed row
+    const int gg0 = lane / cpr, cc0 = lane - gg0 * cpr;
+    const int gg1 = (64 + lane) / cpr, cc1 = 64 + lane - gg1 * cpr;
+    const bool has1 = 64 + lane < 8 * cpr;
     for (size_t s8 = s_begin; s8 < s_end; s8 += 8) {
         const uint32_t slot = (uint32_t)(s8 + (size_t)g);
         const bool sv = s8 + (size_t)g < s_end;
@@ -2295,17 +2304,44 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                 const uint32_t off = slot - rs;
                 in[j] = sv && off < rl;
                 pid[j] = rp + off;
-                if (in[j] && !ackr[j]) {                  // a run of PS acks needs no read
-                    if constexpr (kSplit) {
+                if constexpr (kSplit) {
+                    if (in[j] && !ackr[j]) {              // a run of PS acks needs no read
                         m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
                                      (vl ? l : 0));
                         h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
-                    } else {
-                        const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
-                        m[j] = sw_ld(pk + (vl ? l + 1 : 1));
-                        h[j] = *pk;
+                    }
+                } else {
+                    // the stretch of run r holding group gg's row: rows base + gg
+                    const uint32_t base_row = rp + (uint32_t)s8 - rs;
+                    const uint32_t sg0 = (uint32_t)s8 + (uint32_t)gg0, sg1 = (uint32_t)s8 + (uint32_t)gg1;
+                    const bool ok0 = !ackr[j] && gg0 < 8 && sg0 < s_end && sg0 - rs < rl;
+                    const bool ok1 = !ackr[j] && has1 && sg1 < s_end && sg1 - rs < rl;
+                    if (ok0)
+                        m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)(base_row + (uint32_t)gg0) * stride) + cc0);
+                    if (ok1)
+                        h[j] = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)(base_row + (uint32_t)gg1) * stride) + cc1);
+                }
+            }
+            if constexpr (!kSplit) {
+                // the stretches to LDS, then each group's chunks back: chunk l + 1 of its row
+                // (value lanes) and chunk 0 (the header chunk) for every lane of the group
+                __shared__ u32x4s s_stage[kSwBlock / 64][kP][64 + 8];
+                const int wb = (int)(threadIdx.x >> 6);
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int j = 0; j < kP; ++j) {
+                    s_stage[wb][j][lane] = m[j];
+                    if (has1) s_stage[wb][j][64 + lane] = h[j];
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int j = 0; j < kP; ++j) {
+                    if (in[j] && !ackr[j]) {
+                        m[j] = s_stage[wb][j][g * cpr + (vl ? l + 1 : 1)];
+                        h[j] = s_stage[wb][j][g * cpr];
                     }
                 }
+                __builtin_amdgcn_wave_barrier();
             }
 #pragma unroll
             for (int j = 0; j < kP; ++j) {
