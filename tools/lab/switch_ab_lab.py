@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Switch A/B lab (experiment only): the in-tree libina.so against another build of it
-(LIB_B, default tools/lab/libina_r04f.so: the round-4 evidence session's library) on config 3
+(LIB_B: e.g. make -C distributed-training-ina_amd/csrc OUT=../../tools/lab/libina_b.so
+BUILD=build_b EXTRA=-D...) on config 3
 as NGA-V packets (V env, 256 or 32; 8 workers; 2^17 / 2^20-slot pool; descriptors) in
 worker-major, round-robin and shuffled arrival, packed rows and split rows.  Per order: the
 two libraries' actions, rewritten rows and registers compared byte for byte on fresh
@@ -18,7 +19,9 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
 from ina_amd import _lib, ops  # noqa: E402
 
-libs = {"A": _lib.load(), "B": _lib.open_library(os.environ.get("LIB_B", os.path.join(HERE, "libina_r04f.so")))}
+if "LIB_B" not in os.environ:
+    raise SystemExit("set LIB_B to the library build to compare against")
+libs = {"A": _lib.load(), "B": _lib.open_library(os.environ["LIB_B"])}
 dev = torch.device("cuda")
 V = int(os.environ.get("V", 256))
 W, n = 8, 26_214_400
@@ -63,7 +66,7 @@ def timed(fn):
     return a.elapsed_time(b) * 1e3 / K
 
 
-out = {"V": V, "lib_B": os.path.basename(os.environ.get("LIB_B", "libina_r04f.so"))}
+out = {"V": V, "lib_B": os.path.basename(os.environ["LIB_B"])}
 for order, perm in perms.items():
     stream, desc = (base, base_desc) if perm is None else (base[perm], base_desc[perm])
     hdr, pay = split_rows(stream)
