@@ -690,6 +690,9 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
     }
 }
 
+#ifndef INA_SORT_STAGE
+#define INA_SORT_STAGE 0
+#endif
 // The 2,048-bin chunk pass and the 1,024- / 2,048-bin bucket pass keep two waves' per-digit
 // counts in one LDS word (16 bits each: a wave counts at most 64 x 8 items of a digit, and
 // the offsets below stay inside one chunk or tile, <= 8,192): half the count array, so two
@@ -711,12 +714,14 @@ __device__ __forceinline__ void lds_count_half(uint32_t* h, uint32_t d, bool val
 
 // rs_tile_scatter over the packed counts: each wave's offset of digit d inside the digit's
 // run in this chunk (16-bit halves), the run's first output position in gst[d]
-template <int R, int BINS>
+template <int R, int BINS, bool kStage = false>
 __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], const uint32_t (&v)[R],
                                                      size_t i0, size_t n, int shift, int bits,
                                                      uint32_t (*base)[BINS], const uint32_t* gst,
                                                      uint32_t* __restrict__ kout,
-                                                     uint32_t* __restrict__ vout, int rw = R) {
+                                                     uint32_t* __restrict__ vout, int rw = R,
+                                                     uint32_t* sk = nullptr, uint32_t* sv = nullptr,
+                                                     uint32_t sbase = 0u) {
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const int sh = (wv & 1) * 16;
     uint32_t* row = base[wv >> 1];
@@ -747,8 +752,13 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
         const uint32_t b0 = (row[d] >> sh) & 0xFFFFu;
         if (valid) {
             const uint32_t pos = gst[d] + b0 + rank;
-            kout[pos] = k[r];
-            vout[pos] = v[r];
+            if constexpr (kStage) {                   // the chunk's output staged in LDS
+                sk[pos - sbase] = k[r];
+                sv[pos - sbase] = v[r];
+            } else {
+                kout[pos] = k[r];
+                vout[pos] = v[r];
+            }
             if (rank == 0) atomicAdd(&row[d], (uint32_t)__builtin_popcountll(pm) << sh);
         }
     }
@@ -906,6 +916,22 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         }
     }
     __syncthreads();
+#if INA_SORT_STAGE
+    if constexpr (kHalf) {
+        // the chunk's sorted output lands in LDS, then leaves as one contiguous stretch (the
+        // 2,048-bin scatter writes runs of ~2 items: scattered 4-byte stores)
+        __shared__ uint32_t s_k[kBkThr * R], s_v[kBkThr * R];
+        const uint32_t cb = (uint32_t)(c * (size_t)(kBkThr * R));
+        rs_tile_scatter_half<R, BINS, true>(k, v, i0, npk, lb, hbits, base, gst, kout, vout, R, s_k, s_v, cb);
+        __syncthreads();
+        const uint32_t nc = (uint32_t)min((size_t)(kBkThr * R), npk - (size_t)cb);
+        for (uint32_t i = threadIdx.x; i < nc; i += kBkThr) {
+            kout[cb + i] = s_k[i];
+            vout[cb + i] = s_v[i];
+        }
+        return;
+    }
+#endif
     if constexpr (kHalf) rs_tile_scatter_half<R, BINS>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
     else rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, npk, lb, hbits, base, gst, kout, vout);
 }
