@@ -690,8 +690,12 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
     }
 }
 
+// the 2,048-bin chunk pass stages its sorted chunk in LDS and writes it out contiguously
+// (interleaved A/B at NGA-32 C3 size, shuffled: 732.8 -> 709.2 us packed, 639.7 -> 615.9 us
+// split, bytes equal; profiles/r04/lab/sort_stage_ab_v32.log).  The LDS (104 KiB) costs
+// the second block per CU the packed counts bought; the contiguous stores win.
 #ifndef INA_SORT_STAGE
-#define INA_SORT_STAGE 0
+#define INA_SORT_STAGE 1
 #endif
 // The 2,048-bin chunk pass and the 1,024- / 2,048-bin bucket pass keep two waves' per-digit
 // counts in one LDS word (16 bits each: a wave counts at most 64 x 8 items of a digit, and
