@@ -90,6 +90,14 @@ constexpr int kRsRounds = INA_RS_ROUNDS;
 #ifndef INA_RS_MID_ITEMS
 #define INA_RS_MID_ITEMS 524288
 #endif
+// chunk + bucket sort of more than 2 Mi packets: 8,192-packet chunks (32 rounds), so a
+// bucket's run in each chunk is twice as long and B gathers half as many of them
+#ifndef INA_RS_ROUNDS_BIG
+#define INA_RS_ROUNDS_BIG 32
+#endif
+#ifndef INA_RS_BIG_ITEMS
+#define INA_RS_BIG_ITEMS 2097152
+#endif
 constexpr int kRsBlock = 64 * INA_RS_WAVES;
 constexpr int kRsWaves = kRsBlock / 64;
 static_assert(kRsBins % kRsBlock == 0, "digits split evenly over the block's threads");
@@ -2586,6 +2594,15 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     p.rounds = npk <= (size_t)INA_RS_SMALL_ITEMS ? INA_RS_ROUNDS_SMALL
              : npk <= (size_t)INA_RS_MID_ITEMS   ? INA_RS_ROUNDS_MID
                                                  : kRsRounds;
+    // more than 2 Mi packets through the chunk + bucket sort: 8,192-packet chunks.  NGA-32
+    // at C3 size (6,553,600 packets, 2^20 slots: 1,025 buckets of 6,400, i.e. runs of 4
+    // packets per 4,096-packet chunk) shuffled 709 -> 676 us packed, 616 -> 583 us split;
+    // structured arrival unchanged; at 819,200 NGA-256 packets (100 chunks) +2 %, so not
+    // there (interleaved A/B, bytes equal, profiles/r04/lab/chunk_rounds32_ab_v*.log).  The
+    // digit passes keep 4,096 (they never see this tier: bucket_ok, mode 0, <= 2,048 chunks)
+    if (npk > (size_t)INA_RS_BIG_ITEMS && p.bucket_ok && g_sort_mode.load() == 0 &&
+        npk <= (size_t)kBkMaxChunks * kRsWaves * 64 * INA_RS_ROUNDS_BIG)
+        p.rounds = INA_RS_ROUNDS_BIG;
     if (const int r = g_os_rounds.load()) p.rounds = r;   // ina_set_tuning key 13 (lab sweeps)
     const size_t chunk = (size_t)kRsWaves * 64 * (size_t)p.rounds;
     p.nch = (npk + chunk - 1) / chunk;
@@ -2735,9 +2752,9 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     const SortPlan sp = sort_plan(npk, st->num_slots);
     const SortAux ax = sort_aux(base + 4 * arr, npk, st->num_slots);
     // sort chunk geometry (sort_plan): one instantiation per rounds-per-wave choice
-    constexpr int kR0 = INA_RS_ROUNDS_SMALL, kR1 = INA_RS_ROUNDS_MID, kR2 = kRsRounds;
-    static_assert(kR0 % 4 == 0 && kR1 % 4 == 0 && kR2 % 4 == 0, "chunk sort: 16 waves x rounds/4");
-    const int ri = sp.rounds == kR0 ? 0 : sp.rounds == kR1 ? 1 : 2;
+    constexpr int kR0 = INA_RS_ROUNDS_SMALL, kR1 = INA_RS_ROUNDS_MID, kR2 = kRsRounds, kR3 = INA_RS_ROUNDS_BIG;
+    static_assert(kR0 % 4 == 0 && kR1 % 4 == 0 && kR2 % 4 == 0 && kR3 % 4 == 0, "chunk sort: 16 waves x rounds/4");
+    const int ri = sp.rounds == kR0 ? 0 : sp.rounds == kR1 ? 1 : sp.rounds == kR2 ? 2 : 3;
     const unsigned gc = (unsigned)sp.nch;
     const uint32_t nb = 1u << sp.bits;
 
@@ -2806,7 +2823,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kc, vc, ah, \
                                ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
-            if (ri == 2) INA_A_DETECT(kR2 / 4);
+            if (ri == 3) INA_A_DETECT(kR3 / 4);
+            else if (ri == 2) INA_A_DETECT(kR2 / 4);
             else if (ri == 1) INA_A_DETECT(kR1 / 4);
             else INA_A_DETECT(kR0 / 4);
 #undef INA_A_DETECT
@@ -2816,7 +2834,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
                                ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
-            if (ri == 2) INA_A_SORT(kR2 / 4);
+            if (ri == 3) INA_A_SORT(kR3 / 4);
+            else if (ri == 2) INA_A_SORT(kR2 / 4);
             else if (ri == 1) INA_A_SORT(kR1 / 4);
             else INA_A_SORT(kR0 / 4);
 #undef INA_A_SORT
@@ -2827,7 +2846,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                            dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                            st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah,  \
                            ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
-        if (ri == 2) INA_A_LAUNCH(kR2 / 4);
+        if (ri == 3) INA_A_LAUNCH(kR3 / 4);
+        else if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
         else INA_A_LAUNCH(kR0 / 4);
 #undef INA_A_LAUNCH
@@ -2866,6 +2886,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     } else {
         // LSD digit passes (keys of three digits, batches beyond B's rows, or key 12 = 3):
         // keys + pass-0 histogram, then per pass a column scan and a scatter
+        if (ri == 3) return set_error(INA_EINVAL, "8,192-packet chunks are the bucket sort's only%s", "");
         auto* k_keys = desc ? (ri == 0 ? &k_switch_keys<kR0, true> : ri == 1 ? &k_switch_keys<kR1, true>
                                                                     : &k_switch_keys<kR2, true>)
                             : (ri == 0 ? &k_switch_keys<kR0, false> : ri == 1 ? &k_switch_keys<kR1, false>

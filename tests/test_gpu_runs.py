@@ -483,6 +483,66 @@ def test_nga32_config3_full_size(order):
     assert int(sw.count.max()) == 0
 
 
+@pytest.mark.parametrize("num_slots", [1 << 16, 1 << 20])
+@pytest.mark.parametrize("order", ["shuffled", "worker_major", "round_robin"])
+def test_big_batch_chunks_vs_digit_passes(order, num_slots):
+    """More than 2 Mi packets through the chunk + bucket sort take 8,192-packet chunks
+    (INA_RS_BIG_ITEMS).  Two batches of 8 x 300,000 NGA-4 packets (1 % frag-id collisions;
+    at 2^16 slots every worker wraps the pool four times), state carried: actions, rewritten
+    rows and registers byte for byte against the same batches through the LSD digit passes
+    (tuning key 12 = 3, 4,096-packet chunks), in packed and in split rows."""
+    o = ops()
+    W, per, V = 8, 300_000, 4
+    g = torch.Generator(device=DEV).manual_seed(num_slots % 97 + len(order))
+    batches = []
+    for bi in range(2):
+        rows, descs = [], []
+        for w in range(W):
+            b = torch.randint(-(1 << 31), (1 << 31) - 1, (per * V,), dtype=torch.int32, device=DEV, generator=g)
+            p, d = o.pack_nga(b, V, w + 1, W, 1, 1 + bi * per, num_slots=num_slots, desc=True)
+            rows.append(p)
+            descs.append(d)
+        st, de = torch.cat(rows), torch.cat(descs)
+        hit = torch.rand(st.shape[0], device=DEV, generator=g) < 0.01
+        st[hit, 14] ^= 1                                   # frag id's low byte: not in the descriptor
+        if order == "shuffled":
+            perm = torch.randperm(st.shape[0], device=DEV, generator=g)
+        elif order == "round_robin":
+            perm = torch.arange(st.shape[0], device=DEV).view(W, per).t().reshape(-1)
+        else:
+            perm = None
+        if perm is not None:
+            st, de = st[perm], de[perm]
+        batches.append((st, de))
+    out = {}
+    for mode in (0, 3):
+        o.set_tuning(switch_sort=mode)
+        try:
+            sw, sws = (o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV) for _ in range(2))
+            res, paths = [], []
+            for st, de in batches:
+                pk = st.clone()
+                h = torch.zeros((st.shape[0], 16), dtype=torch.uint8, device=DEV)
+                h[:, :15] = st[:, :15]
+                pay = st[:, 15:15 + 4 * V].contiguous()
+                res += [sw.process(pk, desc=de), pk]
+                paths.append(sw.batch_path(st.shape[0]))
+                res += [sws.process_split(h, pay, desc=de), h, pay]
+            res += [sw.regs.clone(), sw.count.clone(), sw.frag.clone(), sws.regs.clone()]
+            out[mode] = ([x.cpu() for x in res], paths)
+            del sw, sws, res
+        finally:
+            o.set_tuning(switch_sort=0)
+    for x, y in zip(out[0][0], out[3][0]):
+        assert torch.equal(x, y)
+    assert out[3][1] == ["sorted", "sorted"]
+    if num_slots == 1 << 20:
+        want = {"shuffled": "sorted", "worker_major": "runs", "round_robin": "in_order"}[order]
+        assert out[0][1] == [want, want]
+    n_fwd = int((out[0][0][0] == orc.ACT_FWD_AGG).sum())
+    assert n_fwd > 0
+
+
 def test_numpy_integer_seq0_broadcasts():
     """seq0 given as a numpy integer scalar is one seq0 for every worker (numbers.Integral),
     as a Python int is -- make_descriptors and the one-launch worker pack alike."""
