@@ -953,7 +953,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
 #endif
 #if INA_BK_TIMING
 // lab builds only: per-block wall-clock stamps of k_sort_buckets' phases (tools/lab)
-__device__ unsigned long long g_bk_t[kRsBins][6];
+__device__ unsigned long long g_bk_t[kBkMaxChunks][6];   // one row per bucket (<= 2,048)
 #define BK_STAMP(q) do { if (threadIdx.x == 0) g_bk_t[blockIdx.x][q] = wall_clock64(); } while (0)
 #else
 #define BK_STAMP(q) do { } while (0)
@@ -981,8 +981,11 @@ __device__ __forceinline__ void bucket_src(const uint32_t* s_dst, const uint32_t
     for (int r = 0; r < R; ++r) src[r] = s_src[lo[r]] + (i[r] - s_dst[lo[r]]);
 }
 
+// two blocks per CU (8 waves per SIMD) where the LDS allows it (<= 1,024 bins, 53 KiB): the
+// bound caps the scalar registers too -- at 106 SGPRs (R = 8) a SIMD held 7 waves, so one
+// 16-wave block per CU ran (most blocks in flight at once: 256, tools/lab/bucket_phase_lab.py)
 template <int R, int BINS>
-__global__ __launch_bounds__(kBkThr) void k_sort_buckets(const uint32_t* __restrict__ kin,
+__global__ __launch_bounds__(kBkThr, BINS <= 1024 ? 2 * kBkThr / 256 : kBkThr / 256) void k_sort_buckets(const uint32_t* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin,
                                                          uint32_t* __restrict__ kout,
                                                          uint32_t* __restrict__ vout,
