@@ -702,6 +702,12 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
 // (interleaved A/B at NGA-32 C3 size, shuffled: 732.8 -> 709.2 us packed, 639.7 -> 615.9 us
 // split, bytes equal; profiles/r04/lab/sort_stage_ab_v32.log).  The LDS (104 KiB) costs
 // the second block per CU the packed counts bought; the contiguous stores win.
+// (lab) the largest chunk rounds the staging takes: at 8,192-packet chunks it costs one block
+// per CU (139 KiB) and still wins, NGA-32 shuffled 654 vs 691 us unstaged at two blocks per
+// CU (profiles/r04/lab/stage_big_chunk_ab_v32.log)
+#ifndef INA_SORT_STAGE_MAX_R
+#define INA_SORT_STAGE_MAX_R 8
+#endif
 #ifndef INA_SORT_STAGE
 #define INA_SORT_STAGE 1
 #endif
@@ -929,7 +935,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     }
     __syncthreads();
 #if INA_SORT_STAGE
-    if constexpr (kHalf) {
+    if constexpr (kHalf && R <= INA_SORT_STAGE_MAX_R) {
         // the chunk's sorted output lands in LDS, then leaves as one contiguous stretch (the
         // 2,048-bin scatter writes runs of ~2 items: scattered 4-byte stores)
         __shared__ uint32_t s_k[kBkThr * R], s_v[kBkThr * R];
