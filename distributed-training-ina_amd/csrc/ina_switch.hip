@@ -705,6 +705,10 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
 // (lab) the largest chunk rounds the staging takes: at 8,192-packet chunks it costs one block
 // per CU (139 KiB) and still wins, NGA-32 shuffled 654 vs 691 us unstaged at two blocks per
 // CU (profiles/r04/lab/stage_big_chunk_ab_v32.log)
+// the staging reuses the digit-count LDS once the offsets are read (0: its own arrays)
+#ifndef INA_SORT_STAGE_ALIAS
+#define INA_SORT_STAGE_ALIAS 1
+#endif
 #ifndef INA_SORT_STAGE_MAX_R
 #define INA_SORT_STAGE_MAX_R 8
 #endif
@@ -760,6 +764,9 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
     }
     __syncthreads();
     const unsigned long long below = (1ull << lane) - 1ull;
+    uint32_t spos[R];                                 // staged: the items' chunk-local places
+#pragma unroll
+    for (int r = 0; r < R; ++r) spos[r] = 0xFFFFFFFFu;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r >= rw || i0 - (size_t)lane + (size_t)r * 64 >= n) break;   // wave-uniform
@@ -771,8 +778,12 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
         if (valid) {
             const uint32_t pos = gst[d] + b0 + rank;
             if constexpr (kStage) {                   // the chunk's output staged in LDS
+#if INA_SORT_STAGE_ALIAS
+                spos[r] = pos - sbase;
+#else
                 sk[pos - sbase] = k[r];
                 sv[pos - sbase] = v[r];
+#endif
             } else {
                 kout[pos] = k[r];
                 vout[pos] = v[r];
@@ -780,6 +791,19 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
             if (rank == 0) atomicAdd(&row[d], (uint32_t)__builtin_popcountll(pm) << sh);
         }
     }
+#if INA_SORT_STAGE_ALIAS
+    if constexpr (kStage) {
+        // the staging area is the count array itself (sk, sv alias base): every wave's
+        // offsets are read before any item lands there
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (spos[r] != 0xFFFFFFFFu) {
+                sk[spos[r]] = k[r];
+                sv[spos[r]] = v[r];
+            }
+    }
+#endif
 }
 
 // kMode: 0 the chunk pass (keys, detection, digits, scatter); split in two (tuning key 19, the
@@ -938,7 +962,15 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     if constexpr (kHalf && R <= INA_SORT_STAGE_MAX_R) {
         // the chunk's sorted output lands in LDS, then leaves as one contiguous stretch (the
         // 2,048-bin scatter writes runs of ~2 items: scattered 4-byte stores)
+#if INA_SORT_STAGE_ALIAS
+        // the chunk's 2 x 4 x kBkThr x R bytes fit the packed count array (8 x 2,048 words
+        // at R = 8): 139 -> 74 KiB at 8,192-packet chunks, two blocks per CU
+        static_assert(2 * kBkThr * R <= (kBkWaves / 2) * BINS, "staging fits the count array");
+        uint32_t* s_k = &base[0][0];
+        uint32_t* s_v = s_k + kBkThr * R;
+#else
         __shared__ uint32_t s_k[kBkThr * R], s_v[kBkThr * R];
+#endif
         const uint32_t cb = (uint32_t)(c * (size_t)(kBkThr * R));
         rs_tile_scatter_half<R, BINS, true>(k, v, i0, npk, lb, hbits, base, gst, kout, vout, R, s_k, s_v, cb);
         __syncthreads();
