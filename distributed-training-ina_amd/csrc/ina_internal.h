@@ -27,6 +27,7 @@ int set_tiny_max(int v);      // ina_switch.hip
 int set_bucket_tile(int v);   // ina_switch.hip
 int set_runs(int v);          // ina_switch.hip
 int set_pre_all(int v);       // ina_switch.hip
+int set_local(int v);         // ina_switch.hip
 int ew_grid_cap();            // ina_kernels.hip: grid cap of the elementwise kernels (tuning key 14)
 
 }  // namespace ina

@@ -1968,6 +1968,7 @@ int ina_set_tuning(int key, int value) {
         case 17: return set_bucket_tile(value);
         case 18: return set_runs(value);
         case 19: return set_pre_all(value);
+        case 20: return set_local(value);
         default: return INA_EINVAL;
     }
 }

@@ -303,6 +303,11 @@ int set_runs(int v) {
     g_runs = v ? 1 : 0;
     return INA_OK;
 }
+static std::atomic<int> g_local{1};        // ina_set_tuning key 20: near-sorted batches skip the sort (0: off)
+int set_local(int v) {
+    g_local = v ? 1 : 0;
+    return INA_OK;
+}
 // ina_set_tuning key 19: the split chunk pass (detection, decision, then digits) for every key
 // width (1, default) or for keys of 19-22 bits only (0).  Interleaved over packed and split
 // rows at 819,200 NGA-256 packets (tools/lab/switch_pre_lab.py, profiles/r04/lab): worker-
@@ -668,7 +673,15 @@ constexpr int kRunsMax = 64;   // one run per lane of the run kernel's waves
 // (start[R] = npk), key[kRunsMax] (slot | ack bit of each run's first packet)
 constexpr int kCtlForeign = 0, kCtlEpochs = 1, kCtlRuns = 4;
 constexpr int kRunsStart = 1, kRunsKey = 2 + kRunsMax;
-constexpr int kCtlWords = kCtlRuns + kRunsKey + kRunsMax;
+// then the near-sorted path's words (see "near-sorted batches" below): the epoch of the last
+// call that chose it, the smallest slot key, the number of slots its table covers and the
+// number of units
+constexpr int kCtlLocal = kCtlRuns + kRunsKey + kRunsMax;
+constexpr int kLocEpoch = kCtlLocal - kCtlEpochs;     // offsets from the epochs (`unsorted`)
+constexpr int kLocKmin = kLocEpoch + 1, kLocSlots = kLocEpoch + 2, kLocUnits = kLocEpoch + 3;
+constexpr int kLocVerdict = kLocEpoch + 6;            // 2 words: the decision, (epoch << 1) | local
+static_assert((kCtlEpochs + kLocVerdict) % 2 == 0, "the verdict is 8-byte aligned in the control block");
+constexpr int kCtlWords = kCtlLocal + 8;
 static_assert(kCtlWords * 4 <= 1024, "control block fits its 1 KiB");
 
 // the run table from the chunks' break records (a structured batch, total <= kRunsMax breaks),
@@ -698,6 +711,355 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
     }
 }
 
+// lds_count with the count shifted into the wave's half (the partner wave adds to the other
+// half of the same word, hence atomics)
+__device__ __forceinline__ void lds_count_half(uint32_t* h, uint32_t d, bool valid, int sh) {
+    const unsigned long long act = __ballot(valid);
+    if (!act) return;
+    const int first = __builtin_ctzll(act);
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, first);
+    const unsigned long long same = __ballot(valid && d == d0);
+    if (same == act) {
+        if ((int)(threadIdx.x & 63) == first) atomicAdd(&h[d0], (uint32_t)__builtin_popcountll(act) << sh);
+    } else if (valid) {
+        atomicAdd(&h[d], 1u << sh);
+    }
+}
+
+// ---- near-sorted batches: per-slot lists, no sort (round 5) ---------------------------------
+// W senders each emit their packets in sequence order (DataManager.py:116-134); a NIC that
+// interleaves them with local disorder delivers a batch whose every packet sits within some
+// distance D of its place in slot order, yet with far more than kRunsMax descents: neither in
+// order nor dense runs, so it used to take the full chunk + bucket sort.  Such a batch needs no
+// global order -- slots are independent (ngaa.p4:87-168), so each slot only needs its own
+// packets in arrival order (ngaa.p4:120-196):
+//   * the detection pass records each GRANULE's (kGranWaves waves of a chunk: 1/8 of it)
+//     smallest and largest slot key;
+//   * the digit pass's block 0 (local_decide; the other blocks wait for its verdict) turns them
+//     into PM[g] = max over granules <= g and SM[g] = min over granules >= g (both non-decreasing).
+//     UNIT u (kLocU granules) takes the slots [SM(u kLocU), SM((u+1) kLocU)): every packet past
+//     the unit's granules has a key >= the unit's upper bound, and every packet before granule
+//     g_lo(u) = the first g with PM[g] >= its lower bound has a key below it, so the unit's
+//     packets all lie in its WINDOW, granule g_lo(u) to its last granule, whatever the disorder
+//     -- which only widens the windows.  The path is taken when the windows' total scan (x the
+//     LDS passes a wide slot range needs) stays within kLocBeta times the batch and no window
+//     exceeds 65,535 positions; it writes the unit table;
+//   * a unit's place in the list area needs no global scan: A(u) = #packets with a key below
+//     its slots + #foreign packets before its granules = g_lo(u)'s first position + the window's
+//     packets before the unit's granules that are foreign or below its slots, and A(u+1) - A(u)
+//     >= the unit's packets;
+//   * k_local_lists builds the lists, a 4-wave block per unit: its waves scan the unit's window
+//     in position order, per-wave LDS counts of its slots (16-bit halves: counts and cursors stay
+//     inside the window), a block scan, then each packet to its slot's list at the wave's cursor
+//     + its ballot rank among the round's lanes of the same slot -- a stable counting sort: ids[]
+//     (the sort's idle k_out) holds each slot's packets in arrival order, tab[slot - kmin] its
+//     (first entry, length);
+//   * the run kernel's lane groups take 8 slots at a time and walk each list through
+//     group_packet -- the run table's and the sorted run's per-packet code.
+// No key array is sorted, the ids are written once, and the row gather is as local as the arrival.
+constexpr int kGranWaves = 2;                                 // detection-pass waves per granule
+constexpr int kGranPerChunk = kBkWaves / kGranWaves;          // 8 granules per chunk
+constexpr int kLocMaxGran = 8 * kBkThr;                       // the decision: <= 8 granules a thread
+constexpr uint32_t kLocBeta = 3;                              // the windows' scan <= 3 x the batch
+constexpr uint32_t kLocMaxWindow = 65535;                     // 16-bit cursors
+#ifndef INA_LOC_U
+#define INA_LOC_U 4                                           // granules per unit (a half chunk)
+#endif
+constexpr uint32_t kLocU = INA_LOC_U;
+constexpr int kLlWaves = 4;                                   // waves per unit in the list build
+constexpr int kLlBins = 1024;                                 // slots one LDS pass counts
+constexpr int kLlBits = 10;
+constexpr int kLlRounds = 16;                                 // key rounds a lane holds
+
+// wave-wide inclusive max (lane i: max over lanes <= i) and suffix min (lane i: min over lanes >= i)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x = max(x, y);
+    }
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_suffix_min(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_down((int)x, o);
+        if (lane + o < 64) x = min(x, y);
+    }
+    return x;
+}
+
+// unit u: slots [lo, hi), window from granule g_lo to the unit's last granule
+struct LocUnit {
+    uint32_t g_lo, lo, hi, pad;
+};
+
+// The near-sorted decision (call convergent): true when the batch takes the path.  `writer`
+// also writes the unit table and the control words.  s_pm / s_sm: G words each of the caller's LDS (its count array,
+// free before the digits); s_a / s_b: kBkWaves words each.
+__device__ __forceinline__ bool local_decide(const uint32_t* __restrict__ gmin, const uint32_t* __restrict__ gmax,
+                                             uint32_t G, uint32_t gsize, size_t npk,
+                                             uint32_t* __restrict__ unsorted, uint32_t epoch,
+                                             LocUnit* __restrict__ units, bool writer, uint32_t* s_pm,
+                                             uint32_t* s_sm, uint32_t* s_a, uint32_t* s_b) {
+    __shared__ unsigned long long s_cost[kBkWaves];
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    // the bounds into LDS, coalesced (every load in flight at once)
+#pragma unroll
+    for (int j = 0; j < kLocMaxGran / kBkThr; ++j) {
+        const uint32_t g = threadIdx.x + (uint32_t)j * kBkThr;
+        if (g < G) {
+            s_pm[g] = gmax[g];
+            s_sm[g] = gmin[g];
+        }
+    }
+    __syncthreads();
+    // thread t: granules [g0, g1) -- prefix max / suffix min inside the thread ...
+    const uint32_t kpt = (G + kBkThr - 1) / kBkThr;
+    const uint32_t g0 = min(threadIdx.x * kpt, G);
+    const uint32_t g1 = min(g0 + kpt, G);
+    uint32_t tmax = 0, tmin = 0xFFFFFFFFu;
+    for (uint32_t g = g0; g < g1; ++g) s_pm[g] = tmax = max(tmax, s_pm[g]);
+    for (uint32_t g = g1; g-- > g0;) s_sm[g] = tmin = min(tmin, s_sm[g]);
+    // ... and over the threads: the max of the earlier ones, the min of the later ones
+    const uint32_t imx = wave_incl_max(tmax), imn = wave_suffix_min(tmin);
+    if (lane == 63) s_a[wv] = imx;
+    if (lane == 0) s_b[wv] = imn;
+    __syncthreads();
+    uint32_t xmx = 0, xmn = 0xFFFFFFFFu, kmax = 0, kmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int w = 0; w < kBkWaves; ++w) {
+        const uint32_t a = s_a[w], b = s_b[w];
+        xmx = w < wv ? max(xmx, a) : xmx;
+        xmn = w > wv ? min(xmn, b) : xmn;
+        kmax = max(kmax, a);
+        kmin = min(kmin, b);
+    }
+    {
+        const uint32_t up = (uint32_t)__shfl_up((int)imx, 1), dn = (uint32_t)__shfl_down((int)imn, 1);
+        if (lane > 0) xmx = max(xmx, up);
+        if (lane < 63) xmn = min(xmn, dn);
+    }
+    for (uint32_t g = g0; g < g1; ++g) {
+        s_pm[g] = max(s_pm[g], xmx);
+        s_sm[g] = min(s_sm[g], xmn);
+    }
+    __syncthreads();                                          // PM / SM final; s_a is reused
+    if (kmin > kmax) return false;                            // no packet of this switch
+    // the units: slot range, window, scan cost (window x LDS passes)
+    const auto unit_of = [&](uint32_t u) {
+        const uint32_t a = s_sm[u * kLocU];
+        const uint32_t b = (u + 1) * kLocU < G ? s_sm[(u + 1) * kLocU] : 0xFFFFFFFFu;
+        const uint32_t lo = a == 0xFFFFFFFFu ? kmax + 1u : a, hi = b == 0xFFFFFFFFu ? kmax + 1u : b;
+        uint32_t l = 0, r = G;                                // g_lo: PM is non-decreasing
+        while (l < r) {
+            const uint32_t m = (l + r) >> 1;
+            if (s_pm[m] >= lo) r = m; else l = m + 1;
+        }
+        return LocUnit{l, lo, hi, 0u};
+    };
+    const uint32_t nu = (G + kLocU - 1) / kLocU;
+    unsigned long long cost = 0;
+    uint32_t maxwin = 0;
+    for (uint32_t u = threadIdx.x; u < nu; u += kBkThr) {
+        const LocUnit un = unit_of(u);
+        const size_t p0 = (size_t)un.g_lo * gsize, p1 = min((size_t)(u + 1) * kLocU * gsize, npk);
+        const uint32_t win = un.hi > un.lo && p1 > p0 ? (uint32_t)min(p1 - p0, (size_t)0xFFFFFFFFu) : 0u;
+        cost += (unsigned long long)((un.hi - un.lo + kLlBins - 1) / kLlBins) * win;
+        maxwin = max(maxwin, win);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cost += (unsigned long long)__shfl_xor((long long)cost, o);
+        maxwin = max(maxwin, (uint32_t)__shfl_xor((int)maxwin, o));
+    }
+    if (lane == 0) {
+        s_cost[wv] = cost;
+        s_a[wv] = maxwin;
+    }
+    __syncthreads();
+    unsigned long long total = 0;
+    uint32_t mw = 0;
+#pragma unroll
+    for (int w = 0; w < kBkWaves; ++w) {
+        total += s_cost[w];
+        mw = max(mw, s_a[w]);
+    }
+    if (mw > kLocMaxWindow || total > (unsigned long long)kLocBeta * npk) return false;   // the sort
+    if (writer) {
+        for (uint32_t u = threadIdx.x; u < nu; u += kBkThr) units[u] = unit_of(u);
+        if (threadIdx.x == 0) {
+            unsorted[kLocKmin] = kmin;
+            unsorted[kLocSlots] = kmax + 1u - kmin;
+            unsorted[kLocUnits] = nu;
+            unsorted[kLocEpoch] = epoch;                      // the lists, no sort
+        }
+    }
+    return true;
+}
+
+#ifndef INA_LOC_TIMING
+#define INA_LOC_TIMING 0
+#endif
+#if INA_LOC_TIMING
+// lab builds only: per-unit wall-clock stamps of k_local_lists' phases (tools/lab)
+__device__ unsigned long long g_loc_t[8192][4];
+#define LOC_STAMP(q) do { if (threadIdx.x == 0 && u < 8192) g_loc_t[u][q] = wall_clock64(); } while (0)
+#else
+#define LOC_STAMP(q) do { } while (0)
+#endif
+
+// The near-sorted path's lists (see local_decide): one kLlWaves-wave block per unit at a time
+// (units u = the block's XCD-ordered index + k * grid: neighbouring units, whose windows share
+// granules, through one L2).  Wave w takes its share of the unit's window, in position order,
+// holding up to kLlRounds rounds of keys in registers; per pass over kLlBins of the unit's slots:
+// per-wave LDS counts (two waves' 16-bit halves per word: counts and cursors stay inside the
+// window), a block scan -> each slot's first entry and length (tab) and each wave's cursor; then
+// every packet of those slots to its list at the cursor + its ballot rank among the round's
+// lanes of the same slot (a stable counting sort).  ids[e] = packet | PS-ack bit 31 (by its sort
+// key).
+__device__ __forceinline__ size_t switch_block_index();
+__global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_local_lists(const uint32_t* __restrict__ keys, size_t npk,
+                                                               uint32_t num_slots, uint32_t kmask,
+                                                               const uint32_t* __restrict__ unsorted,
+                                                               const LocUnit* __restrict__ units, uint32_t gsize,
+                                                               uint32_t* __restrict__ ids, uint2* __restrict__ tab) {
+    constexpr int kThr = kLlWaves * 64;
+    constexpr int DPT = kLlBins / kThr;                           // consecutive slots a thread scans
+    __shared__ uint32_t cw[kLlWaves / 2][kLlBins];                // per-wave counts, then cursors
+    __shared__ uint32_t s_ws[kLlWaves];
+    const uint32_t ep = unsorted[1];
+    if (unsorted[kLocEpoch] != ep) return;                        // not this path's batch
+    const int lane = threadIdx.x & 63, wv = wave_in_block();
+    const int sh = (wv & 1) * 16;
+    uint32_t* crow = cw[wv >> 1];
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const uint32_t kmin = unsorted[kLocKmin], nunits = unsorted[kLocUnits];
+    for (uint32_t u = (uint32_t)switch_block_index(); u < nunits; u += gridDim.x) {
+        const LocUnit w = units[u];
+        if (w.hi <= w.lo) continue;                               // no slot (block-uniform)
+        LOC_STAMP(0);
+        // positions fit 32 bits (npk <= 2^31 - 1)
+        const uint32_t P0 = w.g_lo * gsize, Pu = u * kLocU * gsize;
+        const uint32_t P1 = (uint32_t)min((size_t)Pu + (size_t)kLocU * gsize, npk);
+        const uint32_t per = ((P1 - P0 + kLlWaves * 64 - 1) / (kLlWaves * 64)) * 64;
+        const uint32_t b0 = min(P0 + (uint32_t)wv * per, P1), b1 = min(b0 + per, P1);
+        const bool held = per <= 64u * kLlRounds;                 // the keys stay in registers
+        uint32_t kk[kLlRounds];
+        if (held) {
+#pragma unroll
+            for (int r = 0; r < kLlRounds; ++r) {
+                const uint32_t p = b0 + (uint32_t)(r * 64 + lane);
+                kk[r] = p < b1 ? keys[p] : num_slots;
+            }
+        }
+        uint32_t area = 0;
+        for (uint32_t q = w.lo; q < w.hi; q += kLlBins) {
+            const uint32_t qn = min((uint32_t)kLlBins, w.hi - q);
+            for (uint32_t d = lane; d < (uint32_t)kLlBins; d += 64) crow[d] = 0u;
+            __syncthreads();                                      // the partner wave zeroes too
+            uint32_t before = 0;                                  // (first pass) the area's count
+            for (uint32_t r0 = b0; r0 < b1; r0 += 64 * kLlRounds) {
+                if (!held) {
+#pragma unroll
+                    for (int r = 0; r < kLlRounds; ++r) {
+                        const uint32_t p = r0 + (uint32_t)(r * 64 + lane);
+                        kk[r] = p < b1 ? keys[p] : num_slots;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < kLlRounds; ++r) {
+                    const uint32_t slot = kk[r] & kmask;
+                    const uint32_t p = r0 + (uint32_t)(r * 64 + lane);
+                    lds_count_half(crow, slot - q, slot < num_slots && slot - q < qn, sh);
+                    before += (p < Pu && p < b1 && (slot < w.lo || slot >= num_slots)) ? 1u : 0u;
+                }
+            }
+            if (q == w.lo) {
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) before += (uint32_t)__shfl_xor((int)before, o);
+                if (lane == 0) s_ws[wv] = before;
+            }
+            __syncthreads();
+            if (q == w.lo) {
+                area = P0;
+#pragma unroll
+                for (int v = 0; v < kLlWaves; ++v) area += s_ws[v];
+            }
+            LOC_STAMP(1);
+            // thread t: slots d = t*DPT + j -- totals, the block scan, then the per-wave cursors
+            uint32_t tc[DPT], tt = 0;
+#pragma unroll
+            for (int j = 0; j < DPT; ++j) {
+                const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+                uint32_t t = 0;
+#pragma unroll
+                for (int v2 = 0; v2 < kLlWaves / 2; ++v2) {
+                    const uint32_t word = cw[v2][d];
+                    t += (word & 0xFFFFu) + (word >> 16);
+                }
+                tc[j] = t;
+                tt += t;
+            }
+            __syncthreads();                                      // s_ws is reused by the scan
+            const uint32_t inc = wave_incl_scan(tt);
+            if (lane == 63) s_ws[wv] = inc;
+            __syncthreads();
+            uint32_t e = inc - tt, passn = 0;
+#pragma unroll
+            for (int v = 0; v < kLlWaves; ++v) {
+                const uint32_t x = s_ws[v];
+                e += v < wv ? x : 0u;
+                passn += x;
+            }
+#pragma unroll
+            for (int j = 0; j < DPT; ++j) {
+                const uint32_t d = threadIdx.x * DPT + (uint32_t)j;
+                if (d < qn) tab[q + d - kmin] = uint2{area + e, tc[j]};
+                uint32_t b = e;
+#pragma unroll
+                for (int v2 = 0; v2 < kLlWaves / 2; ++v2) {
+                    const uint32_t word = cw[v2][d];
+                    const uint32_t lo16 = word & 0xFFFFu;
+                    cw[v2][d] = b | ((b + lo16) << 16);           // cursors, relative to the area
+                    b += lo16 + (word >> 16);
+                }
+                e += tc[j];
+            }
+            __syncthreads();
+            LOC_STAMP(2);
+            for (uint32_t r0 = b0; r0 < b1; r0 += 64 * kLlRounds) { // the lists, in arrival order
+                if (!held) {
+#pragma unroll
+                    for (int r = 0; r < kLlRounds; ++r) {
+                        const uint32_t p = r0 + (uint32_t)(r * 64 + lane);
+                        kk[r] = p < b1 ? keys[p] : num_slots;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < kLlRounds; ++r) {
+                    if (r0 + (uint32_t)(r * 64) >= b1) break;     // wave-uniform
+                    const uint32_t slot = kk[r] & kmask;
+                    const uint32_t d = slot - q;
+                    const bool valid = slot < num_slots && d < qn;
+                    const unsigned long long pm = lanes_with_digit(d, kLlBits, valid);
+                    if (valid) {
+                        const uint32_t rank = (uint32_t)__builtin_popcountll(pm & below);
+                        const uint32_t cur = (crow[d] >> sh) & 0xFFFFu;
+                        ids[area + cur + rank] = (r0 + (uint32_t)(r * 64 + lane)) | (kk[r] & ~kmask);
+                        if (rank == 0) atomicAdd(&crow[d], (uint32_t)__builtin_popcountll(pm) << sh);
+                    }
+                }
+            }
+            area += passn;
+            __syncthreads();                                      // cw of the next pass or unit
+        }
+        LOC_STAMP(3);
+    }
+}
+
 // the 2,048-bin chunk pass stages its sorted chunk in LDS and writes it out contiguously
 // (interleaved A/B at NGA-32 C3 size, shuffled: 732.8 -> 709.2 us packed, 639.7 -> 615.9 us
 // split, bytes equal; profiles/r04/lab/sort_stage_ab_v32.log).  The LDS (104 KiB) costs
@@ -719,21 +1081,6 @@ __device__ __forceinline__ void build_run_table(const uint32_t* __restrict__ brk
 // counts in one LDS word (16 bits each: a wave counts at most 64 x 8 items of a digit, and
 // the offsets below stay inside one chunk or tile, <= 8,192): half the count array, so two
 // chunk blocks or three bucket blocks (1,024 bins) share a CU instead of one.
-// lds_count with the count shifted into the wave's half (the partner wave adds to the other
-// half of the same word, hence atomics)
-__device__ __forceinline__ void lds_count_half(uint32_t* h, uint32_t d, bool valid, int sh) {
-    const unsigned long long act = __ballot(valid);
-    if (!act) return;
-    const int first = __builtin_ctzll(act);
-    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, first);
-    const unsigned long long same = __ballot(valid && d == d0);
-    if (same == act) {
-        if ((int)(threadIdx.x & 63) == first) atomicAdd(&h[d0], (uint32_t)__builtin_popcountll(act) << sh);
-    } else if (valid) {
-        atomicAdd(&h[d], 1u << sh);
-    }
-}
-
 // rs_tile_scatter over the packed counts: each wave's offset of digit d inside the digit's
 // run in this chunk (16-bit halves), the run's first output position in gst[d]
 template <int R, int BINS, bool kStage = false>
@@ -822,15 +1169,19 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                                                         uint32_t* __restrict__ vout, int ack_hint,
                                                         uint32_t* __restrict__ unsorted, uint32_t epoch,
                                                         uint32_t* __restrict__ brk_cnt,
-                                                        uint2* __restrict__ brk_ent) {
+                                                        uint2* __restrict__ brk_ent,
+                                                        uint32_t* __restrict__ gstat, LocUnit* __restrict__ units) {
     // per-wave digit counts, then bases (2,048 bins: two waves' 16-bit halves per word)
     constexpr bool kHalf = BINS > kBkThr;
     __shared__ uint32_t base[kHalf ? kBkWaves / 2 : kBkWaves][BINS];
     __shared__ uint32_t gst[BINS];                    // the chunk's run starts (output positions)
     __shared__ uint32_t wtot[kBkWaves];
     __shared__ uint32_t wbrk[kBkWaves];               // per-wave break counts
+    __shared__ uint32_t wgmn[kBkWaves], wgmx[kBkWaves];   // per-wave slot-key bounds (near-sorted path)
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const size_t c = blockIdx.x;
+    // gstat (near-sorted path on): granule bounds, gmin[G] then gmax[G], G = 8 granules a chunk
+    const uint32_t G = (uint32_t)nch * (uint32_t)kGranPerChunk;
     if constexpr (kMode == 2) {
         if (unsorted[0] != epoch) return;             // in slot order: no sort
         if (brk_cnt) {
@@ -851,6 +1202,32 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                 return;
             }
         }
+        // local disorder within the scan budget: the near-sorted path (the bucket pass builds its
+        // lists), no sort.  PM / SM live in the count array (the host takes the path only for G
+        // <= half of it)
+        // Block 0 decides and publishes the verdict (epoch-tagged, agent scope); the other blocks
+        // only poll it (block 0 is dispatched first and waits on nothing, so every poll ends)
+        if (gstat) {
+            __shared__ uint32_t s_loc;
+            unsigned long long* verdict = reinterpret_cast<unsigned long long*>(unsorted + kLocVerdict);
+            if (c == 0) {
+                const bool loc = local_decide(gstat, gstat + G, G, (uint32_t)(kBkThr * R / kGranPerChunk), npk,
+                                              unsorted, epoch, units, true, &base[0][0],
+                                              &base[0][0] + sizeof(base) / 8, wtot, wbrk);
+                if (threadIdx.x == 0) {
+                    __hip_atomic_store(verdict, ((unsigned long long)epoch << 1) | (loc ? 1ull : 0ull),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_loc = loc ? 1u : 0u;
+                }
+            } else if (threadIdx.x == 0) {
+                unsigned long long v;
+                while (((v = __hip_atomic_load(verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) != epoch)
+                    __builtin_amdgcn_s_sleep(8);
+                s_loc = (uint32_t)(v & 1ull);
+            }
+            __syncthreads();
+            if (s_loc) return;
+        }
     }
     const uint32_t nb = 1u << hbits;
     if constexpr (kMode != 1)
@@ -869,11 +1246,16 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     uint32_t prevf = prev | ((ack_hint && pmine && pack[0]) ? kAckBit : 0u);   // with the ack bit
     bool down = false;                                        // a key below its predecessor's
     unsigned long long bm[R];                                 // breaks of the dense runs
+    uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;                     // this lane's slot-key bounds
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const size_t p = i0 + (size_t)r * 64;
         const bool mine = switch_id >= 0 && sid[r] == (uint32_t)(uint8_t)switch_id;
         const uint32_t key = mine ? idx[r] % num_slots : num_slots;
+        if (kMode == 1 && mine && p < npk) {
+            kmn = min(kmn, key);
+            kmx = max(kmx, key);
+        }
         // bit 31 carries "PS ack" through the sort (no digit reads it)
         k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
         v[r] = (uint32_t)p;
@@ -904,7 +1286,28 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
 #pragma unroll
     for (int r = 0; r < R; ++r) nbw += (uint32_t)__builtin_popcountll(bm[r]);
     if (lane == 0) wbrk[wv] = nbw;
+    if (kMode == 1 && gstat) {                                // the wave's slot-key bounds
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            kmn = min(kmn, (uint32_t)__shfl_xor((int)kmn, o));
+            kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, o));
+        }
+        if (lane == 0) {
+            wgmn[wv] = kmn;
+            wgmx[wv] = kmx;
+        }
+    }
     __syncthreads();
+    if (kMode == 1 && gstat && threadIdx.x < (unsigned)kGranPerChunk) {   // granule = kGranWaves waves
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+#pragma unroll
+        for (int w = 0; w < kGranWaves; ++w) {
+            mn = min(mn, wgmn[threadIdx.x * kGranWaves + w]);
+            mx = max(mx, wgmx[threadIdx.x * kGranWaves + w]);
+        }
+        gstat[c * kGranPerChunk + threadIdx.x] = mn;
+        gstat[G + c * kGranPerChunk + threadIdx.x] = mx;
+    }
     if (kMode != 2 && brk_cnt) {                              // the chunk's breaks, in order
         uint32_t tot = 0, pre = 0;
 #pragma unroll
@@ -1046,7 +1449,7 @@ __global__ __launch_bounds__(kBkThr, BINS <= 1024 ? 2 * kBkThr / 256 : kBkThr / 
     // run kernel reads it there (sorted_copy = 0), so only the foreign bucket's size is needed
     const bool in_order = unsorted[0] != epoch;
     // after the split chunk pass (pre): structured batches were decided, nothing to gather
-    if (pre && (in_order || unsorted[2] == epoch)) return;
+    if (pre && (in_order || unsorted[2] == epoch || unsorted[kLocEpoch] == epoch)) return;
     if (in_order && !sorted_copy && b != skip) return;
     if (!in_order && brk_cnt) {
         // dense ascending runs (brk_cnt != NULL only for the register-resident run kernel):
@@ -1989,7 +2392,7 @@ constexpr int kSlotInFlight = kSplit ? INA_SWITCH_SLOT_INFLIGHT_SPLIT : INA_SWIT
 // same header): ack / collision / count / Processor add, the PS step, the rewritten packet
 // and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
 // header chunk / header row; ack_known: a PS ack by its sort key (then m and h are unread)
-template <bool kPs, bool kSplit>
+template <bool kPs, bool kSplit, int kThr = kSwBlock>
 __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                              size_t stride, uint8_t* __restrict__ pay,
                                              uint8_t* __restrict__ actions, const PsFuse& ps, uint32_t slot,
@@ -1999,7 +2402,7 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
     // returns its fallback, and the compiler may narrow EXEC around a DPP that feeds a per-lane
     // select (it did: l == 0 ? h3 : row_shr(m.w) became a branch on l != 0).  Every lane of the
     // group stores, then reads its neighbour's word (LDS executes one wave's ops in order)
-    __shared__ uint32_t s_xch[kSwBlock];
+    __shared__ uint32_t s_xch[kThr];
     const int l = threadIdx.x & 7;
     const int V = st.V, L = V >> 2;
     const bool vl = l < L;
@@ -2230,6 +2633,93 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
             if (have_reg && vl)
                 __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)hslot * V + 4 * l));
         }
+    }
+}
+
+// Narrow packets (V <= 32) from the near-sorted path's per-slot lists (local_lists): each wave
+// takes 8 consecutive slots at a time (grid-stride; consecutive waves of an XCD take neighbouring
+// slots), lane group g slot s8 + g: its (first entry, length) from the slot table, its list's
+// first 8 packet ids one per lane (loaded beside the slot's count and frag), then the packets in
+// list order = arrival order (ngaa.p4:120-196) through group_packet, kP loads in flight.
+template <bool kPs, bool kSplit>
+__device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
+                                                   size_t stride, uint8_t* __restrict__ pay,
+                                                   uint8_t* __restrict__ actions, const PsFuse& ps,
+                                                   const uint32_t* __restrict__ ids, const uint2* __restrict__ tab,
+                                                   uint32_t kmin, uint32_t nslot, size_t wave, size_t nwaves) {
+    constexpr int kP = kSlotInFlight<kSplit>;
+    static_assert(8 % kP == 0, "a batch of list entries never crosses a group of 8 ids");
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 3, l = lane & 7;
+    const int V = st.V, L = V >> 2;
+    const bool vl = l < L;
+    // the next 8 slots' table entries and first ids are loaded one step ahead (the table ->
+    // ids -> rows chain would otherwise cost two round trips per step more than an in-order batch)
+    const size_t step = nwaves * 8;
+    size_t s8 = wave * 8;
+    uint2 e_nx = s8 + (size_t)g < nslot ? tab[s8 + (size_t)g] : uint2{0u, 0u};
+    uint32_t id_nx = (uint32_t)l < e_nx.y ? ids[e_nx.x + (uint32_t)l] : 0u;
+    for (; s8 < nslot; s8 += step) {
+        const uint32_t hst = e_nx.x, hlen = e_nx.y;
+        uint32_t idl = id_nx;                                      // entries 0..7 of the list
+        const size_t sn = s8 + step + (size_t)g;
+        e_nx = sn < nslot ? tab[sn] : uint2{0u, 0u};
+        uint32_t maxlen = hlen;
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, o));
+        maxlen = __builtin_amdgcn_readfirstlane(maxlen);
+        if (maxlen == 0) {
+            id_nx = (uint32_t)l < e_nx.y ? ids[e_nx.x + (uint32_t)l] : 0u;
+            continue;
+        }
+        const uint32_t slot = kmin + (uint32_t)s8 + (uint32_t)g;
+        const bool has = hlen != 0;
+        uint32_t cnt = 0, frag = 0;
+        if (has) {
+            cnt = st.count[slot];
+            frag = st.frag[slot];
+        }
+        u32x4s reg = {0u, 0u, 0u, 0u};
+        bool have_reg = false;
+        for (uint32_t k0 = 0; k0 < maxlen; k0 += kP) {
+            if (k0 && (k0 & 7u) == 0)                              // entries k0..k0+7
+                idl = k0 + (uint32_t)l < hlen ? ids[hst + k0 + (uint32_t)l] : 0u;
+            u32x4s m[kP], h[kP];
+            uint32_t pid[kP];
+            bool in[kP], acq[kP];
+#pragma unroll
+            for (int j = 0; j < kP; ++j) {
+                const uint32_t k = k0 + (uint32_t)j;
+                in[j] = k < hlen;
+                const uint32_t en = (uint32_t)__shfl((int)idl, 8 * g + (int)(k & 7u));   // every lane active
+                pid[j] = en & ~kAckBit;
+                acq[j] = (en & kAckBit) != 0u;                     // a PS ack by its sort key
+                if (in[j] && !acq[j]) {
+                    if constexpr (kSplit) {
+                        m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) + (vl ? l : 0));
+                        h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+                    } else {
+                        const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
+                        m[j] = sw_ld(pk + (vl ? l + 1 : 1));
+                        h[j] = *pk;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kP; ++j) {
+                if (!__ballot(in[j])) continue;
+                if (!in[j]) continue;
+                group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, pid[j], m[j], h[j], acq[j], cnt,
+                                          frag, reg, have_reg);
+            }
+        }
+        id_nx = (uint32_t)l < e_nx.y ? ids[e_nx.x + (uint32_t)l] : 0u;   // the next step's first ids
+        if (has && l == 0) {
+            st.count[slot] = (uint8_t)cnt;
+            st.frag[slot] = frag;
+        }
+        if (have_reg && vl)
+            __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
     }
 }
 
@@ -2552,13 +3042,21 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                           const uint32_t* __restrict__ nforeign,
                                                           const uint32_t* __restrict__ keys_a,
                                                           const uint32_t* __restrict__ ids_a,
-                                                          const uint32_t* __restrict__ unsorted) {
+                                                          const uint32_t* __restrict__ unsorted,
+                                                          const uint32_t* __restrict__ loc_ids,
+                                                          const uint2* __restrict__ loc_tab) {
     const size_t wave = switch_block_index() * (kSwBlock / 64) + wave_in_block();
     const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
     // (unsorted[1]: the epoch of the sort that filled the scratch, written by its chunk pass,
     // so a run queued apart from its sort needs no host-side state)
     if (unsorted) {
         const uint32_t ep = unsorted[1];
+        if (unsorted[kLocEpoch] == ep) {                   // a near-sorted batch: its per-slot lists
+            if constexpr (kNarrow)
+                lists_slots_narrow<kPs, kSplit>(st, pkts, stride, pay, actions, ps, loc_ids, loc_tab,
+                                                unsorted[kLocKmin], unsorted[kLocSlots], wave, nwaves);
+            return;
+        }
         if (unsorted[0] != ep) {
             // a batch already in slot order: the chunk sort's own output is the sorted order
             // (after the split chunk pass of wide keys: the arrival-order keys, ids_a NULL --
@@ -2667,6 +3165,9 @@ struct SortAux {
                                   // table; the run table follows
     uint32_t* brk_cnt;            // [nch]
     uint2* brk_ent;               // [nch][kRunsMax]
+    uint32_t* gstat;              // near-sorted path: granule key bounds, gmin[G] then gmax[G]
+    LocUnit* units;               // near-sorted path: per unit (>= 2 granules) its slot range and window
+    uint2* tab;                   // near-sorted path: per slot (first list entry, length)
 };
 
 static size_t sort_nch_cap(size_t npk) {
@@ -2683,7 +3184,8 @@ static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
     const size_t hist = align_up(sort_hist_cap(npk, num_slots) * 4, 256);
     const size_t nc = sort_nch_cap(npk);
     return 2 * hist + align_up((size_t)kRsBins * 4, 256) + 1024 + align_up(nc * 4, 256) +
-           nc * (size_t)kRunsMax * 8;
+           align_up(nc * (size_t)kRunsMax * 8, 256) + align_up(2 * nc * kGranPerChunk * 4, 256) +
+           align_up(nc * (kGranPerChunk / 2) * sizeof(LocUnit), 256) + (size_t)num_slots * 8;
 }
 
 static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
@@ -2698,6 +3200,9 @@ static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
     a.unsorted = ctl + kCtlEpochs;
     a.brk_cnt = ctl + 256;
     a.brk_ent = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(a.brk_cnt) + align_up(nc * 4, 256));
+    a.gstat = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.brk_ent) + align_up(nc * (size_t)kRunsMax * 8, 256));
+    a.units = reinterpret_cast<LocUnit*>(reinterpret_cast<uint8_t*>(a.gstat) + align_up(2 * nc * kGranPerChunk * 4, 256));
+    a.tab = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(a.units) + align_up(nc * (kGranPerChunk / 2) * sizeof(LocUnit), 256));
     return a;
 }
 
@@ -2743,6 +3248,11 @@ using namespace ina;
 
 extern "C" {
 
+#if INA_LOC_TIMING
+int ina_lab_loc_times(unsigned long long* host_out) {  // lab builds only
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_loc_t), sizeof(g_loc_t)) == hipSuccess ? 0 : -1;
+}
+#endif
 #if INA_BK_TIMING
 int ina_lab_bk_times(unsigned long long* host_out) {   // lab builds only
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_bk_t), sizeof(g_bk_t)) == hipSuccess ? 0 : -1;
@@ -2812,6 +3322,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     const uint32_t* nforeign = nullptr;
     const uint32_t* unsorted = nullptr;     // bucket sort: the run kernel may read A's output
     uint32_t epoch = 0;
+    uint32_t loc_gsize = 0;                 // the near-sorted path's granule: 1/8 of a sort chunk
     if (small && fast && npk <= (size_t)g_tiny_max.load()) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
         if (!do_run) return INA_OK;
@@ -2850,6 +3361,13 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // dense ascending runs skip the sort (run table, switch_runs_body): the register-
         // resident run kernel only (ina_set_tuning key 18 = 0 turns it off)
         const bool runs_on = fast && g_runs.load() != 0;
+        // near-sorted batches (local disorder) skip the sort and run from per-slot lists: the
+        // narrow run (V <= 32) after the split chunk pass, <= kLocMaxGran granules
+        // (the decision keeps PM and SM in the digit pass's count array: G <= 8,192 granules for the
+        // 2,048-bin pass, <= 4,096 for the 512-bin one)
+        const bool loc = fast && st->V <= kNarrowMaxV && (sp.wide || g_pre_all.load()) && g_local.load() != 0 &&
+                         sp.nch * kGranPerChunk <= (size_t)(sp.wide ? kLocMaxGran : kLocMaxGran / 2);
+        loc_gsize = (uint32_t)((size_t)kRsWaves * 64u * (size_t)sp.rounds / kGranPerChunk);
         // never 0 (fresh scratch reads as "unsorted": the safe side); a stale epoch equal to
         // this one (2^32 calls later) also only costs the full sort
         // keys of 19-22 bits (2,048-bin digits) with the register-resident run kernel: the
@@ -2863,18 +3381,19 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true, 64, 1> : &k_sort_chunks<RR, false, 64, 1>),      \
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kc, vc, ah, \
-                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
+                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units)
             if (ri == 3) INA_A_DETECT(kR3 / 4);
             else if (ri == 2) INA_A_DETECT(kR2 / 4);
             else if (ri == 1) INA_A_DETECT(kR1 / 4);
             else INA_A_DETECT(kR0 / 4);
 #undef INA_A_DETECT
+
 #define INA_A_SORT(RR)                                                                                \
             hipLaunchKernelGGL((sp.wide ? (desc ? &k_sort_chunks<RR, true, kBinsBig, 2> : &k_sort_chunks<RR, false, kBinsBig, 2>) \
                                         : (desc ? &k_sort_chunks<RR, true, kRsBins, 2> : &k_sort_chunks<RR, false, kRsBins, 2>)), \
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
-                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
+                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units)
             if (ri == 3) INA_A_SORT(kR3 / 4);
             else if (ri == 2) INA_A_SORT(kR2 / 4);
             else if (ri == 1) INA_A_SORT(kR1 / 4);
@@ -2886,7 +3405,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                     : (desc ? &k_sort_chunks<RR, true, kRsBins> : &k_sort_chunks<RR, false, kRsBins>)), \
                            dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                            st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah,  \
-                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent)
+                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units)
         if (ri == 3) INA_A_LAUNCH(kR3 / 4);
         else if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
@@ -2918,6 +3437,12 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                dim3(kBkThr), 0, s, kn, vn, kc, vc, ax.hist, ax.rst, (uint32_t)sp.nch, CH, lb,
                                ax.nforeign, skip, ax.unsorted, epoch, fast ? 0 : 1,
                                (runs_on && !pre) ? ax.brk_cnt : nullptr, ax.brk_ent, (uint32_t)npk, pre ? 1 : 0);
+        if (do_sort && loc)
+            // the near-sorted path's per-slot lists into the idle k_out (exits at once unless the
+            // decision chose the path)
+            hipLaunchKernelGGL(k_local_lists, dim3((unsigned)std::min<size_t>(sp.nch * kGranPerChunk / kLocU, 2048)),
+                               dim3(kLlWaves * 64), 0, s, kc, npk, st->num_slots, ack_hint ? ~kAckBit : 0xFFFFFFFFu,
+                               ax.unsorted, ax.units, loc_gsize, k_out, ax.tab);
         if (pre) {                                 // the in-order run reads the arrival-order keys
             kn = kc;
             vn = nullptr;
@@ -2992,7 +3517,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                           : (ps.on ? (narrow ? &k_switch_run2<true, true, false> : &k_switch_run2<true, false, false>)
                                    : (narrow ? &k_switch_run2<false, true, false> : &k_switch_run2<false, false, false>));
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, pay, npk, stride, kc, vc, actions,
-                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted);
+                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted, k_out, ax.tab);
         *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
@@ -3143,10 +3668,15 @@ int ina_switch_batch_path(const void* scratch, size_t npk, uint32_t num_slots, i
         return set_error(INA_EINVAL, "bad arguments%s", "");
     const uint8_t* base = reinterpret_cast<const uint8_t*>(align_up((uintptr_t)scratch, 256));
     const SortAux ax = sort_aux(const_cast<uint8_t*>(base) + 4 * align_up(npk * 4, 256), npk, num_slots);
-    uint32_t e[3];
-    if (hipMemcpy(e, ax.unsorted, sizeof(e), hipMemcpyDeviceToHost) != hipSuccess)
+    uint32_t e[kLocEpoch + 1];
+    // the caller's stream may be a non-blocking one: wait for the whole device first
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(e, ax.unsorted, sizeof(e), hipMemcpyDeviceToHost) != hipSuccess)
         return set_error(INA_EHIP, "reading the control block%s", "");
-    *path = e[0] != e[1] ? INA_PATH_IN_ORDER : e[2] == e[1] ? INA_PATH_RUNS : INA_PATH_SORTED;
+    *path = e[kLocEpoch] == e[1] ? INA_PATH_LOCAL
+          : e[0] != e[1]        ? INA_PATH_IN_ORDER
+          : e[2] == e[1]        ? INA_PATH_RUNS
+                                : INA_PATH_SORTED;
     return INA_OK;
 }
 

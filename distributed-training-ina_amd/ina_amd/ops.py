@@ -749,7 +749,7 @@ class Switch:
         p = C.c_int(0)
         check(load().ina_switch_batch_path(self._scratch.data_ptr(), npk, self.num_slots, C.byref(p)),
               "switch_batch_path")
-        return {1: "in_order", 2: "runs", 3: "sorted"}[p.value]
+        return {1: "in_order", 2: "runs", 3: "sorted", 4: "local"}[p.value]
 
     def _scratch_for(self, npk, dev):
         need = load().ina_switch_scratch_bytes(npk, self.num_slots)
@@ -987,7 +987,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                switch_sort: int | None = None, switch_sort_rounds: int | None = None,
                ew_blocks: int | None = None, switch_tiny_max: int | None = None,
                host_zero_copy: bool | None = None, switch_bucket_tile: int | None = None,
-               switch_runs: bool | None = None, switch_pre_all: bool | None = None):
+               switch_runs: bool | None = None, switch_pre_all: bool | None = None,
+               switch_local: bool | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -1050,6 +1051,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(18, int(bool(switch_runs))), "set_tuning")
     if switch_pre_all is not None:
         check(lib.ina_set_tuning(19, int(bool(switch_pre_all))), "set_tuning")
+    if switch_local is not None:
+        check(lib.ina_set_tuning(20, int(bool(switch_local))), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

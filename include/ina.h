@@ -356,6 +356,7 @@ int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* p
 #define INA_PATH_IN_ORDER 1   /* already in slot order: no sort */
 #define INA_PATH_RUNS 2       /* at most 64 runs of consecutive slots: a run table, no sort */
 #define INA_PATH_SORTED 3     /* the bucket sort (or the LSD digit passes) */
+#define INA_PATH_LOCAL 4      /* near-sorted (local disorder, V <= 32): per-slot lists, no sort */
 int ina_switch_batch_path(const void* scratch, size_t npkts, uint32_t num_slots, int* path);
 
 /* The switch over split rows (hdr: 16-byte header rows, pay: 4V-byte payload rows, see

@@ -25,8 +25,15 @@ del packed
 order = os.environ.get("ORDER", "wm")           # wm: worker-major, rr: round-robin, random
 if order != "wm":
     npw = stream.shape[0] // W
-    perm = (torch.arange(W * npw, device=dev).view(W, npw).t().reshape(-1) if order == "rr"
-            else torch.randperm(W * npw, device=dev, generator=torch.Generator(device=dev).manual_seed(9)))
+    rr = torch.arange(W * npw, device=dev).view(W, npw).t().reshape(-1)
+    if order == "rr":
+        perm = rr
+    elif order.startswith("jit"):       # jitJ: round-robin, each packet displaced by < J positions
+        key = torch.arange(W * npw, device=dev) + torch.randint(
+            0, int(order[3:]), (W * npw,), device=dev, generator=torch.Generator(device=dev).manual_seed(9))
+        perm = rr[torch.sort(key, stable=True).indices]
+    else:
+        perm = torch.randperm(W * npw, device=dev, generator=torch.Generator(device=dev).manual_seed(9))
     stream, desc = stream[perm].contiguous(), desc[perm].contiguous()
 sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
 acts = torch.empty(stream.shape[0], dtype=torch.uint8, device=dev)
