@@ -49,6 +49,7 @@ with pinned H2D/D2H) to gpurun_out/bench_extra.json.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -794,23 +795,24 @@ def measure_e2e(dev, world=1, reps=5, warm=1, rank=0):
 
 
 # -- the whole INA packet path, steady state (SURVEY 8f-1 + 8f-2) ---------------------------
-def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1, split=False):
+def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1, split=False, V=V_SLOT, slots=1 << 17):
     """One step of the INA data path on one GPU, as a PS co-located with the switch runs it
     in steady state: 8 workers quantise their deltas (p_w - p_global, k=16) straight into
     NGA-256 packets (DataManager.py:37 + 111-165, fused), the PS's acks of the previous
     step ride in the same switch batch in front of the packets (fragcheck.p4:26-31), the
     switch aggregates every slot (ngaa.p4:120-196) and each completed slot's sum goes from
     the switch's registers straight into the PS update p_global + (1/(W+1)) * sum * 2^-k
-    (launch.py:46-50) and its ack row (ina_switch_process_apply).  Config-3 sizes: 8 x
+    (launch.py:46-50) and its ack row (ina_switch with a PS step).  Config-3 sizes: 8 x
     26,214,400 fp32, 102,400 slots.  HIP events around `steps` back-to-back steps; the
     roofline is the path's algorithmic bytes (packs, switch + PS, acks) over the step time.
     Parity: every worker packet completes its slot once, every ack frees one, and the
     update at a strided sample equals a numpy restatement bit for bit.
     split=True: the same step over split rows (include/ina.h: 16-byte header rows + aligned
     1 KiB payload rows, the same datagrams) -- ina_quantize_pack_nga_multi_split and
-    ina_switch_process_apply_split."""
+    ina_switch (split rows + PS step).  V=32, slots=2^20: the P4 program's own NGA-32 format
+    (headers.p4:40-73) at the same config-3 size, 8 x 819,200 packets + 819,200 acks."""
     from ina_amd import ops
-    W, n, V, k, slots = W_WORKERS, N_VALUES, V_SLOT, 16, 1 << 17
+    W, n, k = W_WORKERS, N_VALUES, 16
     npk = n // V
     g = torch.Generator(device=dev)
     g.manual_seed(6000 + rank)
@@ -895,11 +897,11 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1, split=False):
             + npk * rb + 8 * n + 16 * npk)                # PS fused: acks in, local + update, ack rows
     path = b_pack + b_sw
     res = {"workload": ("INA packet path, steady state, PS fused into the switch pass: 8 workers x "
-                        f"{n} fp32 -> quantise(p_w - p_global) + NGA-256 pack -> one switch batch of "
+                        f"{n} fp32 -> quantise(p_w - p_global) + NGA-{V} pack -> one switch batch of "
                         f"{npk} PS acks + {npk_all} worker packets -> completed slots applied to "
                         "p_global (launch.py:46-50) + ack rows"
-                        + (" -- split rows: 16-byte header rows + 1 KiB payload rows" if split else
-                           " -- packed rows: 15 + 1024 bytes in a 1,040-byte row")),
+                        + (f" -- split rows: 16-byte header rows + {4 * V}-byte payload rows" if split else
+                           f" -- packed rows: 15 + {4 * V} bytes in a {stride}-byte row")),
            "rows": "split" if split else "packed",
            "value": round(W * n * 4 / avg / 1e9, 2), "unit": "GB/s (worker fp32 bytes aggregated)",
            "ms_per_step": round(avg * 1e3, 3), "steps": steps, "warmup": warm,
@@ -916,6 +918,7 @@ def measure_packet_path(dev, steps=10, warm=3, rank=0, world=1, split=False):
                       "switch_and_ps": {"kernels": "k_sort_chunks, k_sort_buckets (finds 9 dense runs: "
                                                    "no sort), k_switch_run2<true> (writes the ack "
                                                    "rows and their descriptors)",
+                                        "batch_path": sw.batch_path((W + 1) * npk),
                                         "us": round(t_sw * 1e6, 1), "bytes": int(b_sw),
                                         "frac": round(b_sw / t_sw / 1e9 / HBM_PEAK_GBS, 4)},
                       "measures": "HIP events between the two phases of each step, medians"},
@@ -976,18 +979,32 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
     gperm.manual_seed(77 + rank)
     # worker_major_split: the worker-major batch in split rows (16-byte header rows + aligned
     # 4V-byte payload rows: the same datagrams, include/ina.h), the run table path
+    # round_robin_jitterJ: the round-robin arrival with local disorder -- every packet displaced
+    # by fewer than J positions (sort key = position + U[0, J)): W sequence-ordered senders
+    # (DataManager.py:116-134) interleaved by a NIC that reorders within a window (the
+    # near-sorted path: per-slot lists, no sort)
     rr = torch.arange(npk_all, device=dev).view(W, npk).t().reshape(-1)
-    order = {"worker_major": None,
-             "worker_major_split": None,
-             "round_robin": rr,
-             "round_robin_split": rr,
-             "worker_major_sorted": None,
-             "shuffled": torch.randperm(npk_all, device=dev, generator=gperm)}
+    shuf = torch.randperm(npk_all, device=dev, generator=gperm)
+
+    def jitter(J):
+        key = torch.arange(npk_all, device=dev) + torch.randint(0, J, (npk_all,), device=dev, generator=gperm)
+        return rr[torch.sort(key, stable=True).indices]
     if orders is None:                         # NGA-256 defaults: the split row layout once
         orders = ("worker_major", "worker_major_split", "round_robin", "worker_major_sorted", "shuffled")
-    for name in list(order):
-        if orders is not None and name not in orders:
-            del order[name]
+    order = {}
+    for name in orders:
+        base = name[:-len("_split")] if name.endswith("_split") else name
+        if base == "worker_major" or base == "worker_major_sorted":
+            order[name] = None
+        elif base == "round_robin":
+            order[name] = rr
+        elif base == "shuffled":
+            order[name] = shuf
+        elif base.startswith("round_robin_jitter"):
+            J = int(base[len("round_robin_jitter"):])
+            order[name] = order.get(base) if order.get(base) is not None else jitter(J)
+        else:
+            raise ValueError(f"unknown arrival order {name}")
     def split_rows(rows):
         h = torch.zeros((rows.shape[0], 16), dtype=torch.uint8, device=dev)
         h[:, :15] = rows[:, :15]
@@ -1027,51 +1044,93 @@ def measure_switch(dev, reps=10, warm=2, rank=0, world=1, V=V_SLOT, slots=1 << 1
             call = lambda: sw.process_split(hp, pp, acts, desc=ds)   # noqa: E731
         else:
             call = lambda: sw.process(st, acts, desc=ds)             # noqa: E731
-        ops.set_tuning(switch_runs=name != "worker_major_sorted")
-        for _ in range(warm):
-            call()
-        barrier(world)
-        # like the headline's avg_launch_us: one event pair around `reps` back-to-back calls
-        # (a pair per call adds ~7 us of event overhead, tools/lab/event_overhead_lab.py;
-        # reported beside it as us_event_pair_per_call)
-        per_rep = []
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            for _ in range(reps):
-                call()
-            e1.record(s)
-            torch.cuda.synchronize()
-            per_rep.append(e0.elapsed_time(e1) * 1e3 / reps)
-        evs = []
-        for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            call()
-            e1.record(s)
-            evs.append((e0, e1))
-        torch.cuda.synchronize()
-        us = max_over_ranks(statistics.median(per_rep), world)
-        us_pair = max_over_ranks(statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3, world)
-        done = int((acts == 1).sum())
-        res[name] = {"us": round(us, 2), "achieved_GBps": round(algo / us / 1e3, 1),
-                     "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
-                     "ok": all_ranks_true(done == npk, world), "us_event_pair_per_call": round(us_pair, 2),
-                     "batch_path": sw.batch_path(npk_all)}
-        if split:
-            res[name]["rows"] = "split: 16-byte header rows + 4V-byte payload rows"
-            del hp, pp
-        del st, ds, call
-        res[name]["parity_spot_check"] = all_ranks_true(parity(perm, split), world)
-        ops.set_tuning(switch_runs=True)
+        with _tuning(switch_runs=name != "worker_major_sorted"):
+            res[name] = _time_switch_order(call, sw, acts, npk, npk_all, algo, reps, warm, s, world)
+            if split:
+                res[name]["rows"] = "split: 16-byte header rows + 4V-byte payload rows"
+                del hp, pp
+            del st, ds, call
+            res[name]["parity_spot_check"] = all_ranks_true(parity(perm, split), world)
         if world > 1:
-            res[name]["aggregate_GBps"] = round(world * algo / us / 1e3, 1)
+            res[name]["aggregate_GBps"] = round(world * algo / res[name]["us"] / 1e3, 1)
+    for name in res:                           # the near-sorted legs beside the in-order one
+        if name.startswith("round_robin_jitter") and isinstance(res[name], dict):
+            ref = res.get("round_robin_split" if name.endswith("_split") else "round_robin")
+            if isinstance(ref, dict) and ref.get("us"):
+                res[name]["vs_round_robin"] = round(res[name]["us"] / ref["us"], 3)
+    tr = _switch_traffic(V)
+    for name, t in tr.items():
+        if isinstance(res.get(name), dict):
+            res[name]["traffic"] = t
     res["parity_sample"] = (f"{samp.size} slots (every 997th + the last): the completing packet's payload "
                             f"vs the numpy wrapping sum of the {W} workers' values, on a fresh switch "
                             f"in each arrival order; every slot completes exactly once")
     del stream, desc, sw, acts, pristine
     torch.cuda.empty_cache()
     return res
+
+
+@contextlib.contextmanager
+def _tuning(**kw):
+    """Process-wide switch tuning for one leg, restored to the defaults however the leg ends
+    (a leg that raises must not leave the later legs on a non-default path)."""
+    from ina_amd import ops
+    ops.set_tuning(**kw)
+    try:
+        yield
+    finally:
+        ops.set_tuning(**{k: True for k in kw})
+
+
+def _time_switch_order(call, sw, acts, npk, npk_all, algo, reps, warm, s, world):
+    """One arrival order of measure_switch: `warm` untimed calls, then HIP events on the launch
+    stream around `reps` back-to-back calls (3 passes, median) and a pair per call beside it."""
+    for _ in range(warm):
+        call()
+    barrier(world)
+    # like the headline's avg_launch_us: one event pair around `reps` back-to-back calls
+    # (a pair per call adds ~7 us of event overhead, tools/lab/event_overhead_lab.py;
+    # reported beside it as us_event_pair_per_call)
+    per_rep = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            call()
+        e1.record(s)
+        torch.cuda.synchronize()
+        per_rep.append(e0.elapsed_time(e1) * 1e3 / reps)
+    evs = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        call()
+        e1.record(s)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    us = max_over_ranks(statistics.median(per_rep), world)
+    us_pair = max_over_ranks(statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3, world)
+    done = int((acts == 1).sum())
+    return {"us": round(us, 2), "achieved_GBps": round(algo / us / 1e3, 1),
+            "frac": round(algo / us / 1e3 / HBM_PEAK_GBS, 4), "slots_completed": done,
+            "ok": all_ranks_true(done == npk, world), "us_event_pair_per_call": round(us_pair, 2),
+            "batch_path": sw.batch_path(npk_all)}
+
+
+def _switch_traffic(V):
+    """Committed PMC traffic of the run kernel per arrival order (profiles/traffic_switch_v<V>.json,
+    tools/switch_traffic.py: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over
+    tools/prof_switch.py, gfx950 corrections), or {} when none is committed."""
+    try:
+        doc = json.load(open(os.path.join(REPO, "profiles", f"traffic_switch_v{V}.json")))
+    except Exception:                     # noqa: BLE001 -- no file: traffic unmeasured
+        return {}
+    out = {}
+    for order, d in doc.get("orders", {}).items():
+        out[order] = {k: d[k] for k in ("kernel", "avg_us", "hbm_read_bytes", "hbm_write_bytes",
+                                         "algorithmic_bytes", "traffic_ratio") if k in d}
+        out[order]["source"] = doc.get("source", "")
+    return out
 
 
 # -- modes ---------------------------------------------------------------------------------------
@@ -1224,17 +1283,66 @@ def run_reduce(args, rank, world, dev, backend):
         # the P4 program's own format (headers.p4:40-73, parser.p4:43-55: NGA-32, 32 x bit<32>
         # behind the 15-byte header) at config-3 size: 6,553,600 packets, a 2^20-slot pool
         # (keys of 21 bits: the 2,048-bin chunk + bucket sort, and its run / in-order paths)
+        # near-sorted arrivals (round robin with local jitter, packed and split rows) beside the
+        # in-order round robin, and the shuffled batch in both layouts (the full sort)
         run_leg(line, "switch_c3_v32", lambda: measure_switch(dev, rank=rank, world=world, V=32, slots=1 << 20,
                                                               orders=("worker_major", "worker_major_split",
                                                                       "round_robin", "round_robin_split",
-                                                                      "shuffled")))
+                                                                      "round_robin_jitter64",
+                                                                      "round_robin_jitter64_split",
+                                                                      "round_robin_jitter4096",
+                                                                      "round_robin_jitter4096_split",
+                                                                      "shuffled", "shuffled_split")))
         # the INA step in the split-row layout (the device format: same datagrams on the wire,
         # aligned payload rows), and in packed 1,040-byte rows beside it
         run_leg(line, "packet_path", lambda: measure_packet_path(dev, rank=rank, world=world, split=True))
         run_leg(line, "packet_path_packed", lambda: measure_packet_path(dev, rank=rank, world=world))
+        # the same step in NGA-32 packets (the P4 program's format), split rows, 2^20 slots
+        run_leg(line, "packet_path_v32", lambda: measure_packet_path(dev, rank=rank, world=world, split=True,
+                                                                     V=32, slots=1 << 20))
     if cpu_in is not None:
         run_leg(line, "cpu_baseline", lambda: cpu_baseline(args, *cpu_in))
     return line
+
+
+def legs_summary(line: dict) -> dict:
+    """The JSON line's last key: one compact entry per leg -- us (per launch, call or step),
+    roofline frac, parity spot check (and the switch's batch path) -- so the whole run reads
+    at a glance; the full legs stay under their own keys."""
+    def one(d):
+        if not isinstance(d, dict):
+            return None
+        if "error" in d:
+            return {"error": d["error"][:120]}
+        rf = d.get("roofline") if isinstance(d.get("roofline"), dict) else {}
+        us = d.get("us") or rf.get("avg_launch_us") or (d["ms_per_step"] * 1e3 if d.get("ms_per_step") else None)
+        e = {"us": round(float(us), 1) if us else None, "frac": d.get("frac", rf.get("frac")),
+             "parity": d.get("parity_spot_check")}
+        if d.get("batch_path") or d.get("switch_batch_path"):
+            e["path"] = d.get("batch_path") or d.get("switch_batch_path")
+        return e
+    out = {"headline": one(line)}
+    for key in ("c2_fused", "c4_int16", "e2e_pcie", "sharded_c5", "packet_path", "packet_path_packed",
+                "packet_path_v32"):
+        if key in line:
+            out[key] = one(line[key])
+    c5 = line.get("sharded_c5")
+    if isinstance(c5, dict):
+        for sub in ("layout_b", "allreduce", "pipelined", "a2a"):
+            if isinstance(c5.get(sub), dict):
+                out[f"sharded_c5.{sub}"] = one(c5[sub])
+    for sw in ("switch_c3", "switch_c3_v32"):
+        d = line.get(sw)
+        if isinstance(d, dict) and "error" in d:
+            out[sw] = one(d)
+        elif isinstance(d, dict):
+            for k, v in d.items():
+                if isinstance(v, dict) and "us" in v:
+                    out[f"{sw}.{k}"] = one(v)
+    cb = line.get("cpu_baseline")
+    if isinstance(cb, dict):
+        out["cpu_baseline"] = {"value": cb.get("value"), "unit": cb.get("unit"), "parity": cb.get("matches_gpu")}
+    return out
 
 
 def run_leg(parent: dict, key: str, fn) -> dict:
@@ -1272,6 +1380,7 @@ def main():
             os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
             json.dump(extra, open(os.path.join(REPO, "gpurun_out", "bench_extra.json"), "w"), indent=1)
         if rank == 0:
+            line["legs"] = legs_summary(line)      # the last key
             print(json.dumps(line), flush=True)
     finally:
         if world > 1:

@@ -58,7 +58,14 @@ DEFAULTS = {"max_blocks": 16384, "reduce_blocks": 0, "stream_blocks": 16384, "co
 
 
 def _sweep(ops, rows, sweeps, name, knob, values, fn, nbytes):
-    """Time fn at each grid cap of one knob; keep all points, restore the default."""
+    """Time fn at each grid cap of one knob; keep all points, restore the default.  The grid-cap
+    knobs exist in lab builds only (make EXTRA=-DINA_LAB_KEYS=1): the product library refuses
+    them, and then only the default geometry is timed."""
+    try:
+        ops.set_tuning(**{knob: DEFAULTS[knob]})
+    except RuntimeError:
+        rows.append(_row(name, _time(fn), nbytes, note=f"default geometry ({knob}: lab builds only)"))
+        return
     best = None
     for v in values:
         ops.set_tuning(**{knob: v})
@@ -209,7 +216,7 @@ def run_extra(dev):
     rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; keys from descriptors)",
                      _time(lambda: sw.process(stream, acts, desc=desc_all), reps=5, warm=1), sw_bytes,
                      note="the pack kernels' 8-byte packet descriptors feed the slot sort "
-                          "(ina_switch_process_desc)"))
+                          "(ina_switch (descriptors))"))
     rows.append(_row("switch_process 8x NGA-256 (819,200 pkts, incl. slot sort; keys from headers)",
                      _time(lambda: sw.process(stream, acts), reps=5, warm=1), sw_bytes,
                      note="ina_switch_process: the key pass reads each packet's header line"))
@@ -297,7 +304,7 @@ def run_extra(dev):
                      t, path_bytes - npk * 6, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
                      acks_and_slots_ok=ok,
                      note="one switch batch per step: (W+1) x 102,400 packets; bytes as the row above"))
-    # the same with the PS on the switch's GPU: ina_switch_process_apply takes each completed
+    # the same with the PS on the switch's GPU: ina_switch with a PS step takes each completed
     # slot's sum from the switch's registers straight into the update and the ack row (the
     # completed packets are consumed, not written back)
     big.zero_()
@@ -319,7 +326,7 @@ def run_extra(dev):
     rows.append(_row("INA packet path step, steady state, PS fused into the switch pass",
                      t, fused_bytes, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
                      acks_and_slots_ok=ok,
-                     note="ina_switch_process_apply(keep_forwarded=0): bytes = the steady-state row's "
+                     note="ina_switch with a PS step(keep_forwarded=0): bytes = the steady-state row's "
                           "minus the PS's re-read of completed packets and their write-back"))
     # the same with the 8 worker packs as ONE launch (ina_quantize_pack_nga_multi: the
     # shared base is read once for the 8 workers) -- bench.py's packet_path leg
@@ -339,7 +346,7 @@ def run_extra(dev):
     rows.append(_row("INA packet path step, steady state, PS fused, the 8 worker packs in one launch",
                      t, fused_bytes - (Ws - 1) * n3 * 4, aggregated_GBps=round(Ws * n3 * 4 / t / 1e9, 2),
                      acks_and_slots_ok=ok,
-                     note="ina_quantize_pack_nga_multi + ina_switch_process_apply; bytes = the row above "
+                     note="ina_quantize_pack_nga_multi + ina_switch with a PS step; bytes = the row above "
                           "with the shared base read once"))
     # the same step recorded once as a hipGraph and replayed: the step's 15 launches (8
     # worker packs, the descriptor pass, the switch's 5 sort/run launches, ...) leave the

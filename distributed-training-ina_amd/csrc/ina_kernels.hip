@@ -1946,20 +1946,26 @@ extern "C" {
 const char* ina_version(void) { return "ina-mi355x 0.1 (gfx950)"; }
 const char* ina_last_error_string(void) { return g_err; }
 
+#ifndef INA_LAB_KEYS
+#define INA_LAB_KEYS 0
+#endif
 int ina_set_tuning(int key, int value) {
     switch (key) {
         case 0: if (value < 1) return INA_EINVAL; g_max_blocks = value; return INA_OK;
         case 1: if (value != 0 && value != 1 && value != 2 && value != 4) return INA_EINVAL; g_unroll = value; return INA_OK;
         case 2: g_nontemporal = value ? 1 : 0; return INA_OK;
         case 3: if (value < 0) return INA_EINVAL; g_reduce_blocks = value; return INA_OK;
+#if INA_LAB_KEYS
+        // grid-cap sweeps (bench_extra.py, tools/lab): lab builds only (make EXTRA=-DINA_LAB_KEYS=1)
         case 4: if (value < 1) return INA_EINVAL; g_stream_blocks = value; return INA_OK;
         case 14: if (value < 1) return INA_EINVAL; g_ew_blocks = value; return INA_OK;
         case 5: if (value < 1) return INA_EINVAL; g_combine_blocks = value; return INA_OK;
         case 6: if (value < 1) return INA_EINVAL; g_combine_ina_blocks = value; return INA_OK;
+        case 10: return set_switch_win(value);
+#endif
         case 7: return set_h2d_streams(value);
         case 8: if (value < 1) return INA_EINVAL; g_launch_chunks = value; return INA_OK;
         case 9: return set_small_sort(value);
-        case 10: return set_switch_win(value);
         case 11: return set_ack_fast(value);
         case 12: return set_sort_mode(value);
         case 13: return set_os_rounds(value);

@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <mutex>
+#include <unordered_map>
 
 #include "ina.h"
 #include "ina_internal.h"
@@ -576,6 +578,20 @@ int set_bucket_tile(int v) {
     return INA_OK;
 }
 
+// The switch keys one batch runs under, read ONCE per call.  A sort-only call (phase 1)
+// records its snapshot with the scratch it filled (g_sorts), and the run over that scratch
+// (phase 2) follows the record, never the live keys: a thread that tunes between another
+// thread's sort and run changes nothing in that batch (the run used to re-read
+// key 19 and pick arrays the sort never wrote).
+struct SwitchTuning {
+    int small_sort, tiny_max, sort_mode, os_rounds, runs, local, pre_all, ack_fast, win, bucket_tile;
+};
+static SwitchTuning switch_tuning() {
+    return SwitchTuning{g_small_sort.load(), g_tiny_max.load(), g_sort_mode.load(), g_os_rounds.load(),
+                        g_runs.load(),       g_local.load(),    g_pre_all.load(),   g_ack_fast.load(),
+                        g_switch_win.load(), g_bucket_tile.load()};
+}
+
 // key fields of R rounds of 64 packets (all loads issued first): slot index, switch id and
 // the PS-ack flag, from the batch's descriptors (header bytes 4..11) or the headers
 template <int R, bool kDesc>
@@ -791,6 +807,21 @@ __device__ __forceinline__ uint32_t wave_suffix_min(uint32_t x) {
     return x;
 }
 
+#ifndef INA_LOC_TIMING
+#define INA_LOC_TIMING 0
+#endif
+#if INA_LOC_TIMING
+// lab builds only: per-unit wall-clock stamps of k_local_lists' phases (tools/lab)
+__device__ unsigned long long g_loc_t[8192][4];
+#define LOC_STAMP(q) do { if (threadIdx.x == 0 && u < 8192) g_loc_t[u][q] = wall_clock64(); } while (0)
+// the decision pass: rows 8191 (block 0: entry, breaks summed, decided) and 8190 (the last
+// block: entry, verdict seen)
+#define DEC_STAMP(row, q) do { if (threadIdx.x == 0) g_loc_t[row][q] = wall_clock64(); } while (0)
+#else
+#define LOC_STAMP(q) do { } while (0)
+#define DEC_STAMP(row, q) do { } while (0)
+#endif
+
 // unit u: slots [lo, hi), window from granule g_lo to the unit's last granule
 struct LocUnit {
     uint32_t g_lo, lo, hi, pad;
@@ -806,23 +837,24 @@ __device__ __forceinline__ bool local_decide(const uint32_t* __restrict__ gmin, 
                                              uint32_t* s_sm, uint32_t* s_a, uint32_t* s_b) {
     __shared__ unsigned long long s_cost[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
-    // the bounds into LDS, coalesced (every load in flight at once)
+    // thread t: granules [g0, g0 + kpt), in registers (every load in flight at once) -- prefix
+    // max / suffix min inside the thread ...
+    constexpr int kGpt = kLocMaxGran / kBkThr;
+    const uint32_t kpt = (G + kBkThr - 1) / kBkThr;                   // <= kGpt
+    const uint32_t g0 = threadIdx.x * kpt;
+    uint32_t pm[kGpt], sm[kGpt];
 #pragma unroll
-    for (int j = 0; j < kLocMaxGran / kBkThr; ++j) {
-        const uint32_t g = threadIdx.x + (uint32_t)j * kBkThr;
-        if (g < G) {
-            s_pm[g] = gmax[g];
-            s_sm[g] = gmin[g];
-        }
+    for (int j = 0; j < kGpt; ++j) {
+        const uint32_t g = g0 + (uint32_t)j;
+        const bool ok = (uint32_t)j < kpt && g < G;
+        pm[j] = ok ? gmax[g] : 0u;
+        sm[j] = ok ? gmin[g] : 0xFFFFFFFFu;
     }
-    __syncthreads();
-    // thread t: granules [g0, g1) -- prefix max / suffix min inside the thread ...
-    const uint32_t kpt = (G + kBkThr - 1) / kBkThr;
-    const uint32_t g0 = min(threadIdx.x * kpt, G);
-    const uint32_t g1 = min(g0 + kpt, G);
     uint32_t tmax = 0, tmin = 0xFFFFFFFFu;
-    for (uint32_t g = g0; g < g1; ++g) s_pm[g] = tmax = max(tmax, s_pm[g]);
-    for (uint32_t g = g1; g-- > g0;) s_sm[g] = tmin = min(tmin, s_sm[g]);
+#pragma unroll
+    for (int j = 0; j < kGpt; ++j) pm[j] = tmax = max(tmax, pm[j]);
+#pragma unroll
+    for (int j = kGpt - 1; j >= 0; --j) sm[j] = tmin = min(tmin, sm[j]);
     // ... and over the threads: the max of the earlier ones, the min of the later ones
     const uint32_t imx = wave_incl_max(tmax), imn = wave_suffix_min(tmin);
     if (lane == 63) s_a[wv] = imx;
@@ -842,34 +874,50 @@ __device__ __forceinline__ bool local_decide(const uint32_t* __restrict__ gmin, 
         if (lane > 0) xmx = max(xmx, up);
         if (lane < 63) xmn = min(xmn, dn);
     }
-    for (uint32_t g = g0; g < g1; ++g) {
-        s_pm[g] = max(s_pm[g], xmx);
-        s_sm[g] = min(s_sm[g], xmn);
+#pragma unroll
+    for (int j = 0; j < kGpt; ++j) {
+        const uint32_t g = g0 + (uint32_t)j;
+        if ((uint32_t)j < kpt && g < G) {
+            s_pm[g] = max(pm[j], xmx);
+            s_sm[g] = min(sm[j], xmn);
+        }
     }
     __syncthreads();                                          // PM / SM final; s_a is reused
     if (kmin > kmax) return false;                            // no packet of this switch
-    // the units: slot range, window, scan cost (window x LDS passes)
-    const auto unit_of = [&](uint32_t u) {
+    DEC_STAMP(8189, 0);
+    // the units: slot range, window, scan cost (window x LDS passes).  Thread t takes units
+    // [t upt, (t+1) upt) and keeps them in registers: one binary search for g_lo of its first
+    // unit (PM is non-decreasing), then a short forward walk for the next (g_lo grows with u)
+    constexpr uint32_t kUpt = (kLocMaxGran / kLocU + kBkThr - 1) / kBkThr;
+    const uint32_t nu = (G + kLocU - 1) / kLocU;
+    const uint32_t upt = (nu + kBkThr - 1) / kBkThr;                  // <= kUpt (G <= kLocMaxGran)
+    LocUnit mu[kUpt];
+    unsigned long long cost = 0;
+    uint32_t maxwin = 0, glo = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kUpt; ++j) {
+        const uint32_t u = threadIdx.x * upt + j;
+        mu[j] = LocUnit{0u, 0u, 0u, 0u};
+        if (j >= upt || u >= nu) continue;
         const uint32_t a = s_sm[u * kLocU];
         const uint32_t b = (u + 1) * kLocU < G ? s_sm[(u + 1) * kLocU] : 0xFFFFFFFFu;
         const uint32_t lo = a == 0xFFFFFFFFu ? kmax + 1u : a, hi = b == 0xFFFFFFFFu ? kmax + 1u : b;
-        uint32_t l = 0, r = G;                                // g_lo: PM is non-decreasing
-        while (l < r) {
-            const uint32_t m = (l + r) >> 1;
-            if (s_pm[m] >= lo) r = m; else l = m + 1;
-        }
-        return LocUnit{l, lo, hi, 0u};
-    };
-    const uint32_t nu = (G + kLocU - 1) / kLocU;
-    unsigned long long cost = 0;
-    uint32_t maxwin = 0;
-    for (uint32_t u = threadIdx.x; u < nu; u += kBkThr) {
-        const LocUnit un = unit_of(u);
-        const size_t p0 = (size_t)un.g_lo * gsize, p1 = min((size_t)(u + 1) * kLocU * gsize, npk);
-        const uint32_t win = un.hi > un.lo && p1 > p0 ? (uint32_t)min(p1 - p0, (size_t)0xFFFFFFFFu) : 0u;
-        cost += (unsigned long long)((un.hi - un.lo + kLlBins - 1) / kLlBins) * win;
+        uint32_t l = glo, r = G;
+        if (j > 0)
+            for (int s = 0; s < 8 && l < r && s_pm[l] < lo; ++s) ++l;
+        if (l < r && s_pm[l] < lo)
+            while (l < r) {
+                const uint32_t m = (l + r) >> 1;
+                if (s_pm[m] >= lo) r = m; else l = m + 1;
+            }
+        glo = l;
+        mu[j] = LocUnit{l, lo, hi, 0u};
+        const size_t p0 = (size_t)l * gsize, p1 = min((size_t)(u + 1) * kLocU * gsize, npk);
+        const uint32_t win = hi > lo && p1 > p0 ? (uint32_t)min(p1 - p0, (size_t)0xFFFFFFFFu) : 0u;
+        cost += (unsigned long long)((hi - lo + kLlBins - 1) / kLlBins) * win;
         maxwin = max(maxwin, win);
     }
+    DEC_STAMP(8189, 1);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         cost += (unsigned long long)__shfl_xor((long long)cost, o);
@@ -887,9 +935,14 @@ __device__ __forceinline__ bool local_decide(const uint32_t* __restrict__ gmin, 
         total += s_cost[w];
         mw = max(mw, s_a[w]);
     }
+    DEC_STAMP(8189, 2);
     if (mw > kLocMaxWindow || total > (unsigned long long)kLocBeta * npk) return false;   // the sort
     if (writer) {
-        for (uint32_t u = threadIdx.x; u < nu; u += kBkThr) units[u] = unit_of(u);
+#pragma unroll
+        for (uint32_t j = 0; j < kUpt; ++j) {
+            const uint32_t u = threadIdx.x * upt + j;
+            if (j < upt && u < nu) units[u] = mu[j];
+        }
         if (threadIdx.x == 0) {
             unsorted[kLocKmin] = kmin;
             unsorted[kLocSlots] = kmax + 1u - kmin;
@@ -900,16 +953,6 @@ __device__ __forceinline__ bool local_decide(const uint32_t* __restrict__ gmin, 
     return true;
 }
 
-#ifndef INA_LOC_TIMING
-#define INA_LOC_TIMING 0
-#endif
-#if INA_LOC_TIMING
-// lab builds only: per-unit wall-clock stamps of k_local_lists' phases (tools/lab)
-__device__ unsigned long long g_loc_t[8192][4];
-#define LOC_STAMP(q) do { if (threadIdx.x == 0 && u < 8192) g_loc_t[u][q] = wall_clock64(); } while (0)
-#else
-#define LOC_STAMP(q) do { } while (0)
-#endif
 
 // The near-sorted path's lists (see local_decide): one kLlWaves-wave block per unit at a time
 // (units u = the block's XCD-ordered index + k * grid: neighbouring units, whose windows share
@@ -1184,6 +1227,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
     const uint32_t G = (uint32_t)nch * (uint32_t)kGranPerChunk;
     if constexpr (kMode == 2) {
         if (unsorted[0] != epoch) return;             // in slot order: no sort
+        if (c == 0) DEC_STAMP(8191, 0);
+        if (c == nch - 1) DEC_STAMP(8190, 0);
         if (brk_cnt) {
             // the decision after the detection pass: every block sums the chunks' break counts
             // (the same answer everywhere); a batch of at most kRunsMax dense runs gets its run
@@ -1211,6 +1256,7 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
             __shared__ uint32_t s_loc;
             unsigned long long* verdict = reinterpret_cast<unsigned long long*>(unsorted + kLocVerdict);
             if (c == 0) {
+                DEC_STAMP(8191, 1);
                 const bool loc = local_decide(gstat, gstat + G, G, (uint32_t)(kBkThr * R / kGranPerChunk), npk,
                                               unsorted, epoch, units, true, &base[0][0],
                                               &base[0][0] + sizeof(base) / 8, wtot, wbrk);
@@ -1219,11 +1265,13 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     s_loc = loc ? 1u : 0u;
                 }
+                DEC_STAMP(8191, 2);
             } else if (threadIdx.x == 0) {
                 unsigned long long v;
                 while (((v = __hip_atomic_load(verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) != epoch)
                     __builtin_amdgcn_s_sleep(8);
                 s_loc = (uint32_t)(v & 1ull);
+                if (c == nch - 1) DEC_STAMP(8190, 1);
             }
             __syncthreads();
             if (s_loc) return;
@@ -1862,7 +1910,7 @@ __device__ __forceinline__ uint32_t enc_lo(uint32_t prev, uint32_t v) {
 #endif
 }
 
-// PS co-located with the switch (ina_switch_process_apply): a completed slot's sum goes
+// PS co-located with the switch (ina_switch with a PS step): a completed slot's sum goes
 // straight from the VGPRs into the PS update out = local + ws * (sum * 2^-k) and the PS
 // ack row -- exactly what ina_apply_completed_nga computes from the forwarded packet.
 struct PsFuse {
@@ -1879,7 +1927,7 @@ struct PsFuse {
 
 // the run kernel's work for waves wave, wave + nwaves, ... (k_switch_run2: every wave of
 // the grid; k_switch_tiny: the 16 waves of its one workgroup)
-// kPs: PS update fused (ina_switch_process_apply); false costs nothing.  kLat (the
+// kPs: PS update fused (ina_switch with a PS step); false costs nothing.  kLat (the
 // one-launch tiny path, latency-bound): the slot's count and frag are read into SGPRs
 // only after the first batch's packet loads are issued, so a segment waits for one memory
 // round trip instead of three (no gain where the kernel is bandwidth-bound, and it costs
@@ -3112,7 +3160,7 @@ struct SortPlan {
     bool wide, bucket_ok;
 };
 
-static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
+static SortPlan sort_plan(size_t npk, uint32_t num_slots, const SwitchTuning& t) {
     SortPlan p;
     const int eb = end_bit_for(num_slots);
     p.passes = (eb + kRsMaxBits - 1) / kRsMaxBits;
@@ -3139,10 +3187,10 @@ static SortPlan sort_plan(size_t npk, uint32_t num_slots) {
     // structured arrival unchanged; at 819,200 NGA-256 packets (100 chunks) +2 %, so not
     // there (interleaved A/B, bytes equal, profiles/r04/lab/chunk_rounds32_ab_v*.log).  The
     // digit passes keep 4,096 (they never see this tier: bucket_ok, mode 0, <= 2,048 chunks)
-    if (npk > (size_t)INA_RS_BIG_ITEMS && p.bucket_ok && g_sort_mode.load() == 0 &&
+    if (npk > (size_t)INA_RS_BIG_ITEMS && p.bucket_ok && t.sort_mode == 0 &&
         npk <= (size_t)kBkMaxChunks * kRsWaves * 64 * INA_RS_ROUNDS_BIG)
         p.rounds = INA_RS_ROUNDS_BIG;
-    if (const int r = g_os_rounds.load()) p.rounds = r;   // ina_set_tuning key 13 (lab sweeps)
+    if (const int r = t.os_rounds) p.rounds = r;   // ina_set_tuning key 13 (the tests' tier cover)
     const size_t chunk = (size_t)kRsWaves * 64 * (size_t)p.rounds;
     p.nch = (npk + chunk - 1) / chunk;
     p.hist_elems = ((size_t)1 << std::max(p.bits, p.hbits)) * p.nch;
@@ -3176,7 +3224,7 @@ static size_t sort_nch_cap(size_t npk) {
 }
 
 static size_t sort_hist_cap(size_t npk, uint32_t num_slots) {
-    const SortPlan p = sort_plan(npk, num_slots);
+    const SortPlan p = sort_plan(npk, num_slots, SwitchTuning{});     // bits: no key changes them
     return ((size_t)1 << std::max(p.bits, p.hbits)) * sort_nch_cap(npk);
 }
 
@@ -3204,6 +3252,41 @@ static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
     a.units = reinterpret_cast<LocUnit*>(reinterpret_cast<uint8_t*>(a.gstat) + align_up(2 * nc * kGranPerChunk * 4, 256));
     a.tab = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(a.units) + align_up(nc * (kGranPerChunk / 2) * sizeof(LocUnit), 256));
     return a;
+}
+
+// The sorts queued alone (phase 1), by scratch: the switch keys they ran under and the batch
+// they sorted.  The run over that scratch (phase 2) takes its keys from here, and refuses a
+// scratch no sort of this batch filled; a sort + run call (phase 0) over the scratch drops its
+// record, since it overwrites what that sort left.
+struct SortRecord {
+    SwitchTuning t;
+    size_t npk, stride;
+    uint32_t num_slots;
+    int V;
+    bool split;
+};
+static std::mutex g_sorts_mu;
+static std::unordered_map<const void*, SortRecord> g_sorts;
+static std::atomic<size_t> g_sorts_n{0};
+
+static void sort_record_set(const void* scratch, bool keep, const SortRecord& r) {
+    if (!keep && g_sorts_n.load() == 0) return;               // nothing recorded anywhere
+    std::lock_guard<std::mutex> lk(g_sorts_mu);
+    if (keep) g_sorts[scratch] = r;
+    else g_sorts.erase(scratch);
+    g_sorts_n = g_sorts.size();
+}
+
+static bool sort_record_find(const void* scratch, const SortRecord& want, SwitchTuning* t) {
+    std::lock_guard<std::mutex> lk(g_sorts_mu);
+    const auto it = g_sorts.find(scratch);
+    if (it == g_sorts.end()) return false;
+    const SortRecord& r = it->second;
+    if (r.npk != want.npk || r.stride != want.stride || r.num_slots != want.num_slots || r.V != want.V ||
+        r.split != want.split)
+        return false;
+    *t = r.t;
+    return true;
 }
 
 }  // namespace ina
@@ -3293,6 +3376,18 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         return set_error(INA_EINVAL, "null pointer%s", "");
     if (desc && ((uintptr_t)desc & 7u))
         return set_error(INA_EINVAL, "descriptors must be 8-byte aligned%s", "");
+    // the switch keys of this batch: read once here, or (a run alone) its sort's record
+    SwitchTuning t;
+    {
+        const SortRecord rec{SwitchTuning{}, npk, stride, st->num_slots, st->V, split};
+        if (phase == 2) {
+            if (!sort_record_find(scratch, rec, &t))
+                return set_error(INA_EINVAL, "run alone: no sort of this batch was queued into this scratch%s", "");
+        } else {
+            t = switch_tuning();
+            sort_record_set(scratch, phase == 1, SortRecord{t, npk, stride, st->num_slots, st->V, split});
+        }
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     uint8_t* base = reinterpret_cast<uint8_t*>(align_up((uintptr_t)scratch, 256));
     size_t arr = align_up(npk * 4, 256);
@@ -3300,7 +3395,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     uint32_t* k_out = reinterpret_cast<uint32_t*>(base + arr);
     uint32_t* v_in = reinterpret_cast<uint32_t*>(base + 2 * arr);
     uint32_t* v_out = reinterpret_cast<uint32_t*>(base + 3 * arr);
-    const SortPlan sp = sort_plan(npk, st->num_slots);
+    const SortPlan sp = sort_plan(npk, st->num_slots, t);
     const SortAux ax = sort_aux(base + 4 * arr, npk, st->num_slots);
     // sort chunk geometry (sort_plan): one instantiation per rounds-per-wave choice
     constexpr int kR0 = INA_RS_ROUNDS_SMALL, kR1 = INA_RS_ROUNDS_MID, kR2 = kRsRounds, kR3 = INA_RS_ROUNDS_BIG;
@@ -3314,20 +3409,20 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                       st->V <= kMaxV && ((uintptr_t)st->regs & 15u) == 0;
     if (split && !fast) return set_error(INA_EINVAL, "split rows need 16-byte aligned rows and registers%s", "");
     // keys carry the PS-ack bit for the run kernel when bit 31 is outside every digit
-    const bool ack_hint = fast && sp.passes * sp.bits <= 31 && g_ack_fast.load();
-    const bool small = npk <= (size_t)g_small_sort.load();
+    const bool ack_hint = fast && sp.passes * sp.bits <= 31 && t.ack_fast;
+    const bool small = npk <= (size_t)t.small_sort;
     // chunk + bucket sort: keys of one or two digits (the low digit is one workgroup's LDS
     // bins) and at most kBkMaxChunks chunks (B's LDS rows); else the digit passes
-    const bool bucket = !small && g_sort_mode.load() == 0 && sp.bucket_ok && sp.nch <= (size_t)kBkMaxChunks;
+    const bool bucket = !small && t.sort_mode == 0 && sp.bucket_ok && sp.nch <= (size_t)kBkMaxChunks;
     const uint32_t* nforeign = nullptr;
     const uint32_t* unsorted = nullptr;     // bucket sort: the run kernel may read A's output
     uint32_t epoch = 0;
     uint32_t loc_gsize = 0;                 // the near-sorted path's granule: 1/8 of a sort chunk
-    if (small && fast && npk <= (size_t)g_tiny_max.load()) {
+    if (small && fast && npk <= (size_t)t.tiny_max) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
         if (!do_run) return INA_OK;
         uint32_t win = (uint32_t)INA_SWITCH_WIN_SMALL;
-        if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
+        if (const int wv = t.win) win = (uint32_t)wv;
         const bool narrow = (uint64_t)st->num_slots + 1 <= (1u << 20);
 #define INA_TINY(P_, T_, B_, S_) hipLaunchKernelGGL((k_switch_tiny<P_, T_, B_, S_>), dim3(1), dim3(kSmallBlock), 0, s, \
                                                    *st, pkts, pay, (uint32_t)npk, stride, actions, win, ps)
@@ -3360,19 +3455,19 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const int ah = ack_hint ? 1 : 0;
         // dense ascending runs skip the sort (run table, switch_runs_body): the register-
         // resident run kernel only (ina_set_tuning key 18 = 0 turns it off)
-        const bool runs_on = fast && g_runs.load() != 0;
+        const bool runs_on = fast && t.runs != 0;
         // near-sorted batches (local disorder) skip the sort and run from per-slot lists: the
         // narrow run (V <= 32) after the split chunk pass, <= kLocMaxGran granules
         // (the decision keeps PM and SM in the digit pass's count array: G <= 8,192 granules for the
         // 2,048-bin pass, <= 4,096 for the 512-bin one)
-        const bool loc = fast && st->V <= kNarrowMaxV && (sp.wide || g_pre_all.load()) && g_local.load() != 0 &&
+        const bool loc = fast && st->V <= kNarrowMaxV && (sp.wide || t.pre_all) && t.local != 0 &&
                          sp.nch * kGranPerChunk <= (size_t)(sp.wide ? kLocMaxGran : kLocMaxGran / 2);
         loc_gsize = (uint32_t)((size_t)kRsWaves * 64u * (size_t)sp.rounds / kGranPerChunk);
         // never 0 (fresh scratch reads as "unsorted": the safe side); a stale epoch equal to
         // this one (2^32 calls later) also only costs the full sort
         // keys of 19-22 bits (2,048-bin digits) with the register-resident run kernel: the
         // chunk pass split in two (detection, then decision + digits), so structured batches skip the digits
-        const bool pre = (sp.wide || g_pre_all.load()) && fast;
+        const bool pre = (sp.wide || t.pre_all) && fast;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
@@ -3425,7 +3520,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // buckets past the sentinel's (num_slots >> lb) are always empty: no block for them,
         // so at 2^17 slots 257 blocks (one per CU, one generation) instead of 512
         const unsigned gb = std::min<unsigned>(1u << sp.hbits, (st->num_slots >> lb) + 1u);
-        const int tile = g_bucket_tile.load();
+        const int tile = t.bucket_tile;
         const bool big = tile == kLcRoundsBig || (tile == 0 && npk > (size_t)gb * kBigTileAvg);
         if (do_sort)
             // the bucket pass's bins follow the low digit: 1,024 for keys of 19-21 bits (three
@@ -3509,7 +3604,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // a narrow wave moves a whole segment per batch: a window of 64 sorted positions
         // (about 8 segments) keeps the grid at npk / 256 workgroups
         if (narrow && (INA_SWITCH_NARROW_SLOTS || npk > 65536)) win = 64;   // 8 lane groups: ~8 segments
-        if (const int wv = g_switch_win.load()) win = (uint32_t)wv;
+        if (const int wv = t.win) win = (uint32_t)wv;
         const size_t per_block = (size_t)win * (kSwBlock / 64);
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
         auto* run = split ? (ps.on ? (narrow ? &k_switch_run2<true, true, true> : &k_switch_run2<true, false, true>)
@@ -3526,85 +3621,6 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     }
     if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch run launch%s", "");
     return INA_OK;
-}
-
-int ina_switch_process_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                            const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                            ina_stream_t stream) {
-    PsFuse off{};
-    bool fused = false;
-    return switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, off, &fused);
-}
-
-int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                       uint8_t* actions, void* scratch, ina_stream_t stream) {
-    return ina_switch_process_desc(st, pkts, npk, stride, nullptr, actions, scratch, stream);
-}
-
-int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                             uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
-                             double weight_step, float* out, size_t n, uint8_t* acks,
-                             size_t ack_stride, int keep_forwarded, ina_stream_t stream) {
-    return ina_switch_process_apply_desc(st, pkts, npk, stride, nullptr, actions, scratch, seq0, local, k,
-                                         weight_step, out, n, acks, ack_stride, keep_forwarded, stream);
-}
-
-static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                             const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                             uint32_t seq0, const float* local, int k, double weight_step,
-                             float* out, size_t n, uint8_t* acks, size_t ack_stride,
-                             ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream, int phase,
-                             uint8_t* pay = nullptr);
-
-int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                                  const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                                  uint32_t seq0, const float* local, int k, double weight_step,
-                                  float* out, size_t n, uint8_t* acks, size_t ack_stride,
-                                  int keep_forwarded, ina_stream_t stream) {
-    return switch_apply_impl(st, pkts, npk, stride, desc, actions, scratch, seq0, local, k, weight_step,
-                             out, n, acks, ack_stride, nullptr, keep_forwarded, stream, 0);
-}
-
-int ina_switch_process_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                                     const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                                     uint32_t seq0, const float* local, int k, double weight_step,
-                                     float* out, size_t n, uint8_t* acks, size_t ack_stride,
-                                     ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream) {
-    return switch_apply_impl(st, pkts, npk, stride, desc, actions, scratch, seq0, local, k, weight_step,
-                             out, n, acks, ack_stride, ack_desc, keep_forwarded, stream, 0);
-}
-
-int ina_switch_sort_desc(const ina_switch_state_t* st, const uint8_t* pkts, size_t npk, size_t stride,
-                         const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                         ina_stream_t stream) {
-    PsFuse off{};
-    bool fused = false;
-    return switch_process_impl(st, const_cast<uint8_t*>(pkts), npk, stride, desc, actions, scratch, stream,
-                               off, &fused, 1);
-}
-
-int ina_switch_run_sorted(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                          uint8_t* actions, void* scratch, ina_stream_t stream) {
-    PsFuse off{};
-    bool fused = false;
-    return switch_process_impl(st, pkts, npk, stride, nullptr, actions, scratch, stream, off, &fused, 2);
-}
-
-int ina_switch_run_sorted_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                                uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
-                                double weight_step, float* out, size_t n, uint8_t* acks,
-                                size_t ack_stride, int keep_forwarded, ina_stream_t stream) {
-    return switch_apply_impl(st, pkts, npk, stride, nullptr, actions, scratch, seq0, local, k, weight_step,
-                             out, n, acks, ack_stride, nullptr, keep_forwarded, stream, 2);
-}
-
-int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
-                                        uint8_t* actions, void* scratch, uint32_t seq0, const float* local,
-                                        int k, double weight_step, float* out, size_t n, uint8_t* acks,
-                                        size_t ack_stride, ina_nga_desc_t* ack_desc, int keep_forwarded,
-                                        ina_stream_t stream) {
-    return switch_apply_impl(st, pkts, npk, stride, nullptr, actions, scratch, seq0, local, k, weight_step,
-                             out, n, acks, ack_stride, ack_desc, keep_forwarded, stream, 2);
 }
 
 static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
@@ -3628,7 +3644,7 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
     // rather than after, so keep_forwarded always means what include/ina.h says
     if (st->V % 4 || st->V > 256 || stride % 16 || ((uintptr_t)pkts & 15u) || ((uintptr_t)st->regs & 15u))
         return set_error(INA_EINVAL,
-                         "process_apply needs V %% 4 == 0 <= 256 and 16-byte aligned rows and registers%s", "");
+                         "the PS step needs V %% 4 == 0 <= 256 and 16-byte aligned rows and registers%s", "");
     const size_t nslots = (n + (size_t)st->V - 1) / (size_t)st->V;
     PsFuse ps{local, out, n, ldexpf(1.0f, -k), (float)weight_step, seq0,
               nslots > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)nslots, acks, ack_stride, 1,
@@ -3636,7 +3652,7 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
     bool fused = false;
     if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused, phase, pay))
         return rc;
-    if (fused) return INA_OK;
+    if (fused || phase == INA_SWITCH_SORT) return INA_OK;         // (a sort alone: the PS step runs with the run)
     if (pay) return set_error(INA_EHIP, "split rows: the PS step was not fused%s", "");
     // layouts the register-resident run kernel does not take: the two steps one by one
     if (int rc = ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,
@@ -3645,22 +3661,31 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
     return ack_desc ? ina_nga_descriptors(acks, nslots, ack_stride, ack_desc, stream) : INA_OK;
 }
 
-int ina_switch_process_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npk,
-                             const ina_nga_desc_t* desc, uint8_t* actions, void* scratch, ina_stream_t stream) {
-    if (npk && !pay) return set_error(INA_EINVAL, "null payload rows%s", "");
+int ina_switch(const ina_switch_state_t* st, const ina_switch_batch_t* b, const ina_switch_ps_t* ps, int phase,
+               ina_stream_t stream) {
+    if (!b) return set_error(INA_EINVAL, "null batch%s", "");
+    if (phase != INA_SWITCH_ALL && phase != INA_SWITCH_SORT && phase != INA_SWITCH_RUN)
+        return set_error(INA_EINVAL, "phase must be INA_SWITCH_ALL, _SORT or _RUN%s", "");
+    const bool split = b->pay != nullptr;
+    const size_t stride = split ? 16 : b->stride;
+    if (ps) {
+        if (split && ps->ack_stride != 16 && ps->ack_stride != 0)
+            return set_error(INA_EINVAL, "split rows: the ack rows are header rows (ack_stride 16)%s", "");
+        return switch_apply_impl(st, b->rows, b->npkts, stride, b->desc, b->actions, b->scratch, ps->seq0,
+                                 ps->local, ps->k, ps->weight_step, ps->out, ps->n, ps->acks,
+                                 split ? 16 : ps->ack_stride, ps->ack_desc, ps->keep_forwarded, stream, phase,
+                                 b->pay);
+    }
     PsFuse off{};
     bool fused = false;
-    return switch_process_impl(st, hdr, npk, 16, desc, actions, scratch, stream, off, &fused, 0, pay);
+    return switch_process_impl(st, b->rows, b->npkts, stride, b->desc, b->actions, b->scratch, stream, off, &fused,
+                               phase, b->pay);
 }
 
-int ina_switch_process_apply_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npk,
-                                   const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                                   uint32_t seq0, const float* local, int k, double weight_step,
-                                   float* out, size_t n, uint8_t* ack_hdr, ina_nga_desc_t* ack_desc,
-                                   int keep_forwarded, ina_stream_t stream) {
-    if (npk && !pay) return set_error(INA_EINVAL, "null payload rows%s", "");
-    return switch_apply_impl(st, hdr, npk, 16, desc, actions, scratch, seq0, local, k, weight_step, out, n,
-                             ack_hdr, 16, ack_desc, keep_forwarded, stream, 0, pay);
+int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,
+                       uint8_t* actions, void* scratch, ina_stream_t stream) {
+    const ina_switch_batch_t b{pkts, nullptr, npk, stride, nullptr, actions, scratch};
+    return ina_switch(st, &b, nullptr, INA_SWITCH_ALL, stream);
 }
 
 int ina_switch_batch_path(const void* scratch, size_t npk, uint32_t num_slots, int* path) {

@@ -48,6 +48,20 @@ class SwitchState(C.Structure):
                 ("count", C.c_void_p), ("frag", C.c_void_p), ("regs", C.c_void_p)]
 
 
+class SwitchBatch(C.Structure):          # include/ina.h ina_switch_batch_t
+    _fields_ = [("rows", C.c_void_p), ("pay", C.c_void_p), ("npkts", C.c_size_t), ("stride", C.c_size_t),
+                ("desc", C.c_void_p), ("actions", C.c_void_p), ("scratch", C.c_void_p)]
+
+
+class SwitchPs(C.Structure):             # include/ina.h ina_switch_ps_t
+    _fields_ = [("seq0", C.c_uint32), ("k", C.c_int), ("weight_step", C.c_double), ("local", C.c_void_p),
+                ("out", C.c_void_p), ("n", C.c_size_t), ("acks", C.c_void_p), ("ack_stride", C.c_size_t),
+                ("ack_desc", C.c_void_p), ("keep_forwarded", C.c_int)]
+
+
+INA_SWITCH_ALL, INA_SWITCH_SORT, INA_SWITCH_RUN = 0, 1, 2
+
+
 # exported symbol -> argtypes (restype int unless listed in _RESTYPE)
 _vp, _sz, _i, _u32, _d = C.c_void_p, C.c_size_t, C.c_int, C.c_uint32, C.c_double
 SIGNATURES = {
@@ -74,33 +88,18 @@ SIGNATURES = {
     "ina_nga_descriptors": [_vp, _sz, _sz, _vp, _vp],
     "ina_quantize_pack_nga_multi": [_vp, _i, _vp, _sz, _i, _vp, _vp, _sz, _vp, _vp],
     "ina_nga_make_descriptors": [_vp, _i, _sz, _vp, _vp],
-    "ina_switch_sort_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _vp],
-    "ina_switch_run_sorted": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
-    "ina_switch_run_sorted_apply": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i, _d,
-                                    _vp, _sz, _vp, _sz, _i, _vp],
     "ina_unpack_nga": [_vp, _sz, _i, _sz, C.POINTER(NgaFields), _vp, _vp],
     "ina_pack_c128": [_vp, _i, _i, _u32, _i, _vp, _vp],
     "ina_apply_completed_nga": [_vp, _sz, _i, _sz, _vp, _u32, _vp, _i, _d, _vp, _sz, _vp, _sz, _vp],
     "ina_pack_nga_split": [_vp, _sz, C.POINTER(NgaParams), _vp, _vp, _vp, _vp, _vp],
     "ina_quantize_pack_nga_multi_split": [_vp, _i, _vp, _sz, _i, _vp, _vp, _vp, _vp, _vp],
     "ina_unpack_nga_split": [_vp, _vp, _sz, _i, C.POINTER(NgaFields), _vp, _vp],
-    "ina_switch_process_split": [C.POINTER(SwitchState), _vp, _vp, _sz, _vp, _vp, _vp, _vp],
-    "ina_switch_process_apply_split": [C.POINTER(SwitchState), _vp, _vp, _sz, _vp, _vp, _vp, _u32, _vp, _i,
-                                       _d, _vp, _sz, _vp, _vp, _i, _vp],
     "ina_send_packets_split_fd": [_i, _vp, _vp, _sz, _i, _u32],
     "ina_recv_packets_split_fd": [_i, _vp, _vp, _sz, _i, _sz, _i, _vp],
     "ina_switch_scratch_bytes": [_sz, _u32],
     "ina_switch_batch_path": [_vp, _sz, _u32, C.POINTER(C.c_int)],
     "ina_switch_process": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp],
-    "ina_switch_process_apply": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i, _d,
-                                 _vp, _sz, _vp, _sz, _i, _vp],
-    "ina_switch_process_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _vp],
-    "ina_switch_process_apply_ackdesc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _u32, _vp,
-                                         _i, _d, _vp, _sz, _vp, _sz, _vp, _i, _vp],
-    "ina_switch_run_sorted_apply_ackdesc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _u32, _vp, _i,
-                                            _d, _vp, _sz, _vp, _sz, _vp, _i, _vp],
-    "ina_switch_process_apply_desc": [C.POINTER(SwitchState), _vp, _sz, _sz, _vp, _vp, _vp, _u32, _vp,
-                                      _i, _d, _vp, _sz, _vp, _sz, _i, _vp],
+    "ina_switch": [C.POINTER(SwitchState), C.POINTER(SwitchBatch), C.POINTER(SwitchPs), _i, _vp],
     "ina_route_ipv4": [_vp, _vp, _u32, _sz, _vp, _vp, _i, _vp, _vp],
     "ina_checksum_i32": [_vp, _sz, _vp, _vp],
     "ina_absmax_f32": [_vp, _vp, _sz, _vp, _vp],

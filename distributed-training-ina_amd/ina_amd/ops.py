@@ -711,6 +711,21 @@ class Switch:
         self._done.record(ts)
         self._done_stream = ts.cuda_stream
 
+    def _call(self, ts, rows, pay, npk, stride, d, actions, scratch, phase, ps=None, what="switch"):
+        """One ina_switch call (include/ina.h): the batch struct, the PS step (or None), the
+        phase -- ordered after the previous call on this switch's scratch."""
+        b = _lib.SwitchBatch(rows.data_ptr(), pay.data_ptr() if pay is not None else None, npk, stride,
+                             d.data_ptr() if d is not None else None, actions.data_ptr(), scratch.data_ptr())
+        st = self._begin(ts)
+        check(load().ina_switch(C.byref(self._state), C.byref(b), C.byref(ps) if ps is not None else None,
+                                phase, st), what)
+        self._end(ts)
+
+    @staticmethod
+    def _ps(seq0, local, k, weight_step, out, ack_ptr, ack_stride, ack_desc_ptr, keep_forwarded):
+        return _lib.SwitchPs(seq0 & 0xFFFFFFFF, k, weight_step, local.data_ptr(), out.data_ptr(), local.numel(),
+                             ack_ptr, ack_stride, ack_desc_ptr, int(keep_forwarded))
+
     def process(self, pkts: torch.Tensor, actions: torch.Tensor | None = None,
                 desc: torch.Tensor | None = None) -> torch.Tensor:
         """Runs packets (uint8 [npkts, stride], arrival order) through the switch in place;
@@ -729,20 +744,15 @@ class Switch:
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
         self._sorted = None                       # the scratch is reused below
-        ts = torch.cuda.current_stream(pkts.device)
-        st = self._begin(ts)
-        check(load().ina_switch_process_desc(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                             d.data_ptr() if d is not None else None,
-                                             actions.data_ptr(), self._scratch.data_ptr(),
-                                             st), "switch_process")
-        self._end(ts)
+        self._call(torch.cuda.current_stream(pkts.device), pkts, None, npk, stride, d, actions, self._scratch,
+                   _lib.INA_SWITCH_ALL, what="switch_process")
         return actions
 
     def batch_path(self, npk: int) -> str:
         """Which slot-sort path the last call over this switch's scratch took for its batch of
         npk packets (batches past the one-workgroup small-batch paths): "in_order" (no sort),
-        "runs" (dense ascending runs, no sort) or "sorted" (the bucket sort or the LSD digit
-        passes).  Synchronises the device (a diagnostic)."""
+        "runs" (dense ascending runs, no sort), "local" (near-sorted: per-slot lists, no sort)
+        or "sorted" (the bucket sort or the LSD digit passes).  Synchronises the device (a diagnostic)."""
         if self._scratch is None:
             raise ValueError("no batch has run on this switch")
         torch.cuda.synchronize(self._scratch.device)
@@ -759,7 +769,7 @@ class Switch:
 
     def sort(self, pkts: torch.Tensor, desc: torch.Tensor, actions: torch.Tensor | None = None,
              stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-        """The slot sort of process(pkts, desc=desc) alone (ina_switch_sort_desc): it reads
+        """The slot sort of process(pkts, desc=desc) alone (ina_switch, INA_SWITCH_SORT): it reads
         only the descriptors, so it may be queued before -- or on `stream`, beside -- the
         kernels still filling pkts' payload; run() / run_apply() finish the batch over the
         same scratch (the scratch is this switch's, one batch at a time).  Every call on this
@@ -779,10 +789,7 @@ class Switch:
         ts = stream if stream is not None else torch.cuda.current_stream(pkts.device)
         if stream is not None:
             scratch.record_stream(stream)        # in use there until run() joins it
-        st = self._begin(ts)
-        check(load().ina_switch_sort_desc(C.byref(self._state), pkts.data_ptr(), npk, stride, d.data_ptr(),
-                                          actions.data_ptr(), scratch.data_ptr(), st), "switch_sort")
-        self._end(ts)
+        self._call(ts, pkts, None, npk, stride, d, actions, scratch, _lib.INA_SWITCH_SORT, what="switch_sort")
         self._sorted = (pkts.data_ptr(), npk, stride, actions.data_ptr(), scratch.data_ptr())
         self._sorted_desc = d
         return actions
@@ -819,12 +826,8 @@ class Switch:
         _fits(actions, npk, "actions")
         _same_device(pkts, actions)
         scratch = self._take_sorted(pkts, actions)
-        ts = torch.cuda.current_stream(pkts.device)
-        st = self._begin(ts)
-        check(load().ina_switch_run_sorted(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                           actions.data_ptr(), scratch.data_ptr(), st),
-              "switch_run_sorted")
-        self._end(ts)
+        self._call(torch.cuda.current_stream(pkts.device), pkts, None, npk, stride, None, actions, scratch,
+                   _lib.INA_SWITCH_RUN, what="switch_run")
         return actions
 
     def run_apply(self, pkts: torch.Tensor, actions: torch.Tensor, seq0: int, local: torch.Tensor,
@@ -842,15 +845,9 @@ class Switch:
         ack_ptr, ack_stride = (acks.data_ptr(), acks.shape[1]) if acks is not None else (None, 0)
         ad = _ack_desc_arg(ack_desc, acks)
         scratch = self._take_sorted(pkts, actions)
-        ts = torch.cuda.current_stream(pkts.device)
-        st = self._begin(ts)
-        check(load().ina_switch_run_sorted_apply_ackdesc(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                                         actions.data_ptr(), scratch.data_ptr(),
-                                                         seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
-                                                         out.data_ptr(), local.numel(), ack_ptr, ack_stride,
-                                                         ad, int(keep_forwarded), st),
-              "switch_run_sorted_apply")
-        self._end(ts)
+        self._call(torch.cuda.current_stream(pkts.device), pkts, None, npk, stride, None, actions, scratch,
+                   _lib.INA_SWITCH_RUN, self._ps(seq0, local, k, weight_step, out, ack_ptr, ack_stride, ad,
+                                                 keep_forwarded), what="switch_run_apply")
         return actions, out
 
     def process_apply(self, pkts: torch.Tensor, seq0: int, local: torch.Tensor, k: int,
@@ -879,23 +876,16 @@ class Switch:
         if self._scratch is None or self._scratch.numel() < need:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=pkts.device)
         self._sorted = None
-        ts = torch.cuda.current_stream(pkts.device)
-        st = self._begin(ts)
         ad = _ack_desc_arg(ack_desc, acks)
-        check(load().ina_switch_process_apply_ackdesc(C.byref(self._state), pkts.data_ptr(), npk, stride,
-                                                      d.data_ptr() if d is not None else None,
-                                                      actions.data_ptr(), self._scratch.data_ptr(),
-                                                      seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
-                                                      out.data_ptr(), local.numel(), ack_ptr, ack_stride,
-                                                      ad, int(keep_forwarded), st),
-              "switch_process_apply")
-        self._end(ts)
+        self._call(torch.cuda.current_stream(pkts.device), pkts, None, npk, stride, d, actions, self._scratch,
+                   _lib.INA_SWITCH_ALL, self._ps(seq0, local, k, weight_step, out, ack_ptr, ack_stride, ad,
+                                                 keep_forwarded), what="switch_process_apply")
         return actions, out
 
 
     def process_split(self, hdr: torch.Tensor, pay: torch.Tensor, actions: torch.Tensor | None = None,
                       desc: torch.Tensor | None = None) -> torch.Tensor:
-        """process() over split rows (ina_switch_process_split): header rows uint8 [npkts, 16]
+        """process() over split rows (ina_switch, batch.pay set): header rows uint8 [npkts, 16]
         and payload rows uint8 [npkts, 4V]; same actions, registers and forwarded bytes."""
         npk = hdr.shape[0]
         hdr, pay = _split_rows(npk, self.V, hdr.device, hdr, pay)
@@ -906,12 +896,8 @@ class Switch:
         _same_device(hdr, pay, actions)
         scratch = self._scratch_for(npk, hdr.device)
         self._sorted = None
-        ts = torch.cuda.current_stream(hdr.device)
-        st = self._begin(ts)
-        check(load().ina_switch_process_split(C.byref(self._state), hdr.data_ptr(), pay.data_ptr(), npk,
-                                              d.data_ptr() if d is not None else None, actions.data_ptr(),
-                                              scratch.data_ptr(), st), "switch_process_split")
-        self._end(ts)
+        self._call(torch.cuda.current_stream(hdr.device), hdr, pay, npk, 16, d, actions, scratch,
+                   _lib.INA_SWITCH_ALL, what="switch_process_split")
         return actions
 
     def process_apply_split(self, hdr: torch.Tensor, pay: torch.Tensor, seq0: int, local: torch.Tensor,
@@ -919,7 +905,7 @@ class Switch:
                             ack_hdr: torch.Tensor | None = None, ack_desc: torch.Tensor | None = None,
                             keep_forwarded: bool = True, actions: torch.Tensor | None = None,
                             desc: torch.Tensor | None = None):
-        """process_apply() over split rows (ina_switch_process_apply_split): the PS ack rows are
+        """process_apply() over split rows (ina_switch with batch.pay and a PS step): the PS ack rows are
         header rows (uint8 [slots, 16]) with their descriptors in ack_desc.  Returns (actions, out)."""
         _req(local, torch.float32, "local")
         npk = hdr.shape[0]
@@ -940,14 +926,10 @@ class Switch:
         _same_device(hdr, pay, actions, local, out, *([ack_hdr] if ack_hdr is not None else []))
         scratch = self._scratch_for(npk, hdr.device)
         self._sorted = None
-        ts = torch.cuda.current_stream(hdr.device)
-        st = self._begin(ts)
-        check(load().ina_switch_process_apply_split(
-            C.byref(self._state), hdr.data_ptr(), pay.data_ptr(), npk, d.data_ptr() if d is not None else None,
-            actions.data_ptr(), scratch.data_ptr(), seq0 & 0xFFFFFFFF, local.data_ptr(), k, weight_step,
-            out.data_ptr(), local.numel(), ack_hdr.data_ptr() if ack_hdr is not None else None, ad,
-            int(keep_forwarded), st), "switch_process_apply_split")
-        self._end(ts)
+        self._call(torch.cuda.current_stream(hdr.device), hdr, pay, npk, 16, d, actions, scratch,
+                   _lib.INA_SWITCH_ALL,
+                   self._ps(seq0, local, k, weight_step, out, ack_hdr.data_ptr() if ack_hdr is not None else None,
+                            16, ad, keep_forwarded), what="switch_process_apply_split")
         return actions, out
 
 
@@ -1014,8 +996,12 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     consecutive slots (worker-major arrival, PS acks in front) skip the slot sort (True, the
     default; False always sorts); switch_pre_all splits the sort's first pass into detection,
     decision and digits for every key width (True, the default; False: keys of 19-22 bits only);
-    unroll is the
-    sum-reduce's 16-byte chunks per worker per thread."""
+    switch_local lets near-sorted batches (V <= 32, local disorder) run from per-slot lists
+    without a sort (True, the default); unroll is the sum-reduce's 16-byte chunks per worker
+    per thread.  Each switch batch reads the switch keys once (a run() follows what its sort()
+    recorded).  stream_blocks, combine_blocks, combine_ina_blocks, ew_blocks and switch_window
+    are grid-cap sweeps that only lab builds of the library accept (make EXTRA=-DINA_LAB_KEYS=1);
+    the product library refuses them (RuntimeError)."""
     lib = load()
     if reduce_blocks is not None:
         check(lib.ina_set_tuning(3, int(reduce_blocks)), "set_tuning")

@@ -145,8 +145,10 @@ int main() {
     ina_switch_state_t st = {slots, V, 1, 0, d_count, d_frag, d_regs};
     void* d_scratch;
     HK(hipMalloc(&d_scratch, ina_switch_scratch_bytes((size_t)W * npk, slots)));
-    CK(ina_switch_process_apply(&st, d_stream, (size_t)W * npk, stride, d_act, d_scratch, 1, d_zero, k,
-                                1.0, d_out, n, nullptr, 0, 0, s));
+    // one call: the packed batch, the PS step fused (ina_switch_ps_t), sort + run
+    const ina_switch_batch_t batch{d_stream, nullptr, (size_t)W * npk, stride, nullptr, d_act, d_scratch};
+    const ina_switch_ps_t ps{1, k, 1.0, d_zero, d_out, n, nullptr, 0, nullptr, 0};
+    CK(ina_switch(&st, &batch, &ps, INA_SWITCH_ALL, s));
     HK(hipStreamSynchronize(s));
     std::vector<float> out(n);
     std::vector<uint8_t> act((size_t)W * npk);
@@ -172,8 +174,8 @@ int main() {
         HK(hipMemsetAsync(d_frag, 0, slots * 4, s));
         HK(hipMemsetAsync(d_regs, 0, (size_t)slots * V * 4, s));
         HK(hipMemsetAsync(d_out, 0xff, n * 4, s));
-        CK(ina_switch_process_apply_split(&st, d_hdr, d_pay, (size_t)W * npk, nullptr, d_act, d_scratch, 1,
-                                          d_zero, k, 1.0, d_out, n, nullptr, nullptr, 0, s));
+        const ina_switch_batch_t sb{d_hdr, d_pay, (size_t)W * npk, 0, nullptr, d_act, d_scratch};
+        CK(ina_switch(&st, &sb, &ps, INA_SWITCH_ALL, s));
         HK(hipStreamSynchronize(s));
         std::vector<uint8_t> act2(act.size());
         HK(hipMemcpy(out.data(), d_out, n * 4, hipMemcpyDeviceToHost));
@@ -183,9 +185,40 @@ int main() {
         HK(hipFree(d_hdr));
         HK(hipFree(d_pay));
     }
+    // the same step in two phases: the slot sort from the packets' descriptors, the switch
+    // tuning flipped in between (the run follows what its sort recorded), then the run
+    {
+        ina_nga_desc_t* d_desc;
+        HK(hipMalloc(&d_desc, (size_t)W * npk * 8));
+        // the packed rows were consumed (keep_forwarded = 0 leaves them as they arrived)
+        CK(ina_nga_descriptors(d_stream, (size_t)W * npk, stride, d_desc, s));
+        HK(hipMemsetAsync(d_count, 0, slots, s));
+        HK(hipMemsetAsync(d_frag, 0, slots * 4, s));
+        HK(hipMemsetAsync(d_regs, 0, (size_t)slots * V * 4, s));
+        HK(hipMemsetAsync(d_out, 0xff, n * 4, s));
+        const ina_switch_batch_t tb{d_stream, nullptr, (size_t)W * npk, stride, d_desc, d_act, d_scratch};
+        CK(ina_switch(&st, &tb, nullptr, INA_SWITCH_SORT, s));
+        CK(ina_set_tuning(18, 0));                 // runs off, digits for every width, LSD passes
+        CK(ina_set_tuning(19, 0));
+        CK(ina_set_tuning(12, 3));
+        CK(ina_switch(&st, &tb, &ps, INA_SWITCH_RUN, s));
+        CK(ina_set_tuning(18, 1));
+        CK(ina_set_tuning(19, 1));
+        CK(ina_set_tuning(12, 0));
+        HK(hipStreamSynchronize(s));
+        std::vector<uint8_t> act3(act.size());
+        HK(hipMemcpy(out.data(), d_out, n * 4, hipMemcpyDeviceToHost));
+        HK(hipMemcpy(act3.data(), d_act, act3.size(), hipMemcpyDeviceToHost));
+        if (act3 != act) ++bad;
+        for (size_t i = 0; i < n; ++i) bad += std::memcmp(&out[i], &f[i], 4) != 0;
+        // a run with no sort of its batch in the scratch is refused
+        const ina_switch_batch_t other{d_stream, nullptr, (size_t)W * npk - 1, stride, nullptr, d_act, d_scratch};
+        if (ina_switch(&st, &other, nullptr, INA_SWITCH_RUN, s) != INA_EINVAL) ++bad;
+        HK(hipFree(d_desc));
+    }
     // the error path: a bad argument returns a code, sets a message, never exits
     const int rc = ina_sum_reduce_i32((const int32_t* const*)d_q, 0, d_sum, n, s);
     if (rc != INA_EINVAL || std::strlen(ina_last_error_string()) == 0) ++bad;
-    std::printf("capi_check: %zu values x %d workers (bulk reduce, NGA-256 pack/unpack, one-launch worker packs, switch + fused PS step, packed and split rows), %zu mismatches\n", n, W, bad);
+    std::printf("capi_check: %zu values x %d workers (bulk reduce, NGA-256 pack/unpack, one-launch worker packs, switch + fused PS step, packed and split rows, two-phase sort/run across a tuning change), %zu mismatches\n", n, W, bad);
     return bad ? 1 : 0;
 }

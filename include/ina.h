@@ -62,26 +62,26 @@ typedef void* ina_stream_t; /* hipStream_t */
 const char* ina_version(void);
 const char* ina_last_error_string(void);
 
-/* Launch-geometry knobs (process-wide; results never change, only speed).  Keys:
+/* Launch-geometry knobs (process-wide; results never change, only speed; every switch batch
+ * reads the switch keys once, and a run alone follows what its sort recorded).  Keys:
  * 0 elementwise grid cap, 1 reduce chunks per worker per thread (0 = per-W auto, 1/2/4), 2 reduce
- * non-temporal loads/stores (0/1), 3 reduce grid (0 = 64*W rule), 4 chunk-loop grid,
- * 5 fp32 PS-combine grid, 6 INA PS-combine grid, 7 host-ingest H2D streams (1/2),
- * 8 16-byte chunks per flat packet-kernel launch, 9 largest switch batch for the
- * one-workgroup sort (0 never, 1 default 768, 2..2048), 10 switch run-kernel window in sorted positions (0 = auto, 1..64),
- * 11 switch lane-parallel path for PS acks alone in their slot's segment (0/1), 12 switch
- * slot sort (0 auto = chunk + bucket sort for keys of one or two digits, else the LSD digit
- * passes; 3 the digit passes for every batch), 13 slot-sort chunk rounds per wave (0 auto,
- * 4, 8, 16), 14 grid cap of the one-in one-out elementwise kernels (quantise, dequantise,
- * PS apply, int16 wire), 15 largest switch batch sorted and run in ONE launch of one
- * workgroup (0 = off, <= 2048; it applies only to batches that also take key 9's
- * one-workgroup path, so it is capped by key 9's threshold), 16 host reduce on pinned
- * device-mapped buffers in place over PCIe (1, default) or through the chunked copy
- * pipeline (0), 17 the slot sort's bucket tile in 64-item rounds per wave (0 auto: 8 when
- * the average bucket exceeds 3,584 packets, else 4; or 4, 8), 18 switch batches made of at
- * most 64 runs of consecutive slots (worker-major arrival, PS acks in front) skip the slot
- * sort and run from a table of the runs (1, default; 0 = always sort), 19 the slot sort's
- * first pass split into detection + decision + digits for every key width (1, default:
- * structured batches then skip the digits) or only for keys of 19-22 bits (0).
+ * non-temporal loads/stores (0/1), 3 reduce grid (0 = 64*W rule), 7 host-ingest H2D streams
+ * (1/2), 8 16-byte chunks per flat packet-kernel launch, 9 largest switch batch for the
+ * one-workgroup sort (0 never, 1 default 768, 2..2048), 11 switch lane-parallel path for PS
+ * acks alone in their slot's segment (0/1), 12 switch slot sort (0 auto = chunk + bucket sort
+ * for keys of one or two digits, else the LSD digit passes; 3 the digit passes for every
+ * batch), 13 slot-sort chunk rounds per wave (0 auto, 4, 8, 16), 15 largest switch batch
+ * sorted and run in ONE launch of one workgroup (0 = off, <= 2048; it applies only to batches
+ * that also take key 9's one-workgroup path, so it is capped by key 9's threshold), 16 host
+ * reduce on pinned device-mapped buffers in place over PCIe (1, default) or through the
+ * chunked copy pipeline (0), 17 the slot sort's bucket tile in 64-item rounds per wave (0
+ * auto: 8 when the average bucket exceeds 3,584 packets, else 4; or 4, 8), 18 switch batches
+ * made of at most 64 runs of consecutive slots (worker-major arrival, PS acks in front) skip
+ * the slot sort and run from a table of the runs (1, default; 0 = always sort), 19 the slot
+ * sort's first pass split into detection + decision + digits for every key width (1, default:
+ * structured batches then skip the digits) or only for keys of 19-22 bits (0), 20 near-sorted
+ * batches (V <= 32, local disorder) skip the sort and run from per-slot lists (1, default; 0 =
+ * sort).  (Keys 4, 5, 6, 10 and 14, grid-cap sweeps, exist in lab builds only.)
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 
@@ -203,7 +203,7 @@ int ina_quantize_pack_nga(const float* x, const float* base, size_t n, int k,
  * headers.p4:27-38).  They play the part of a NIC's receive descriptors: the producer of
  * the packets hands them over beside the payload, so the switch sorts a batch from 8 bytes
  * per packet instead of fetching one 128-byte line of every packet's header
- * (ina_switch_process_desc).  The pack entry points write them as they write each header
+ * (ina_switch, batch.desc).  The pack entry points write them as they write each header
  * (desc may be NULL); ina_nga_descriptors gathers them from packets that arrive without.
  * desc: device memory, 8-byte aligned, npkts entries. */
 typedef uint64_t ina_nga_desc_t;
@@ -289,66 +289,71 @@ typedef struct ina_switch_state {
     uint32_t* regs;
 } ina_switch_state_t;
 size_t ina_switch_scratch_bytes(size_t npkts, uint32_t num_slots);
+
+/* One batch through the switch (every layout and option in one call).
+ *   rows     packed rows (stride bytes apart, stride >= 15 + 4V), or -- pay != NULL -- the
+ *            split header rows (16 bytes apart; stride is ignored), see "split NGA rows";
+ *   pay      split payload rows (4V bytes apart), NULL for packed rows;
+ *   desc     the packets' descriptors (ina_pack_nga_desc / ina_nga_descriptors; desc[p] must
+ *            equal bytes 4..11 of packet p): the slot sort reads them instead of the headers,
+ *            results identical; NULL: the sort reads the headers;
+ *   actions  npkts INA_ACT_* out;  scratch  ina_switch_scratch_bytes(npkts, num_slots) bytes. */
+typedef struct ina_switch_batch {
+    uint8_t* rows;
+    uint8_t* pay;
+    size_t npkts;
+    size_t stride;
+    const ina_nga_desc_t* desc;
+    uint8_t* actions;
+    void* scratch;
+} ina_switch_batch_t;
+
+/* The PS co-located with the switch on one GPU, fused into the switch's pass: a completed
+ * slot's sum goes from the switch's registers straight into out[slot*V + j] = local +
+ * float(weight_step) * (sum * 2^-k) (slot = frag_id - seq0, slot*V + j < n) and its PS ack row
+ * (the packet's header with is_ack = 1, fragcheck.p4:26-31) -- the same results as the switch
+ * followed by ina_apply_completed_nga.  acks: ack rows ack_stride bytes apart (NULL: none;
+ * split rows: header rows, ack_stride 16 or 0); ack_desc (may be NULL; needs acks): each ack
+ * row's descriptor beside it, for every row the call writes, so the next batch -- these acks
+ * in front of the next step's packets -- is sorted without a gather pass (layouts the fused
+ * run kernel does not take -- unaligned packed rows -- apply afterwards and then refresh the
+ * descriptors of all ceil(n/V) rows).  keep_forwarded = 0: completed packets are consumed and
+ * their buffers left as they arrived.  Replaces the Tofino -> PS hop of ngaa.p4:170-175 +
+ * NGAPacket.py:62-143 + launch.py:42-52 when both live on the GPU.  16-byte aligned local,
+ * out, rows and registers; V % 4 == 0. */
+typedef struct ina_switch_ps {
+    uint32_t seq0;
+    int k;
+    double weight_step;
+    const float* local;
+    float* out;
+    size_t n;
+    uint8_t* acks;
+    size_t ack_stride;
+    ina_nga_desc_t* ack_desc;
+    int keep_forwarded;
+} ina_switch_ps_t;
+
+/* phase: the whole call, or its two halves.  With descriptors the slot sort reads nothing but
+ * them, so INA_SWITCH_SORT can be queued as soon as they exist -- before, or on another stream
+ * beside, the kernels that still fill the payload (descriptors from the header parameters
+ * alone: ina_nga_make_descriptors); rows must already be the batch's final address.
+ * INA_SWITCH_RUN then runs the batch over that scratch (the caller orders the two: same stream
+ * or an event) under the switch tuning keys the sort recorded -- ina_set_tuning between them,
+ * from any thread, changes nothing in this batch.  A run over a scratch that no sort of this
+ * batch (npkts, stride, layout, V, num_slots) filled is refused (INA_EINVAL).  (Batches the
+ * small-batch paths take, which sort from the headers, are sorted inside the run.) */
+#define INA_SWITCH_ALL 0
+#define INA_SWITCH_SORT 1
+#define INA_SWITCH_RUN 2
+/* ps may be NULL (the switch alone).  Same semantics, actions, registers and forwarded bytes
+ * in every layout (a collision rewrites the header row's flag byte, a forwarded packet its
+ * payload row). */
+int ina_switch(const ina_switch_state_t* st, const ina_switch_batch_t* batch, const ina_switch_ps_t* ps,
+               int phase, ina_stream_t stream);
+/* The common case in one line: packed rows, headers read by the sort, no PS step. */
 int ina_switch_process(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
                        uint8_t* actions, void* scratch, ina_stream_t stream);
-/* The PS co-located with the switch on one GPU: ina_switch_process followed by
- * ina_apply_completed_nga in ONE pass -- a completed slot's sum goes from the switch's
- * registers straight into out[slot*V + j] = local + weight_step * sum * 2^-k (slot =
- * frag_id - seq0) and its PS ack row, with the same results as the two calls.  With
- * keep_forwarded = 0 the completed packets are consumed and their buffers left as they
- * arrived (everything else as ina_switch_process).  Replaces the Tofino -> PS hop of
- * ngaa.p4:170-175 + NGAPacket.py:62-143 + launch.py:42-52 when both live on the GPU. */
-int ina_switch_process_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
-                             size_t stride, uint8_t* actions, void* scratch, uint32_t seq0,
-                             const float* local, int k, double weight_step, float* out, size_t n,
-                             uint8_t* acks, size_t ack_stride, int keep_forwarded,
-                             ina_stream_t stream);
-/* The same two calls with the batch's packet descriptors (ina_pack_nga_desc /
- * ina_nga_descriptors; desc[p] must equal bytes 4..11 of packet p): the slot sort reads
- * the descriptors instead of the headers; results identical. */
-int ina_switch_process_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
-                            const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                            ina_stream_t stream);
-int ina_switch_process_apply_desc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
-                                  size_t stride, const ina_nga_desc_t* desc, uint8_t* actions,
-                                  void* scratch, uint32_t seq0, const float* local, int k,
-                                  double weight_step, float* out, size_t n, uint8_t* acks,
-                                  size_t ack_stride, int keep_forwarded, ina_stream_t stream);
-/* The same with the ack rows' descriptors written beside them: ack_desc[slot] = bytes 4..11
- * of ack row `slot` (ina_nga_descriptors' format) for every row the call writes, so the
- * next batch -- these acks in front of the next step's packets -- is sorted from
- * descriptors without a gather pass over the ack rows.  ack_desc needs acks (8-byte
- * aligned, one entry per row). */
-int ina_switch_process_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
-                                     size_t stride, const ina_nga_desc_t* desc, uint8_t* actions,
-                                     void* scratch, uint32_t seq0, const float* local, int k,
-                                     double weight_step, float* out, size_t n, uint8_t* acks,
-                                     size_t ack_stride, ina_nga_desc_t* ack_desc, int keep_forwarded,
-                                     ina_stream_t stream);
-/* The same calls in two phases.  With descriptors the slot sort reads nothing but them, so
- * it can be queued as soon as they exist -- before, or on another stream beside, the
- * kernels that still fill the packets' payload (descriptors from the header parameters
- * alone: ina_nga_make_descriptors).  ina_switch_sort_desc queues the sort into `scratch`
- * (pkts is not read, but must be the batch's final address); ina_switch_run_sorted[_apply]
- * then runs the batch over that scratch -- the caller orders the two (same stream or an
- * event) and changes no ina_set_tuning switch key between them.  A run over a scratch that
- * no sort of this same batch (state, pkts, npkts, stride, actions) filled is undefined: it
- * reads that sort's packet ids.  Same actions, registers,
- * packets and update as ina_switch_process[_apply]_desc.  (Batches the small-batch paths
- * take, which sort from the headers, are sorted inside the run call.) */
-int ina_switch_sort_desc(const ina_switch_state_t* st, const uint8_t* pkts, size_t npkts, size_t stride,
-                         const ina_nga_desc_t* desc, uint8_t* actions, void* scratch, ina_stream_t stream);
-int ina_switch_run_sorted(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
-                          uint8_t* actions, void* scratch, ina_stream_t stream);
-int ina_switch_run_sorted_apply(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts, size_t stride,
-                                uint8_t* actions, void* scratch, uint32_t seq0, const float* local, int k,
-                                double weight_step, float* out, size_t n, uint8_t* acks,
-                                size_t ack_stride, int keep_forwarded, ina_stream_t stream);
-int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* pkts, size_t npkts,
-                                        size_t stride, uint8_t* actions, void* scratch, uint32_t seq0,
-                                        const float* local, int k, double weight_step, float* out,
-                                        size_t n, uint8_t* acks, size_t ack_stride,
-                                        ina_nga_desc_t* ack_desc, int keep_forwarded, ina_stream_t stream);
 
 /* Diagnostic: which slot-sort path the last call over `scratch` took (a batch of npkts
  * packets, more than 768 of them; the one-workgroup small-batch paths do not record one; the
@@ -358,20 +363,6 @@ int ina_switch_run_sorted_apply_ackdesc(const ina_switch_state_t* st, uint8_t* p
 #define INA_PATH_SORTED 3     /* the bucket sort (or the LSD digit passes) */
 #define INA_PATH_LOCAL 4      /* near-sorted (local disorder, V <= 32): per-slot lists, no sort */
 int ina_switch_batch_path(const void* scratch, size_t npkts, uint32_t num_slots, int* path);
-
-/* The switch over split rows (hdr: 16-byte header rows, pay: 4V-byte payload rows, see
- * "split NGA rows"): the same semantics, actions, registers and forwarded bytes as
- * ina_switch_process_desc on the packed rows (a collision rewrites the header row's flag
- * byte, a forwarded packet its payload row).  The PS step's ack rows are header rows
- * (16 bytes apart) with their descriptors in ack_desc (may be NULL). */
-int ina_switch_process_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npkts,
-                             const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                             ina_stream_t stream);
-int ina_switch_process_apply_split(const ina_switch_state_t* st, uint8_t* hdr, uint8_t* pay, size_t npkts,
-                                   const ina_nga_desc_t* desc, uint8_t* actions, void* scratch,
-                                   uint32_t seq0, const float* local, int k, double weight_step,
-                                   float* out, size_t n, uint8_t* ack_hdr, ina_nga_desc_t* ack_desc,
-                                   int keep_forwarded, ina_stream_t stream);
 
 /* ---- ipRoute (ngaa.p4:39-61, entries as bfrt/setup.py:85-95 installs them) -------
  * Every packet the ingress does not drop (actions FWD_AGG, FWD_COLLISION, FWD_ACK,

@@ -58,3 +58,36 @@ def test_run_leg_reports_a_failing_leg_and_keeps_the_line():
     bench.run_leg(bad, "sub", lambda: {"x": 1})        # sub-legs attach to an errored parent
     assert line["b"]["sub"] == {"x": 1} and line["value"] == 1.0
     json.dumps(line)
+
+
+def test_legs_summary_is_compact_and_last():
+    sys.path.insert(0, REPO)
+    import bench
+    line = {"value": 5.0, "roofline": {"avg_launch_us": 146.4, "frac": 0.81}, "parity_spot_check": True,
+            "c2_fused": {"roofline": {"avg_launch_us": 79.8, "frac": 0.8}, "parity_spot_check": True},
+            "e2e_pcie": {"ms_per_step": 15.05, "roofline": {"frac": 0.97}, "parity_spot_check": True},
+            "switch_c3_v32": {"workload": "w", "round_robin_split": {"us": 243.5, "frac": 0.6,
+                                                                     "parity_spot_check": True,
+                                                                     "batch_path": "in_order"},
+                              "parity_sample": "s"},
+            "packet_path_v32": {"error": "RuntimeError: out of memory"}}
+    line["legs"] = bench.legs_summary(line)
+    legs = json.loads(json.dumps(line))["legs"]
+    assert list(json.loads(json.dumps(line)))[-1] == "legs"
+    assert legs["headline"] == {"us": 146.4, "frac": 0.81, "parity": True}
+    assert legs["c2_fused"]["us"] == 79.8 and legs["e2e_pcie"]["us"] == 15050.0
+    assert legs["switch_c3_v32.round_robin_split"] == {"us": 243.5, "frac": 0.6, "parity": True,
+                                                       "path": "in_order"}
+    assert legs["packet_path_v32"]["error"].startswith("RuntimeError")
+
+
+def test_leg_tuning_is_restored_when_a_leg_raises(monkeypatch):
+    sys.path.insert(0, REPO)
+    import bench
+    from ina_amd import ops
+    seen = []
+    monkeypatch.setattr(ops, "set_tuning", lambda **kw: seen.append(kw))
+    with pytest.raises(RuntimeError):
+        with bench._tuning(switch_runs=False):
+            raise RuntimeError("leg failed")
+    assert seen == [{"switch_runs": False}, {"switch_runs": True}]

@@ -138,21 +138,14 @@ def _einval_cases():
         "ina_apply_completed_nga": (None, 2, 32, 144, None, 1, None, 16, 0.5, None, 64, None, 144,
                                     None),
         "ina_switch_process": (ctypes.byref(st), None, 2, 144, None, None, None),
-        "ina_switch_process_desc": (ctypes.byref(st), None, 2, 144, None, None, None, None),
-        "ina_switch_process_apply_desc": (ctypes.byref(st), None, 2, 144, None, None, None, 1, None, 16,
-                                          0.5, None, 64, None, 144, 1, None),
+        "ina_switch": (ctypes.byref(st), ctypes.byref(_lib.SwitchBatch(None, None, 2, 144, None, None, None)),
+                       None, _lib.INA_SWITCH_ALL, None),
         "ina_pack_nga_desc": (None, 64, ctypes.byref(prm), None, None, 144, None, None),
         "ina_quantize_pack_nga_desc": (None, None, 64, 16, ctypes.byref(prm), None, 144, None, None),
         "ina_nga_descriptors": (None, 2, 144, None, None),
         "ina_nga_make_descriptors": ((_lib.NgaParams * 2)(prm, prm), 2, 64, P([None, None]), None),
-        "ina_switch_sort_desc": (ctypes.byref(st), None, 2, 144, None, None, None, None),
-        "ina_switch_run_sorted": (ctypes.byref(st), None, 2, 144, None, None, None),
-        "ina_switch_run_sorted_apply": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
-                                        None, 64, None, 144, 1, None),
         "ina_quantize_pack_nga_multi": (P([None, None]), 2, None, 64, 16,
                                         (_lib.NgaParams * 2)(prm, prm), P([None, None]), 144, None, None),
-        "ina_switch_process_apply": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
-                                     None, 64, None, 144, 1, None),
         "ina_route_ipv4": (None, None, 0, 4, None, None, 1, None, None),
         "ina_checksum_i32": (None, 64, None, None),
         "ina_absmax_f32": (None, None, 64, None, None),
@@ -164,13 +157,6 @@ def _einval_cases():
                                               (_lib.NgaParams * 2)(prm, prm), P([None, None]),
                                               P([None, None]), None, None),
         "ina_unpack_nga_split": (None, None, 2, 32, None, None, None),
-        "ina_switch_process_split": (ctypes.byref(st), None, None, 2, None, None, None, None),
-        "ina_switch_process_apply_split": (ctypes.byref(st), None, None, 2, None, None, None, 1, None, 16,
-                                           0.5, None, 64, None, None, 1, None),
-        "ina_switch_process_apply_ackdesc": (ctypes.byref(st), None, 2, 144, None, None, None, 1, None, 16,
-                                             0.5, None, 64, None, 144, None, 1, None),
-        "ina_switch_run_sorted_apply_ackdesc": (ctypes.byref(st), None, 2, 144, None, None, 1, None, 16, 0.5,
-                                                None, 64, None, 144, None, 1, None),
     }
 
 
@@ -211,8 +197,8 @@ def test_set_tuning_rejects_unknown_keys_and_values():
     assert lib.ina_set_tuning(-1, 1) == _lib.INA_EINVAL
     assert lib.ina_set_tuning(1, 3) == _lib.INA_EINVAL          # reduce chunks: 1, 2 or 4
     assert lib.ina_set_tuning(7, 3) == _lib.INA_EINVAL          # H2D streams: 1 or 2
-    assert lib.ina_set_tuning(10, 65) == _lib.INA_EINVAL        # switch window <= 64
-    assert lib.ina_set_tuning(10, 0) == _lib.INA_OK             # 0 = automatic
+    for lab_key in (4, 5, 6, 10, 14):                           # grid-cap sweeps: lab builds only
+        assert lib.ina_set_tuning(lab_key, 1) == _lib.INA_EINVAL
     assert lib.ina_set_tuning(11, 1) == _lib.INA_OK
     assert lib.ina_set_tuning(12, 4) == _lib.INA_EINVAL        # sort: 0 auto, 3 digit passes
     assert lib.ina_set_tuning(12, 1) == _lib.INA_EINVAL        # one-sweep: moved to tools/lab
@@ -244,14 +230,41 @@ def test_switch_scratch_bytes_monotonic():
 
 
 def test_process_apply_refuses_misaligned_registers():
-    """ina_switch_process_apply takes only layouts its fused kernel handles, so
+    """ina_switch with a PS step takes only layouts its fused kernel handles, so
     keep_forwarded=0 always holds: misaligned slot registers are refused
     before any device work (the pointers are never dereferenced)."""
     from ina_amd import _lib
     lib = _lib.load()
     fake = 1 << 20                                   # aligned, never touched
     st = _lib.SwitchState(64, 32, 1, 0, fake, fake, fake + 8)
-    rc = lib.ina_switch_process_apply(ctypes.byref(st), fake, 4, 144, fake, fake, 1, fake, 16, 0.5,
-                                      fake, 64, None, 144, 0, None)
+    b = _lib.SwitchBatch(fake, None, 4, 144, None, fake, fake)
+    ps = _lib.SwitchPs(1, 16, 0.5, fake, fake, 64, None, 144, None, 0)
+    rc = lib.ina_switch(ctypes.byref(st), ctypes.byref(b), ctypes.byref(ps), _lib.INA_SWITCH_ALL, None)
     assert rc == _lib.INA_EINVAL
     assert b"registers" in lib.ina_last_error_string()
+
+
+def test_switch_call_validates_before_device_work():
+    """ina_switch (include/ina.h): an unknown phase, a null batch, a split PS step whose ack
+    rows are not header rows, and a run alone over a scratch no sort of that batch filled are
+    refused with a message -- no pointer is dereferenced."""
+    from ina_amd import _lib
+    lib = _lib.load()
+    fake = 1 << 20
+    st = _lib.SwitchState(1 << 13, 32, 1, 0, fake, fake, fake)
+    b = _lib.SwitchBatch(fake, None, 4096, 144, fake, fake, fake + 4096)
+    assert lib.ina_switch(ctypes.byref(st), ctypes.byref(b), None, 3, None) == _lib.INA_EINVAL
+    assert b"phase" in lib.ina_last_error_string()
+    assert lib.ina_switch(ctypes.byref(st), None, None, _lib.INA_SWITCH_ALL, None) == _lib.INA_EINVAL
+    split = _lib.SwitchBatch(fake, fake, 4096, 0, fake, fake, fake + 4096)
+    ps = _lib.SwitchPs(1, 16, 0.5, fake, fake, 64, fake, 144, None, 0)
+    assert lib.ina_switch(ctypes.byref(st), ctypes.byref(split), ctypes.byref(ps), _lib.INA_SWITCH_ALL,
+                          None) == _lib.INA_EINVAL
+    assert b"header rows" in lib.ina_last_error_string()
+    # never sorted into this scratch: refused (it used to read stale packet ids)
+    assert lib.ina_switch(ctypes.byref(st), ctypes.byref(b), None, _lib.INA_SWITCH_RUN, None) == _lib.INA_EINVAL
+    assert b"no sort of this batch" in lib.ina_last_error_string()
+    # a sort alone needs the descriptors
+    nodesc = _lib.SwitchBatch(fake, None, 4096, 144, None, fake, fake + 4096)
+    assert lib.ina_switch(ctypes.byref(st), ctypes.byref(nodesc), None, _lib.INA_SWITCH_SORT,
+                          None) == _lib.INA_EINVAL

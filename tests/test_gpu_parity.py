@@ -1070,7 +1070,7 @@ def test_switch_bucket_rows_limit_equals_digit_passes(extra):
 @pytest.mark.parametrize("V,W,per,tail", [(32, 4, 60, 11), (256, 8, 700, 0), (32, 3, 3000, 5),
                                           (64, 16, 200, 37), (32, 2, 30, 3), (256, 3, 30, 0)])   # last two: <= 128-packet batches (one launch)
 def test_switch_process_apply_equals_two_steps(V, W, per, tail, keep):
-    """ina_switch_process_apply (the PS on the switch's GPU) == ina_switch_process then
+    """ina_switch with a PS step (the PS on the switch's GPU) == ina_switch_process then
     ina_apply_completed_nga: same actions, switch registers, parameter update (bit for bit)
     and PS ack rows, over two steps with the acks riding in front of the second step's
     packets; keep_forwarded=False leaves completed packets as they arrived."""
@@ -1120,10 +1120,10 @@ def test_switch_process_apply_equals_two_steps(V, W, per, tail, keep):
                                            (32, 4, 3000, "shuffled"), (256, 3, 30, "worker"),
                                            (32, 4, 150, "worker"), (64, 16, 200, "shuffled")])
 def test_switch_two_phase_equals_one_call(V, W, per, order, sort_mode):
-    """ina_switch_sort_desc queued on a side stream from descriptors made from the header
+    """ina_switch (INA_SWITCH_SORT) queued on a side stream from descriptors made from the header
     fields alone (ina_nga_make_descriptors + the ack rows' descriptors), BEFORE the packets'
-    payload is packed on the main stream, then ina_switch_run_sorted_apply after both ==
-    ina_switch_process_apply_desc on the packed batch: same actions, PS update (bit for bit),
+    payload is packed on the main stream, then ina_switch (INA_SWITCH_RUN + PS step) after both ==
+    ina_switch (descriptors + PS step) on the packed batch: same actions, PS update (bit for bit),
     ack rows and switch state over two steady-state steps.  Covers the bucket sort, the
     digit passes (sort_mode 3), presorted batches and the one-workgroup small-batch paths
     (<= 768 and <= 128 packets, which sort inside the run call)."""

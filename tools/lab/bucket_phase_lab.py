@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
 from ina_amd import _lib, ops  # noqa: E402
 
 lab = C.CDLL(os.path.join(HERE, "libina_bktime.so"))
-for nm in ("ina_switch_process_desc", "ina_switch_scratch_bytes"):
+for nm in ("ina_switch", "ina_switch_scratch_bytes"):
     getattr(lab, nm).argtypes = _lib.SIGNATURES[nm]
 lab.ina_switch_scratch_bytes.restype = C.c_size_t
 lab.ina_lab_bk_times.argtypes = [C.c_void_p]
@@ -61,9 +61,10 @@ for oname, (pk, ds) in orders.items():
         work.copy_(pk)
         count.zero_()
         frag.zero_()
-        assert lab.ina_switch_process_desc(C.byref(st), work.data_ptr(), npk, stride, ds.data_ptr(),
-                                           acts.data_ptr(), scratch.data_ptr(),
-                                           torch.cuda.current_stream().cuda_stream) == 0
+        b = _lib.SwitchBatch(work.data_ptr(), None, npk, stride, ds.data_ptr(), acts.data_ptr(),
+                             scratch.data_ptr())
+        assert lab.ina_switch(C.byref(st), C.byref(b), None, _lib.INA_SWITCH_ALL,
+                              torch.cuda.current_stream().cuda_stream) == 0
         torch.cuda.synchronize()
         assert lab.ina_lab_bk_times(buf.ctypes.data) == 0
         if rep < 2:

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of ina_switch_process_apply across libina builds (experiment only):
+"""Interleaved A/B of ina_switch with a PS step across libina builds (experiment only):
 8 workers x NGA-256 packets of a config-3 bucket, PS step fused; switch state reset
 between launches; outputs must agree."""
 import ctypes as C
@@ -40,7 +40,7 @@ scratch_bytes = 0
 vs = []
 for p in sys.argv[1:]:
     lib = C.CDLL(p)
-    for nm in ("ina_switch_process_apply", "ina_switch_scratch_bytes"):
+    for nm in ("ina_switch", "ina_switch_scratch_bytes"):
         getattr(lib, nm).argtypes = _lib.SIGNATURES[nm]
     lib.ina_switch_scratch_bytes.restype = C.c_size_t
     scratch_bytes = max(scratch_bytes, lib.ina_switch_scratch_bytes(npk_all, slots))
@@ -56,10 +56,11 @@ def run(v):
     v["frag"].zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    rc = v["lib"].ina_switch_process_apply(C.byref(v["st"]), stream.data_ptr(), npk_all, stride,
-                                           v["acts"].data_ptr(), v["scratch"].data_ptr(), 1,
-                                           local.data_ptr(), 16, 0.125, v["out"].data_ptr(), n,
-                                           v["acks"].data_ptr(), stride, 0, st)
+    b = _lib.SwitchBatch(stream.data_ptr(), None, npk_all, stride, None, v["acts"].data_ptr(),
+                         v["scratch"].data_ptr())
+    ps = _lib.SwitchPs(1, 16, 0.125, local.data_ptr(), v["out"].data_ptr(), n, v["acks"].data_ptr(), stride,
+                       None, 0)
+    rc = v["lib"].ina_switch(C.byref(v["st"]), C.byref(b), C.byref(ps), _lib.INA_SWITCH_ALL, st)
     e1.record()
     assert rc == 0
     return e0, e1

@@ -49,6 +49,19 @@ for J in [int(x) for x in os.environ.get("J", "64,4096").split(",")]:
         torch.cuda.synchronize()
         assert lab.ina_lab_loc_times(buf.ctypes.data) == 0
         b = buf.astype(np.int64)
+        d0, dl = b[8191], b[8190]           # the decision pass: block 0 and the last block
+        if rep >= 2:
+            res.setdefault("dec_breaks", []).append(float(d0[1] - d0[0]) / 100)
+            res.setdefault("dec_decide", []).append(float(d0[2] - d0[1]) / 100)
+            dsub = b[8189]                   # inside the decision: PM/SM, units, reduction
+            res.setdefault("dec_pmsm", []).append(float(dsub[0] - d0[1]) / 100)
+            res.setdefault("dec_units", []).append(float(dsub[1] - dsub[0]) / 100)
+            res.setdefault("dec_reduce", []).append(float(dsub[2] - dsub[1]) / 100)
+            res.setdefault("dec_write", []).append(float(d0[2] - dsub[2]) / 100)
+            res.setdefault("dec_last_entry", []).append(float(dl[0] - d0[0]) / 100)
+            res.setdefault("dec_last_seen", []).append(float(dl[1] - d0[0]) / 100)
+            res.setdefault("dec_to_lists", []).append(float(b[:8189, 0][b[:8189, 0] > 0].min() - d0[2]) / 100)
+        b = b[:8189]
         b = b[(b[:, 0] > 0) & (b[:, 3] >= b[:, 0])]
         if rep < 2:
             continue

@@ -1,5 +1,5 @@
 """Profile target: the one-GPU INA packet path in steady state with the PS step fused into
-the switch pass (the 8 workers' fused quantise+packs in one launch, one ina_switch_process_apply over
+the switch pass (the 8 workers' fused quantise+packs in one launch, one ina_switch with a PS step over
 [last step's acks | 8 x 102,400 NGA-256 packets]); run under rocprofv3 --kernel-trace
 --stats for the per-kernel breakdown of bench_extra's last packet-path row).  The run kernel
 writes the ack rows' descriptors (ack_desc), as bench.py's packet_path does.  SPLIT=1: the
