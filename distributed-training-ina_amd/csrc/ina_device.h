@@ -38,6 +38,18 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 // buffer resource word 3 for a raw (stride 0, untyped) gfx9 buffer: 32-bit data format
 constexpr int kRawBufferWord3 = 0x00020000;
 constexpr int kAuxSC1 = 16;
+// INA_STORE_CHECK = 1 (checked builds: make BUILD=build_chk OUT=... EXTRA=-DINA_STORE_CHECK=1):
+// every stream_store verifies the CONTRACT above -- its lane's distance from the wave's base is
+// in [0, 2^31 - sizeof(T)] -- and counts each store that breaks it in a per-source device
+// counter (ina_store_check_violations reads and clears them; tests/test_gpu_store_views.py and
+// the conftest hook of a checked run assert zero).  Counted, not trapped: a trap is a GPU fault,
+// and on this pool a faulting kernel can take the machine's GPUs down with it.
+#ifndef INA_STORE_CHECK
+#define INA_STORE_CHECK 0
+#endif
+#if INA_STORE_CHECK
+static __device__ unsigned long long g_store_violations;   // one per source file
+#endif
 template <typename T>
 __device__ __forceinline__ void stream_store(T v, T* p) {
 #if INA_STORE_SC1
@@ -48,6 +60,11 @@ __device__ __forceinline__ void stream_store(T v, T* p) {
     const uint64_t a0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
                         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
     const uint32_t d = (uint32_t)(a - a0);
+#if INA_STORE_CHECK
+    const int64_t dist = (int64_t)(a - a0);
+    if (dist < 0 || dist > (int64_t)0x7FFFFFFF - (int64_t)sizeof(T))
+        atomicAdd(&g_store_violations, 1ull);
+#endif
     __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)a0, 0, 0x7FFFFFFF, kRawBufferWord3);
     if constexpr (sizeof(T) == 16)

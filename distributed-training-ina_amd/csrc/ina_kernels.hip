@@ -2587,3 +2587,26 @@ int ina_checksum_i32(const int32_t* x, size_t n, uint32_t* out_dev, ina_stream_t
 }
 
 }  // extern "C"
+
+#if INA_STORE_CHECK
+namespace ina {
+unsigned long long store_violations_kernels() {
+    unsigned long long v = 0, z = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_store_violations), sizeof(v)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_store_violations), &z, sizeof(z)) != hipSuccess)
+        return ~0ull;                                  // unreadable: report as a violation
+    return v;
+}
+}  // namespace ina
+#endif
+
+#if INA_STORE_CHECK
+// checked builds only (not in include/ina.h): the stream_store contract violations of every
+// source since the last call, cleared by the call
+extern "C" int ina_store_check_violations(unsigned long long* count) {
+    if (!count) return INA_EINVAL;
+    if (hipDeviceSynchronize() != hipSuccess) return INA_EHIP;
+    *count = ina::store_violations_kernels() + ina::store_violations_shard() + ina::store_violations_switch();
+    return INA_OK;
+}
+#endif

@@ -194,3 +194,15 @@ int ina_i16_wire_finish(const int32_t* wire_sum, size_t n, int k, int V, int16_t
 }
 
 }  // extern "C"
+
+#if INA_STORE_CHECK
+namespace ina {
+unsigned long long store_violations_shard() {
+    unsigned long long v = 0, z = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_store_violations), sizeof(v)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_store_violations), &z, sizeof(z)) != hipSuccess)
+        return ~0ull;                                  // unreadable: report as a violation
+    return v;
+}
+}  // namespace ina
+#endif

@@ -2564,6 +2564,12 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
 // (group g: the g-th head), walking each segment's packets in position order (= arrival
 // order inside the slot, ngaa.p4:120-196) with kP positions' loads in flight.  Per packet the
 // same group_packet as the run-table path; a segment may run past the window's end.
+// (lab) an in-order batch in split NGA-32 rows: the window's 64 payload rows are loaded up
+// front, right behind the keys (they do not depend on them), and staged in LDS, the 64 header
+// rows one per lane; the lane groups then walk their segments from LDS and a permute
+#ifndef INA_SWITCH_INORDER_STAGE
+#define INA_SWITCH_INORDER_STAGE 0
+#endif
 template <bool kPs, bool kSplit>
 __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                     uint8_t* __restrict__ pay, size_t npk, size_t stride,
@@ -2581,12 +2587,36 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
     // written by every lane of the wave: see group_packet on DPP / permutes and EXEC)
     __shared__ uint32_t s_wid[kSwBlock], s_wack[kSwBlock];
     const int wb = (int)threadIdx.x & ~63;
+#if INA_SWITCH_INORDER_STAGE
+    constexpr bool kStage = kSplit;
+    __shared__ u32x4s s_pay[kStage ? kSwBlock / 64 : 1][kStage ? 512 : 1];
+    const bool stage = kStage && ids == nullptr && V == 32 && win == 64;
+    const int wv_ = wave_in_block();
+#else
+    constexpr bool stage = false;
+#endif
     for (size_t w0 = wave * win; w0 < npk; w0 += nwaves * win) {
         const size_t i = w0 + (size_t)lane;
         const uint32_t kr = i < npk ? keys[i] : NS;
         const uint32_t ki = kr & kmask;                   // slot (bit 31: PS-ack hint)
         const uint32_t idw = i < npk ? (ids ? ids[i] : (uint32_t)i) : 0u;
         const uint32_t kp = (i > 0 && i <= npk) ? (keys[i - 1] & kmask) : 0xFFFFFFFFu;
+        u32x4s hrow = {0u, 0u, 0u, 0u};                   // (stage) header row of position lane
+#if INA_SWITCH_INORDER_STAGE
+        if (stage) {                                      // wave-uniform
+            // chunk k*64 + lane = row k*8 + lane/8, chunk lane%8: 1 KiB contiguous per load
+            u32x4s pr[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const size_t q = w0 + (size_t)(k * 8 + (lane >> 3));
+                pr[k] = q < npk ? sw_ld(reinterpret_cast<const u32x4s*>(pay + q * 128) + (lane & 7))
+                                : u32x4s{0u, 0u, 0u, 0u};
+            }
+            if (i < npk) hrow = *reinterpret_cast<const u32x4s*>(pkts + i * 16);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s_pay[wv_][k * 64 + lane] = pr[k];
+        }
+#endif
         const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
         __builtin_amdgcn_wave_barrier();
         s_wid[threadIdx.x] = idw;
@@ -2641,6 +2671,13 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                     const uint32_t k = k0 + (uint32_t)j;
                     const uint32_t q = hst + k;           // window-relative position
                     in[j] = has && k < hlen;
+                    if (stage) {                          // every lane: the permute's sources
+                        const int src = (int)(q < 64u ? q : 0u);
+                        h[j].x = (uint32_t)__shfl((int)hrow.x, src);
+                        h[j].y = (uint32_t)__shfl((int)hrow.y, src);
+                        h[j].z = (uint32_t)__shfl((int)hrow.z, src);
+                        h[j].w = (uint32_t)__shfl((int)hrow.w, src);
+                    }
                     // id and ack hint: the window's (LDS), past the window from memory
                     pid[j] = 0u;
                     acq[j] = false;
@@ -2656,6 +2693,12 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                     }
                     if (in[j] && !acq[j]) {
                         if constexpr (kSplit) {
+#if INA_SWITCH_INORDER_STAGE
+                            if (stage && q < 64u) {
+                                m[j] = s_pay[wv_][q * 8u + (uint32_t)(vl ? l : 0)];
+                                continue;
+                            }
+#endif
                             m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
                                          (vl ? l : 0));
                             h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
@@ -3721,3 +3764,15 @@ int ina_route_ipv4(const uint8_t* actions, const uint32_t* dst_ip, uint32_t dst_
 }
 
 }  // extern "C"
+
+#if INA_STORE_CHECK
+namespace ina {
+unsigned long long store_violations_switch() {
+    unsigned long long v = 0, z = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_store_violations), sizeof(v)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_store_violations), &z, sizeof(z)) != hipSuccess)
+        return ~0ull;                                  // unreadable: report as a violation
+    return v;
+}
+}  // namespace ina
+#endif

@@ -11,7 +11,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libina.so")
+# INA_LIBRARY=<name>.so beside libina.so: a variant build of the same sources (the checked
+# stream_store build, libina_storecheck.so), for test runs only
+LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("INA_LIBRARY", "libina.so")))
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 INA_OK, INA_EINVAL, INA_EHIP, INA_ESOCK, INA_ENOMEM = 0, -1, -2, -3, -4

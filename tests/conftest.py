@@ -28,3 +28,20 @@ def gpu_available() -> bool:
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(REPO, "tests", "golden")
+
+
+@pytest.fixture(autouse=True)
+def _store_contract_checked(request):
+    """Under a checked build (INA_LIBRARY=libina_storecheck.so, csrc/ina_device.h
+    INA_STORE_CHECK) every GPU test ends with zero stream_store contract violations."""
+    yield
+    if request.node.get_closest_marker("gpu") is None or not os.environ.get("INA_LIBRARY"):
+        return
+    import ctypes
+    from ina_amd import _lib
+    lib = _lib.load()
+    if not hasattr(lib, "ina_store_check_violations"):
+        return
+    n = ctypes.c_ulonglong(0)
+    assert lib.ina_store_check_violations(ctypes.byref(n)) == 0
+    assert n.value == 0, f"{n.value} stream_store contract violations"

@@ -21,6 +21,11 @@ for st in $STAGES; do
     test)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -25 "$OUT/pytest_gpu.log"; ok_or_fail pytest $rc ;;
+    testchk)
+      # the whole GPU suite under the checked stream_store build (make -C csrc storecheck)
+      INA_LIBRARY=libina_storecheck.so timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 120 \
+        --timeout-method thread > "$OUT/pytest_gpu_storecheck.log" 2>&1
+      rc=$?; tail -25 "$OUT/pytest_gpu_storecheck.log"; ok_or_fail pytest_storecheck $rc ;;
     lab:*)
       nm=${st#lab:}
       timeout -k 10 300 python tools/lab/$nm.py > "$OUT/$nm.log" 2>&1
