@@ -968,7 +968,8 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(8
                                                                uint32_t num_slots, uint32_t kmask,
                                                                const uint32_t* __restrict__ unsorted,
                                                                const LocUnit* __restrict__ units, uint32_t gsize,
-                                                               uint32_t* __restrict__ ids, uint2* __restrict__ tab) {
+                                                               uint32_t* __restrict__ ids, uint2* __restrict__ tab,
+                                                               uint8_t* __restrict__ actions) {
     constexpr int kThr = kLlWaves * 64;
     constexpr int DPT = kLlBins / kThr;                           // consecutive slots a thread scans
     __shared__ uint32_t cw[kLlWaves / 2][kLlBins];                // per-wave counts, then cursors
@@ -982,7 +983,13 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(8
     const uint32_t kmin = unsorted[kLocKmin], nunits = unsorted[kLocUnits];
     for (uint32_t u = (uint32_t)switch_block_index(); u < nunits; u += gridDim.x) {
         const LocUnit w = units[u];
-        if (w.hi <= w.lo) continue;                               // no slot (block-uniform)
+        if (w.hi <= w.lo) {                                       // no slot (block-uniform): only
+            const uint32_t Pu = u * kLocU * gsize;                // its positions' drops
+            const uint32_t P1 = (uint32_t)min((size_t)Pu + (size_t)kLocU * gsize, npk);
+            for (uint32_t p = Pu + threadIdx.x; p < P1; p += kLlWaves * 64)
+                if ((keys[p] & kmask) < num_slots) actions[p] = INA_ACT_DROP;
+            continue;
+        }
         LOC_STAMP(0);
         // positions fit 32 bits (npk <= 2^31 - 1)
         const uint32_t P0 = w.g_lo * gsize, Pu = u * kLocU * gsize;
@@ -1018,6 +1025,10 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(8
                     const uint32_t p = r0 + (uint32_t)(r * 64 + lane);
                     lds_count_half(crow, slot - q, slot < num_slots && slot - q < qn, sh);
                     before += (p < Pu && p < b1 && (slot < w.lo || slot >= num_slots)) ? 1u : 0u;
+                    // the unit's own positions: every packet of this switch starts as a drop, so
+                    // the run stores only the other actions (1 in W) -- scattered byte stores
+                    // by list order cost 29 us at NGA-32 C3 size, these are by position
+                    if (q == w.lo && p >= Pu && p < b1 && slot < num_slots) actions[p] = INA_ACT_DROP;
                 }
             }
             if (q == w.lo) {
@@ -2436,16 +2447,35 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
 #endif
 template <bool kSplit>
 constexpr int kSlotInFlight = kSplit ? INA_SWITCH_SLOT_INFLIGHT_SPLIT : INA_SWITCH_SLOT_INFLIGHT;
+// (lab) split rows: lane l of a group loads the header row of the group's packet k0 + l (one
+// 16-byte load per lane instead of every lane loading every in-flight packet's header), and
+// packet j's header reaches the group's lanes by a permute from lane 8g + j -- the VGPRs that
+// buy more packets in flight (kSlotInFlight up to 8)
+#ifndef INA_SWITCH_HDR_SHFL
+#define INA_SWITCH_HDR_SHFL 0
+#endif
+static_assert(!INA_SWITCH_HDR_SHFL || INA_SWITCH_SLOT_INFLIGHT_SPLIT <= 8, "one header per lane of a group");
+__device__ __forceinline__ u32x4s group_hdr(const u32x4s& hl, int g, int j) {
+    const int src = 8 * g + j;
+    return u32x4s{(uint32_t)__shfl((int)hl.x, src), (uint32_t)__shfl((int)hl.y, src),
+                  (uint32_t)__shfl((int)hl.z, src), (uint32_t)__shfl((int)hl.w, src)};
+}
 // one packet of a lane group's slot (group-uniform: every lane of the group runs it with the
 // same header): ack / collision / count / Processor add, the PS step, the rewritten packet
 // and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
 // header chunk / header row; ack_known: a PS ack by its sort key (then m and h are unread)
+// (lab, timing only -- WRONG results) drop the narrow run's per-packet action bytes (1), its
+// forwarded-payload stores (2) or both (3), to price each store stream
+#ifndef INA_LAB_DROP_STORES
+#define INA_LAB_DROP_STORES 0
+#endif
 template <bool kPs, bool kSplit, int kThr = kSwBlock>
 __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                              size_t stride, uint8_t* __restrict__ pay,
                                              uint8_t* __restrict__ actions, const PsFuse& ps, uint32_t slot,
                                              uint32_t pid, const u32x4s& m, const u32x4s& h, bool ack_known,
-                                             uint32_t& cnt, uint32_t& frag, u32x4s& reg, bool& have_reg) {
+                                             uint32_t& cnt, uint32_t& frag, u32x4s& reg, bool& have_reg,
+                                             bool drop_written = false) {
     // neighbour lanes' words go through LDS, not DPP: a DPP move whose source lane is disabled
     // returns its fallback, and the compiler may narrow EXEC around a DPP that feeds a per-lane
     // select (it did: l == 0 ? h3 : row_shr(m.w) became a branch on l != 0).  Every lane of the
@@ -2530,7 +2560,8 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
                 if constexpr (kSplit) {
                     const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
                                    __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
-                    if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid * (size_t)(4 * V)) + l);
+                    if (vl && !(INA_LAB_DROP_STORES & 2))
+                        sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid * (size_t)(4 * V)) + l);
                 } else {
                     // chunk l + 1: bytes 1..3 of values 4l..4l+3, then byte 0 of value
                     // 4l + 4 (the next lane's; the group's last value lane keeps the
@@ -2555,7 +2586,8 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
             }
         }
     }
-    if (l == 0) actions[pid] = act;
+    // (drop_written: the near-sorted path's lists kernel stored the drops by position)
+    if (l == 0 && !(INA_LAB_DROP_STORES & 1) && !(drop_written && act == INA_ACT_DROP)) actions[pid] = act;
 }
 
 // Narrow packets (V <= 32) in sorted order (the bucket sort's arrays, or a batch already in
@@ -2666,6 +2698,18 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                 u32x4s m[kP], h[kP];
                 uint32_t pid[kP];
                 bool in[kP], acq[kP];
+#if INA_SWITCH_HDR_SHFL
+                u32x4s hl = {0u, 0u, 0u, 0u};             // the header of the group's packet k0 + l
+                if constexpr (kSplit) {
+                    const uint32_t kl = k0 + (uint32_t)l, ql = hst + kl;
+                    if (!stage && has && l < kP && kl < hlen) {
+                        const uint32_t pl = ql < 64u ? s_wid[wb + (int)ql]
+                                                     : (ids ? ids[w0 + ql] : (uint32_t)(w0 + ql));
+                        const bool al = ql < 64u ? s_wack[wb + (int)ql] != 0u : (keys[w0 + ql] & ~kmask) != 0u;
+                        if (!al) hl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pl * 16);
+                    }
+                }
+#endif
 #pragma unroll
                 for (int j = 0; j < kP; ++j) {
                     const uint32_t k = k0 + (uint32_t)j;
@@ -2701,7 +2745,9 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
 #endif
                             m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
                                          (vl ? l : 0));
+#if !INA_SWITCH_HDR_SHFL
                             h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+#endif
                         } else {
                             const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
                             m[j] = sw_ld(pk + (vl ? l + 1 : 1));
@@ -2712,6 +2758,10 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
 #pragma unroll
                 for (int j = 0; j < kP; ++j) {
                     if (!__ballot(in[j])) continue;
+#if INA_SWITCH_HDR_SHFL
+                    if constexpr (kSplit)
+                        if (!stage) h[j] = group_hdr(hl, g, j);   // every lane (a permute)
+#endif
                     if (!in[j]) continue;
                     group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, hslot, pid[j], m[j], h[j], acq[j],
                                               cnt, frag, reg, have_reg);
@@ -2772,9 +2822,21 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
         }
         u32x4s reg = {0u, 0u, 0u, 0u};
         bool have_reg = false;
+#if INA_SWITCH_HDR_SHFL
+        u32x4s hl = {0u, 0u, 0u, 0u};                                 // the header of entry (k0 & ~7) + l
+#endif
         for (uint32_t k0 = 0; k0 < maxlen; k0 += kP) {
             if (k0 && (k0 & 7u) == 0)                              // entries k0..k0+7
                 idl = k0 + (uint32_t)l < hlen ? ids[hst + k0 + (uint32_t)l] : 0u;
+#if INA_SWITCH_HDR_SHFL
+            if constexpr (kSplit) {
+                if ((k0 & 7u) == 0) {
+                    hl = u32x4s{0u, 0u, 0u, 0u};
+                    if (k0 + (uint32_t)l < hlen && (idl & kAckBit) == 0u)
+                        hl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)idl * 16);
+                }
+            }
+#endif
             u32x4s m[kP], h[kP];
             uint32_t pid[kP];
             bool in[kP], acq[kP];
@@ -2788,7 +2850,9 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
                 if (in[j] && !acq[j]) {
                     if constexpr (kSplit) {
                         m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) + (vl ? l : 0));
+#if !INA_SWITCH_HDR_SHFL
                         h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+#endif
                     } else {
                         const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
                         m[j] = sw_ld(pk + (vl ? l + 1 : 1));
@@ -2799,9 +2863,12 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
 #pragma unroll
             for (int j = 0; j < kP; ++j) {
                 if (!__ballot(in[j])) continue;
+#if INA_SWITCH_HDR_SHFL
+                if constexpr (kSplit) h[j] = group_hdr(hl, g, (int)((k0 + (uint32_t)j) & 7u));
+#endif
                 if (!in[j]) continue;
                 group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, pid[j], m[j], h[j], acq[j], cnt,
-                                          frag, reg, have_reg);
+                                          frag, reg, have_reg, true);
             }
         }
         id_nx = (uint32_t)l < e_nx.y ? ids[e_nx.x + (uint32_t)l] : 0u;   // the next step's first ids
@@ -2953,6 +3020,18 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
             u32x4s m[kP], h[kP];
             uint32_t pid[kP];
             bool in[kP], ackr[kP];
+#if INA_SWITCH_HDR_SHFL
+            u32x4s hl = {0u, 0u, 0u, 0u};                 // the header of run r0 + l's packet
+            if constexpr (kSplit) {
+                const uint32_t r = r0 + (uint32_t)l;
+                const int rr = (int)(r < R ? r : 0u);
+                const uint32_t rs = (uint32_t)__shfl((int)rslot, rr), rl = (uint32_t)__shfl((int)rlen, rr);
+                const uint32_t rp = (uint32_t)__shfl((int)rpos, rr), ra = (uint32_t)__shfl((int)rack_u, rr);
+                const uint32_t off = slot - rs;
+                if (l < kP && r < R && sv && off < rl && ra == 0u)
+                    hl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)(rp + off) * 16);
+            }
+#endif
 #pragma unroll
             for (int j = 0; j < kP; ++j) {
                 const uint32_t r = r0 + (uint32_t)j;
@@ -2968,7 +3047,9 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                     if (in[j] && !ackr[j]) {              // a run of PS acks needs no read
                         m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
                                      (vl ? l : 0));
+#if !INA_SWITCH_HDR_SHFL
                         h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+#endif
                     }
                 } else {
                     // the stretch of run r holding group gg's row: rows base + gg
@@ -3006,6 +3087,9 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
 #pragma unroll
             for (int j = 0; j < kP; ++j) {
                 if (!__ballot(in[j])) continue;          // no slot of this wave in run r0 + j
+#if INA_SWITCH_HDR_SHFL
+                if constexpr (kSplit) h[j] = group_hdr(hl, g, j);
+#endif
                 if (!in[j]) continue;
                 touched = true;
                 group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, pid[j], m[j], h[j], ackr[j],
@@ -3580,7 +3664,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             // decision chose the path)
             hipLaunchKernelGGL(k_local_lists, dim3((unsigned)std::min<size_t>(sp.nch * kGranPerChunk / kLocU, 2048)),
                                dim3(kLlWaves * 64), 0, s, kc, npk, st->num_slots, ack_hint ? ~kAckBit : 0xFFFFFFFFu,
-                               ax.unsorted, ax.units, loc_gsize, k_out, ax.tab);
+                               ax.unsorted, ax.units, loc_gsize, k_out, ax.tab, actions);
         if (pre) {                                 // the in-order run reads the arrival-order keys
             kn = kc;
             vn = nullptr;

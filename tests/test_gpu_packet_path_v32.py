@@ -57,7 +57,8 @@ def test_packet_path_v32_full_c3_vs_oracle():
         assert int((a[npk:] == orc.ACT_FWD_AGG).sum()) == npk, step       # each slot completes once
         if step > 0:
             assert (a[:npk] == orc.ACT_FWD_ACK).all(), step                # every ack frees its slot
-        assert sw.batch_path((W + 1) * npk) in ("runs", "in_order"), step
+        if step > 0:                                                      # 9 dense runs: no sort
+            assert sw.batch_path((W + 1) * npk) == "runs", step
         want = orc.ps_combine_ina_f32(local, xs_s, k, ws)
         got = upd[ti].cpu().numpy()
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), step

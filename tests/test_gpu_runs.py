@@ -84,7 +84,10 @@ def check_batches(o, V, batches, want_path, use_desc=True, write_dropped=True, n
             fwd = want_act != orc.ACT_DROP
             assert np.array_equal(got[fwd], want_pk[fwd]), i
         if want_path is not None:
-            assert sw_dev.batch_path(len(stream)) == want_path, i
+            # a tuple: any of these paths (V <= 32 batches the near-sorted path may take instead
+            # of the sort -- small batches, whose windows stay within the scan budget)
+            want = want_path if isinstance(want_path, tuple) else (want_path,)
+            assert sw_dev.batch_path(len(stream)) in want, i
         if not regs_each and i < len(batches) - 1:
             continue
         cnt, frag, regs = sw_orc.registers()
@@ -110,7 +113,7 @@ def test_dense_runs_vs_oracle(R, V):
     specs = worker_major(8, per, acks=True) if R == 9 else [(5, per, w) for w in range(R)]
     batches = [runs_batch(rng, V, specs, min(R, 255), stride) for _ in range(3)]
     assert len(batches[0]) > 2048
-    path = "in_order" if R == 1 else "runs" if R <= 64 else "sorted"
+    path = "in_order" if R == 1 else "runs" if R <= 64 else (("sorted", "local") if V <= 32 else "sorted")
     check_batches(o, V, batches, path)
 
 
@@ -410,8 +413,15 @@ def test_wide_key_pools_vs_oracle(num_slots, order):
         elif order == "round_robin":
             b = b.reshape(W, per, stride).transpose(1, 0, 2).reshape(W * per, stride).copy()
         batches.append(b)
-    want = {"shuffled": "sorted", "skewed": "sorted", "worker_major": "runs", "round_robin": "in_order"}[order]
+    sorted_ = ("sorted", "local") if V <= 32 else "sorted"      # small batches: the lists' budget holds
+    want = {"shuffled": sorted_, "skewed": sorted_, "worker_major": "runs", "round_robin": "in_order"}[order]
     check_batches(o, V, batches, want, num_slots=num_slots, regs_each=False)
+    if order in ("shuffled", "skewed"):                      # the 2,048-bin sort itself
+        o.set_tuning(switch_local=False)
+        try:
+            check_batches(o, V, batches, "sorted", num_slots=num_slots, regs_each=False)
+        finally:
+            o.set_tuning(switch_local=True)
     o.set_tuning(switch_sort=3)
     try:
         check_batches(o, V, batches, None, num_slots=num_slots, regs_each=False)
