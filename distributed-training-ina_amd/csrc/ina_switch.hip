@@ -2447,28 +2447,10 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
 #endif
 template <bool kSplit>
 constexpr int kSlotInFlight = kSplit ? INA_SWITCH_SLOT_INFLIGHT_SPLIT : INA_SWITCH_SLOT_INFLIGHT;
-// (lab) split rows: lane l of a group loads the header row of the group's packet k0 + l (one
-// 16-byte load per lane instead of every lane loading every in-flight packet's header), and
-// packet j's header reaches the group's lanes by a permute from lane 8g + j -- the VGPRs that
-// buy more packets in flight (kSlotInFlight up to 8)
-#ifndef INA_SWITCH_HDR_SHFL
-#define INA_SWITCH_HDR_SHFL 0
-#endif
-static_assert(!INA_SWITCH_HDR_SHFL || INA_SWITCH_SLOT_INFLIGHT_SPLIT <= 8, "one header per lane of a group");
-__device__ __forceinline__ u32x4s group_hdr(const u32x4s& hl, int g, int j) {
-    const int src = 8 * g + j;
-    return u32x4s{(uint32_t)__shfl((int)hl.x, src), (uint32_t)__shfl((int)hl.y, src),
-                  (uint32_t)__shfl((int)hl.z, src), (uint32_t)__shfl((int)hl.w, src)};
-}
 // one packet of a lane group's slot (group-uniform: every lane of the group runs it with the
 // same header): ack / collision / count / Processor add, the PS step, the rewritten packet
 // and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
 // header chunk / header row; ack_known: a PS ack by its sort key (then m and h are unread)
-// (lab, timing only -- WRONG results) drop the narrow run's per-packet action bytes (1), its
-// forwarded-payload stores (2) or both (3), to price each store stream
-#ifndef INA_LAB_DROP_STORES
-#define INA_LAB_DROP_STORES 0
-#endif
 template <bool kPs, bool kSplit, int kThr = kSwBlock>
 __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                              size_t stride, uint8_t* __restrict__ pay,
@@ -2560,8 +2542,7 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
                 if constexpr (kSplit) {
                     const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
                                    __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
-                    if (vl && !(INA_LAB_DROP_STORES & 2))
-                        sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid * (size_t)(4 * V)) + l);
+                    if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid * (size_t)(4 * V)) + l);
                 } else {
                     // chunk l + 1: bytes 1..3 of values 4l..4l+3, then byte 0 of value
                     // 4l + 4 (the next lane's; the group's last value lane keeps the
@@ -2587,7 +2568,7 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
         }
     }
     // (drop_written: the near-sorted path's lists kernel stored the drops by position)
-    if (l == 0 && !(INA_LAB_DROP_STORES & 1) && !(drop_written && act == INA_ACT_DROP)) actions[pid] = act;
+    if (l == 0 && !(drop_written && act == INA_ACT_DROP)) actions[pid] = act;
 }
 
 // Narrow packets (V <= 32) in sorted order (the bucket sort's arrays, or a batch already in
@@ -2596,12 +2577,6 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
 // (group g: the g-th head), walking each segment's packets in position order (= arrival
 // order inside the slot, ngaa.p4:120-196) with kP positions' loads in flight.  Per packet the
 // same group_packet as the run-table path; a segment may run past the window's end.
-// (lab) an in-order batch in split NGA-32 rows: the window's 64 payload rows are loaded up
-// front, right behind the keys (they do not depend on them), and staged in LDS, the 64 header
-// rows one per lane; the lane groups then walk their segments from LDS and a permute
-#ifndef INA_SWITCH_INORDER_STAGE
-#define INA_SWITCH_INORDER_STAGE 0
-#endif
 template <bool kPs, bool kSplit>
 __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                     uint8_t* __restrict__ pay, size_t npk, size_t stride,
@@ -2619,36 +2594,12 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
     // written by every lane of the wave: see group_packet on DPP / permutes and EXEC)
     __shared__ uint32_t s_wid[kSwBlock], s_wack[kSwBlock];
     const int wb = (int)threadIdx.x & ~63;
-#if INA_SWITCH_INORDER_STAGE
-    constexpr bool kStage = kSplit;
-    __shared__ u32x4s s_pay[kStage ? kSwBlock / 64 : 1][kStage ? 512 : 1];
-    const bool stage = kStage && ids == nullptr && V == 32 && win == 64;
-    const int wv_ = wave_in_block();
-#else
-    constexpr bool stage = false;
-#endif
     for (size_t w0 = wave * win; w0 < npk; w0 += nwaves * win) {
         const size_t i = w0 + (size_t)lane;
         const uint32_t kr = i < npk ? keys[i] : NS;
         const uint32_t ki = kr & kmask;                   // slot (bit 31: PS-ack hint)
         const uint32_t idw = i < npk ? (ids ? ids[i] : (uint32_t)i) : 0u;
         const uint32_t kp = (i > 0 && i <= npk) ? (keys[i - 1] & kmask) : 0xFFFFFFFFu;
-        u32x4s hrow = {0u, 0u, 0u, 0u};                   // (stage) header row of position lane
-#if INA_SWITCH_INORDER_STAGE
-        if (stage) {                                      // wave-uniform
-            // chunk k*64 + lane = row k*8 + lane/8, chunk lane%8: 1 KiB contiguous per load
-            u32x4s pr[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const size_t q = w0 + (size_t)(k * 8 + (lane >> 3));
-                pr[k] = q < npk ? sw_ld(reinterpret_cast<const u32x4s*>(pay + q * 128) + (lane & 7))
-                                : u32x4s{0u, 0u, 0u, 0u};
-            }
-            if (i < npk) hrow = *reinterpret_cast<const u32x4s*>(pkts + i * 16);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s_pay[wv_][k * 64 + lane] = pr[k];
-        }
-#endif
         const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
         __builtin_amdgcn_wave_barrier();
         s_wid[threadIdx.x] = idw;
@@ -2698,30 +2649,11 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                 u32x4s m[kP], h[kP];
                 uint32_t pid[kP];
                 bool in[kP], acq[kP];
-#if INA_SWITCH_HDR_SHFL
-                u32x4s hl = {0u, 0u, 0u, 0u};             // the header of the group's packet k0 + l
-                if constexpr (kSplit) {
-                    const uint32_t kl = k0 + (uint32_t)l, ql = hst + kl;
-                    if (!stage && has && l < kP && kl < hlen) {
-                        const uint32_t pl = ql < 64u ? s_wid[wb + (int)ql]
-                                                     : (ids ? ids[w0 + ql] : (uint32_t)(w0 + ql));
-                        const bool al = ql < 64u ? s_wack[wb + (int)ql] != 0u : (keys[w0 + ql] & ~kmask) != 0u;
-                        if (!al) hl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pl * 16);
-                    }
-                }
-#endif
 #pragma unroll
                 for (int j = 0; j < kP; ++j) {
                     const uint32_t k = k0 + (uint32_t)j;
                     const uint32_t q = hst + k;           // window-relative position
                     in[j] = has && k < hlen;
-                    if (stage) {                          // every lane: the permute's sources
-                        const int src = (int)(q < 64u ? q : 0u);
-                        h[j].x = (uint32_t)__shfl((int)hrow.x, src);
-                        h[j].y = (uint32_t)__shfl((int)hrow.y, src);
-                        h[j].z = (uint32_t)__shfl((int)hrow.z, src);
-                        h[j].w = (uint32_t)__shfl((int)hrow.w, src);
-                    }
                     // id and ack hint: the window's (LDS), past the window from memory
                     pid[j] = 0u;
                     acq[j] = false;
@@ -2737,17 +2669,9 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                     }
                     if (in[j] && !acq[j]) {
                         if constexpr (kSplit) {
-#if INA_SWITCH_INORDER_STAGE
-                            if (stage && q < 64u) {
-                                m[j] = s_pay[wv_][q * 8u + (uint32_t)(vl ? l : 0)];
-                                continue;
-                            }
-#endif
                             m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
                                          (vl ? l : 0));
-#if !INA_SWITCH_HDR_SHFL
                             h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
-#endif
                         } else {
                             const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
                             m[j] = sw_ld(pk + (vl ? l + 1 : 1));
@@ -2758,10 +2682,6 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
 #pragma unroll
                 for (int j = 0; j < kP; ++j) {
                     if (!__ballot(in[j])) continue;
-#if INA_SWITCH_HDR_SHFL
-                    if constexpr (kSplit)
-                        if (!stage) h[j] = group_hdr(hl, g, j);   // every lane (a permute)
-#endif
                     if (!in[j]) continue;
                     group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, hslot, pid[j], m[j], h[j], acq[j],
                                               cnt, frag, reg, have_reg);
@@ -2822,21 +2742,9 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
         }
         u32x4s reg = {0u, 0u, 0u, 0u};
         bool have_reg = false;
-#if INA_SWITCH_HDR_SHFL
-        u32x4s hl = {0u, 0u, 0u, 0u};                                 // the header of entry (k0 & ~7) + l
-#endif
         for (uint32_t k0 = 0; k0 < maxlen; k0 += kP) {
             if (k0 && (k0 & 7u) == 0)                              // entries k0..k0+7
                 idl = k0 + (uint32_t)l < hlen ? ids[hst + k0 + (uint32_t)l] : 0u;
-#if INA_SWITCH_HDR_SHFL
-            if constexpr (kSplit) {
-                if ((k0 & 7u) == 0) {
-                    hl = u32x4s{0u, 0u, 0u, 0u};
-                    if (k0 + (uint32_t)l < hlen && (idl & kAckBit) == 0u)
-                        hl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)idl * 16);
-                }
-            }
-#endif
             u32x4s m[kP], h[kP];
             uint32_t pid[kP];
             bool in[kP], acq[kP];
@@ -2850,9 +2758,7 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
                 if (in[j] && !acq[j]) {
                     if constexpr (kSplit) {
                         m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) + (vl ? l : 0));
-#if !INA_SWITCH_HDR_SHFL
                         h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
-#endif
                     } else {
                         const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
                         m[j] = sw_ld(pk + (vl ? l + 1 : 1));
@@ -2863,9 +2769,6 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
 #pragma unroll
             for (int j = 0; j < kP; ++j) {
                 if (!__ballot(in[j])) continue;
-#if INA_SWITCH_HDR_SHFL
-                if constexpr (kSplit) h[j] = group_hdr(hl, g, (int)((k0 + (uint32_t)j) & 7u));
-#endif
                 if (!in[j]) continue;
                 group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, pid[j], m[j], h[j], acq[j], cnt,
                                           frag, reg, have_reg, true);
@@ -3020,18 +2923,6 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
             u32x4s m[kP], h[kP];
             uint32_t pid[kP];
             bool in[kP], ackr[kP];
-#if INA_SWITCH_HDR_SHFL
-            u32x4s hl = {0u, 0u, 0u, 0u};                 // the header of run r0 + l's packet
-            if constexpr (kSplit) {
-                const uint32_t r = r0 + (uint32_t)l;
-                const int rr = (int)(r < R ? r : 0u);
-                const uint32_t rs = (uint32_t)__shfl((int)rslot, rr), rl = (uint32_t)__shfl((int)rlen, rr);
-                const uint32_t rp = (uint32_t)__shfl((int)rpos, rr), ra = (uint32_t)__shfl((int)rack_u, rr);
-                const uint32_t off = slot - rs;
-                if (l < kP && r < R && sv && off < rl && ra == 0u)
-                    hl = *reinterpret_cast<const u32x4s*>(pkts + (size_t)(rp + off) * 16);
-            }
-#endif
 #pragma unroll
             for (int j = 0; j < kP; ++j) {
                 const uint32_t r = r0 + (uint32_t)j;
@@ -3047,9 +2938,7 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                     if (in[j] && !ackr[j]) {              // a run of PS acks needs no read
                         m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
                                      (vl ? l : 0));
-#if !INA_SWITCH_HDR_SHFL
                         h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
-#endif
                     }
                 } else {
                     // the stretch of run r holding group gg's row: rows base + gg
@@ -3087,9 +2976,6 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
 #pragma unroll
             for (int j = 0; j < kP; ++j) {
                 if (!__ballot(in[j])) continue;          // no slot of this wave in run r0 + j
-#if INA_SWITCH_HDR_SHFL
-                if constexpr (kSplit) h[j] = group_hdr(hl, g, j);
-#endif
                 if (!in[j]) continue;
                 touched = true;
                 group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, pid[j], m[j], h[j], ackr[j],
