@@ -785,7 +785,10 @@ constexpr uint32_t kLocU = INA_LOC_U;
 constexpr int kLlWaves = 4;                                   // waves per unit in the list build
 constexpr int kLlBins = 1024;                                 // slots one LDS pass counts
 constexpr int kLlBits = 10;
-constexpr int kLlRounds = 16;                                 // key rounds a lane holds
+#ifndef INA_LL_ROUNDS
+#define INA_LL_ROUNDS 20      // a J = 64 unit window (5 granules) held: 310.1 -> 304.3 us (r05v)
+#endif
+constexpr int kLlRounds = INA_LL_ROUNDS;                      // key rounds a lane holds
 
 // wave-wide inclusive max (lane i: max over lanes <= i) and suffix min (lane i: min over lanes >= i)
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
@@ -964,7 +967,10 @@ __device__ __forceinline__ bool local_decide(const uint32_t* __restrict__ gmin, 
 // lanes of the same slot (a stable counting sort).  ids[e] = packet | PS-ack bit 31 (by its sort
 // key).
 __device__ __forceinline__ size_t switch_block_index();
-__global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_local_lists(const uint32_t* __restrict__ keys, size_t npk,
+#ifndef INA_LL_WAVES_PER_EU
+#define INA_LL_WAVES_PER_EU 8
+#endif
+__global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(INA_LL_WAVES_PER_EU, 8))) void k_local_lists(const uint32_t* __restrict__ keys, size_t npk,
                                                                uint32_t num_slots, uint32_t kmask,
                                                                const uint32_t* __restrict__ unsorted,
                                                                const LocUnit* __restrict__ units, uint32_t gsize,
