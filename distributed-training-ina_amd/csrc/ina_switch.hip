@@ -3671,13 +3671,10 @@ static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t
     bool fused = false;
     if (int rc = switch_process_impl(st, pkts, npk, stride, desc, actions, scratch, stream, ps, &fused, phase, pay))
         return rc;
+    // the checks above admit only the layouts the register-resident run kernels take, so the
+    // PS step always runs fused (ack_desc: exactly the rows the call writes, in every layout)
     if (fused || phase == INA_SWITCH_SORT) return INA_OK;         // (a sort alone: the PS step runs with the run)
-    if (pay) return set_error(INA_EHIP, "split rows: the PS step was not fused%s", "");
-    // layouts the register-resident run kernel does not take: the two steps one by one
-    if (int rc = ina_apply_completed_nga(pkts, npk, st->V, stride, actions, seq0, local, k, weight_step, out,
-                                         n, acks, ack_stride, stream))
-        return rc;
-    return ack_desc ? ina_nga_descriptors(acks, nslots, ack_stride, ack_desc, stream) : INA_OK;
+    return set_error(INA_EHIP, "internal: the PS step was not fused%s", "");
 }
 
 int ina_switch(const ina_switch_state_t* st, const ina_switch_batch_t* b, const ina_switch_ps_t* ps, int phase,

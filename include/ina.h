@@ -314,11 +314,11 @@ typedef struct ina_switch_batch {
  * (the packet's header with is_ack = 1, fragcheck.p4:26-31) -- the same results as the switch
  * followed by ina_apply_completed_nga.  acks: ack rows ack_stride bytes apart (NULL: none;
  * split rows: header rows, ack_stride 16 or 0); ack_desc (may be NULL; needs acks): each ack
- * row's descriptor beside it, for every row the call writes, so the next batch -- these acks
- * in front of the next step's packets -- is sorted without a gather pass (layouts the fused
- * run kernel does not take -- unaligned packed rows -- apply afterwards and then refresh the
- * descriptors of all ceil(n/V) rows).  keep_forwarded = 0: completed packets are consumed and
- * their buffers left as they arrived.  Replaces the Tofino -> PS hop of ngaa.p4:170-175 +
+ * row's descriptor beside it, for exactly the rows the call writes, so the next batch -- these
+ * acks in front of the next step's packets -- is sorted without a gather pass.  The step always
+ * runs fused in the switch's run kernel (the layouts below are the ones it takes; others are
+ * refused before the switch touches its state).  keep_forwarded = 0: completed packets are
+ * consumed and their buffers left as they arrived.  Replaces the Tofino -> PS hop of ngaa.p4:170-175 +
  * NGAPacket.py:62-143 + launch.py:42-52 when both live on the GPU.  16-byte aligned local,
  * out, rows and registers; V % 4 == 0. */
 typedef struct ina_switch_ps {
