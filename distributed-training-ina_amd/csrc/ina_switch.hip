@@ -3097,8 +3097,16 @@ __device__ __forceinline__ size_t switch_block_index() {
 #endif
 }
 
+// occupancy target of the narrow split-row run without the PS step: 8 waves per SIMD takes its
+// SGPRs to the 80 that admit 8 blocks per CU (8 spilled to VGPR lanes; 86 admitted 7)
+#ifndef INA_SWITCH_WAVES_RUN_NS
+#define INA_SWITCH_WAVES_RUN_NS 8     // NGA-32 C3 split: worker-major 232.2 -> 223.0, round-robin 259.2 -> 252.6 us (r05x)
+#endif
+#ifndef INA_SWITCH_WAVES_PS_NS
+#define INA_SWITCH_WAVES_PS_NS 8      // NGA-32 packet path: switch + PS 329.3 -> 297.6 us, step 636.9 -> 608.9 (r05y)
+#endif
 template <bool kPs, bool kNarrow, bool kSplit>
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? INA_SWITCH_WAVES : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? ((kNarrow && kSplit) ? INA_SWITCH_WAVES_PS_NS : INA_SWITCH_WAVES) : (kNarrow && kSplit) ? INA_SWITCH_WAVES_RUN_NS : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts,
                                                           uint8_t* __restrict__ pay, size_t npk,
                                                           size_t stride,
