@@ -3,7 +3,8 @@ the switch pass (the 8 workers' fused quantise+packs in one launch, one ina_swit
 [last step's acks | 8 x 102,400 NGA-256 packets]); run under rocprofv3 --kernel-trace
 --stats for the per-kernel breakdown of bench_extra's last packet-path row).  The run kernel
 writes the ack rows' descriptors (ack_desc), as bench.py's packet_path does.  SPLIT=1: the
-same step over split rows (16-byte header rows + 1 KiB payload rows)."""
+same step over split rows (16-byte header rows + 1 KiB payload rows).  V=32: NGA-32 packets
+(8 x 819,200 + 819,200 acks, a 2^20-slot pool), bench.py's packet_path_v32."""
 import os
 import sys
 
@@ -13,7 +14,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "distributed-training-ina_amd"))
 from ina_amd import ops  # noqa: E402
 
-n, W, V, slots = 26_214_400, 8, 256, 1 << 17
+n, W = 26_214_400, 8
+V = int(os.environ.get("V", 256))
+slots = (1 << 17) if V == 256 else (1 << 20)
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(3)
 xs = [torch.randn(n, device=dev, generator=g) * 1e-2 for _ in range(W)]
