@@ -19,6 +19,9 @@ import pytest
 from tests.conftest import REPO
 from tests._dist_gpu_rank import bucket
 
+# the ranks load the library this run tests (INA_LIBRARY: a checked variant build)
+LIB_NAME = os.path.basename(os.environ.get("INA_LIBRARY", "libina.so"))
+
 RANK_SCRIPT = os.path.join(REPO, "tests", "_dist_gpu_rank.py")
 
 
@@ -56,7 +59,7 @@ def test_sharded_i32_two_ranks_device_kernels(tmp_path, world, n, coll):
     want = orc.dequantize_i32(want_int, k)
     for r, d in enumerate(res):
         assert int(d["world"][0]) == world
-        assert d["lib"][0].endswith("libina.so")
+        assert d["lib"][0].endswith(LIB_NAME)
         assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want_int[lo:hi])
@@ -98,7 +101,7 @@ def test_range_layout_b_i32_device_kernels(tmp_path, world, n, W):
     want_int = orc.quantize_reduce_i32([bucket(w, n, "i32") for w in range(W)], k)
     want = orc.dequantize_i32(want_int, k)
     for r, d in enumerate(res):
-        assert d["lib"][0].endswith("libina.so")
+        assert d["lib"][0].endswith(LIB_NAME)
         assert np.array_equal(d["full"].view(np.uint32), want.view(np.uint32)), f"rank {r}"
         lo, hi = d["range"]
         assert np.array_equal(d["shard"], want_int[lo:hi])
