@@ -1325,6 +1325,10 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
         v[r] = (uint32_t)p;
         if (kMode != 2 && p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
+        // a batch this pass sorts: every packet of this switch starts as a drop, by position, so
+        // the narrow run stores only the other actions (1 in W) -- scattered byte stores in
+        // sorted order wrote back a line each (shuffled NGA-32 run kernel: 440 MB written, r05e)
+        if (kMode == 2 && p < npk && mine) actions[p] = INA_ACT_DROP;
         if constexpr (kMode != 1) {
             if constexpr (kHalf) lds_count_half(base[wv >> 1], (key >> lb) & (nb - 1), p < npk, (wv & 1) * 16);
             else lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
@@ -2589,7 +2593,8 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                                                     const uint32_t* __restrict__ keys,
                                                     const uint32_t* __restrict__ ids,
                                                     uint8_t* __restrict__ actions, uint32_t win, uint32_t kmask,
-                                                    const PsFuse& ps, size_t wave, size_t nwaves) {
+                                                    const PsFuse& ps, size_t wave, size_t nwaves,
+                                                    bool drop_written = false) {
     constexpr int kP = kSlotInFlight<kSplit>;
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, l = lane & 7;
@@ -2690,7 +2695,7 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                     if (!__ballot(in[j])) continue;
                     if (!in[j]) continue;
                     group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, hslot, pid[j], m[j], h[j], acq[j],
-                                              cnt, frag, reg, have_reg);
+                                              cnt, frag, reg, have_reg, drop_written);
                 }
             }
             if (has && l == 0) {
@@ -2797,11 +2802,11 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                                  const uint32_t* __restrict__ ids,
                                                  uint8_t* __restrict__ actions, uint32_t win,
                                                  uint32_t kmask, const PsFuse& ps, size_t wave,
-                                                 size_t nwaves) {
+                                                 size_t nwaves, bool drop_written = false) {
 #if INA_SWITCH_NARROW_SLOTS
     if constexpr (kNarrow) {
         window_slots_narrow<kPs, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps, wave,
-                                         nwaves);
+                                         nwaves, drop_written);
         return;
     }
 #endif
@@ -3119,8 +3124,9 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                           const uint32_t* __restrict__ ids_a,
                                                           const uint32_t* __restrict__ unsorted,
                                                           const uint32_t* __restrict__ loc_ids,
-                                                          const uint2* __restrict__ loc_tab) {
+                                                          const uint2* __restrict__ loc_tab, int drop_prefill) {
     const size_t wave = switch_block_index() * (kSwBlock / 64) + wave_in_block();
+    bool sorted_batch = false;                            // (drop_prefill: its digit pass stored the drops)
     const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
     // (unsorted[1]: the epoch of the sort that filled the scratch, written by its chunk pass,
     // so a run queued apart from its sort needs no host-side state)
@@ -3144,13 +3150,15 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
             switch_runs_body<kPs, kNarrow, kSplit>(st, pkts, stride, pay, actions, kmask, ps,
                                                    unsorted + (kCtlRuns - kCtlEpochs), wave, nwaves);
             return;
+        } else {
+            sorted_batch = true;
         }
     }
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
     switch_run2_body<kPs, false, kNarrow, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps,
-                                                  wave, nwaves);
+                                                  wave, nwaves, drop_prefill != 0 && sorted_batch);
 }
 
 // batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
@@ -3445,6 +3453,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     const uint32_t* unsorted = nullptr;     // bucket sort: the run kernel may read A's output
     uint32_t epoch = 0;
     uint32_t loc_gsize = 0;                 // the near-sorted path's granule: 1/8 of a sort chunk
+    bool drop_prefill = false;              // the digit pass (mode 2) stores a sorted batch's drops
     if (small && fast && npk <= (size_t)t.tiny_max) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
         if (!do_run) return INA_OK;
@@ -3495,6 +3504,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // keys of 19-22 bits (2,048-bin digits) with the register-resident run kernel: the
         // chunk pass split in two (detection, then decision + digits), so structured batches skip the digits
         const bool pre = (sp.wide || t.pre_all) && fast;
+        drop_prefill = pre;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
@@ -3639,7 +3649,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                           : (ps.on ? (narrow ? &k_switch_run2<true, true, false> : &k_switch_run2<true, false, false>)
                                    : (narrow ? &k_switch_run2<false, true, false> : &k_switch_run2<false, false, false>));
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, pay, npk, stride, kc, vc, actions,
-                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted, k_out, ax.tab);
+                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted, k_out, ax.tab,
+                           drop_prefill ? 1 : 0);
         *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
