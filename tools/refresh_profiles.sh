@@ -3,15 +3,15 @@
 # swtrace:SPLIT=1 swpmc:SPLIT=1 pathtrace:SPLIT=1 pathpmc:SPLIT=1 pathtrace:SPLIT=0
 # swtrace:V=32,SLOTS=1048576,ORDER=wm [...]) into profiles/<round> and regenerate the traffic
 # summaries.  Stages that did not run are skipped.
-# usage: tools/refresh_profiles.sh TAG        (INA_EVIDENCE_ROUND=r04 by default)
+# usage: tools/refresh_profiles.sh TAG        (INA_EVIDENCE_ROUND=r05 by default)
 set -eu
 TAG=$1
 S=gpurun_out/$TAG
-D=profiles/${INA_EVIDENCE_ROUND:-r04}
+D=profiles/${INA_EVIDENCE_ROUND:-r05}
 mkdir -p "$D/pmc"
 cpif() { [ -f "$1" ] && cp "$1" "$2" || true; }
 cpif "$S/bench.json" "$D/bench.json"
-for f in pytest_gpu.log contract.log smoke.log; do cpif "$S/$f" "$D/$f"; done
+for f in pytest_gpu.log pytest_gpu_storecheck.log contract.log smoke.log; do cpif "$S/$f" "$D/$f"; done
 cpif "$S/prof/run_kernel_stats.csv" "$D/kernel_stats_bench.csv"
 for c in FETCH_SIZE WRITE_SIZE; do
   cpif "$S/pmc_$c/run_counter_collection.csv" "$D/pmc/bench_$c.csv"
@@ -35,4 +35,12 @@ cpif "$S/rehearse2.json" "$D/rehearse_2ranks_gloo.json"
 cpif "$S/sharded1_i32.json" "$D/sharded_c5_1gpu_i32.json"
 cpif "$S/sharded1_i16.json" "$D/sharded_c5_1gpu_i16.json"
 cpif "$S/config1.log" "$D/config1_loopback.log"
+# every switch / packet-path trace and PMC pass of the session (swtrace:K=V,.. swpmc:K=V,..
+# pathtrace:K=V,..), named after its env
+for d in "$S"/swtrace_* "$S"/pathtrace_*; do
+  [ -f "$d/run_kernel_stats.csv" ] && cp "$d/run_kernel_stats.csv" "$D/kernel_stats_$(basename "$d").csv"
+done
+for d in "$S"/swpmc_*; do
+  [ -f "$d/run_counter_collection.csv" ] && cp "$d/run_counter_collection.csv" "$D/pmc/$(basename "$d").csv"
+done
 echo "profiles refreshed from $TAG into $D"
