@@ -429,6 +429,45 @@ def test_wide_key_pools_vs_oracle(num_slots, order):
         o.set_tuning(switch_sort=0)
 
 
+@pytest.mark.parametrize("acks", [False, True])
+@pytest.mark.parametrize("num_slots", [1 << 18, 1 << 20, (1 << 21) - 1])
+def test_wide_key_split_sorted_vs_oracle(num_slots, acks):
+    """Shuffled NGA-32 batches in split rows over pools of 19-22-bit keys -- the 2,048-bin sort
+    and the narrow sorted run over 16-byte header rows + 128-byte payload rows, the near-sorted
+    path off.  Against the P4 restatement with 2 % collisions, 2 % other degrees and PS acks:
+    actions, the header rows (collision flags), the payload rows (dropped packets rewritten
+    too) and the registers, state carried across batches."""
+    o = ops()
+    rng = np.random.default_rng(num_slots % 997 + acks)
+    V, W, per = 32, 8, 1500
+    stride = o.nga_stride(V)
+    seq0 = int(rng.integers(0, num_slots))
+    specs = ([(seq0, per, "ack")] if acks else []) + [(seq0, per, w) for w in range(W)]
+    sw_dev = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=True)
+    sw_orc = orc.Switch(V, num_slots=num_slots, switch_id=1)
+    o.set_tuning(switch_local=False)                  # the sort itself (small batches fit the lists)
+    try:
+        for i in range(2):
+            b = runs_batch(rng, V, specs, W, stride, num_slots=num_slots)
+            b = b[rng.permutation(len(b))]
+            want_pk, want_act = sw_orc.run(b, stride=stride)
+            hdr = np.zeros((len(b), 16), np.uint8)
+            hdr[:, :15] = b[:, :15]
+            hd, pd = dev(hdr), dev(np.ascontiguousarray(b[:, 15:15 + 4 * V]))
+            act = sw_dev.process_split(hd, pd, desc=o.nga_descriptors(dev(b)))
+            assert sw_dev.batch_path(len(b)) == "sorted", i
+            assert np.array_equal(host(act), want_act), i
+            assert np.array_equal(host(hd)[:, :15], want_pk[:, :15]), i
+            assert np.array_equal(host(pd), want_pk[:, 15:15 + 4 * V]), i
+            assert (want_act == orc.ACT_FWD_COLLISION).any(), i
+    finally:
+        o.set_tuning(switch_local=True)
+    cnt, frag, regs = sw_orc.registers()
+    assert np.array_equal(host(sw_dev.count), cnt)
+    assert np.array_equal(host(sw_dev.frag).view(np.uint32), frag)
+    assert np.array_equal(host(sw_dev.regs).view(np.uint32), regs)
+
+
 @pytest.mark.parametrize("tile", [0, 8])
 def test_wide_key_multi_tile_buckets(tile):
     """2^20-slot pool, 24,000 packets in slots 0..2,999 (three 1,024-slot buckets of 8,000
