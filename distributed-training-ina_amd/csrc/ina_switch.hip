@@ -2452,11 +2452,25 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
 #ifndef INA_SWITCH_SLOT_INFLIGHT
 #define INA_SWITCH_SLOT_INFLIGHT 2
 #endif
+#ifndef INA_PACKED_UNALIGNED
+#define INA_PACKED_UNALIGNED 1
+#endif
 #ifndef INA_SWITCH_SLOT_INFLIGHT_SPLIT
 #define INA_SWITCH_SLOT_INFLIGHT_SPLIT 1
 #endif
 template <bool kSplit>
 constexpr int kSlotInFlight = kSplit ? INA_SWITCH_SLOT_INFLIGHT_SPLIT : INA_SWITCH_SLOT_INFLIGHT;
+// Packed rows (the payload at byte 15 of the row): a lane's four values are one 16-byte access at
+// byte 15 + 16 l -- an unaligned global load / store (gfx950 runs HSA code in unaligned access
+// mode; the compiler emits one dwordx4 with offset 15) instead of the aligned chunk l + 1 and the
+// neighbour lane's word through LDS
+__device__ __forceinline__ u32x4s ld_row16(const uint8_t* p) {
+    u32x4s v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+__device__ __forceinline__ void st_row16(uint8_t* p, const u32x4s& v) { __builtin_memcpy(p, &v, 16); }
+
 // one packet of a lane group's slot (group-uniform: every lane of the group runs it with the
 // same header): ack / collision / count / Processor add, the PS step, the rewritten packet
 // and its action byte.  m: this lane's payload chunk (packed rows: row chunk l + 1), h: the
@@ -2496,7 +2510,7 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
             if (cnt == hcount) cnt = 0;
             const bool first = cnt == 1u;
             u32x4s v;                        // values 4l..4l+3
-            if constexpr (kSplit) {
+            if constexpr (kSplit || INA_PACKED_UNALIGNED) {
                 v.x = __builtin_bswap32(m.x); v.y = __builtin_bswap32(m.y);
                 v.z = __builtin_bswap32(m.z); v.w = __builtin_bswap32(m.w);
             } else {
@@ -2553,6 +2567,10 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
                     const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
                                    __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
                     if (vl) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pid * (size_t)(4 * V)) + l);
+                } else if constexpr (INA_PACKED_UNALIGNED) {
+                    const u32x4s e{__builtin_bswap32(reg.x), __builtin_bswap32(reg.y),
+                                   __builtin_bswap32(reg.z), __builtin_bswap32(reg.w)};
+                    if (vl) st_row16(pkts + (size_t)pid * stride + 15 + 16 * l, e);
                 } else {
                     // chunk l + 1: bytes 1..3 of values 4l..4l+3, then byte 0 of value
                     // 4l + 4 (the next lane's; the group's last value lane keeps the
@@ -2685,7 +2703,10 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                             h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
                         } else {
                             const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
-                            m[j] = sw_ld(pk + (vl ? l + 1 : 1));
+                            if constexpr (INA_PACKED_UNALIGNED)
+                                m[j] = ld_row16(pkts + (size_t)pid[j] * stride + 15 + 16 * (vl ? l : 0));
+                            else
+                                m[j] = sw_ld(pk + (vl ? l + 1 : 1));
                             h[j] = *pk;
                         }
                     }
@@ -2772,7 +2793,10 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
                         h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
                     } else {
                         const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
-                        m[j] = sw_ld(pk + (vl ? l + 1 : 1));
+                        if constexpr (INA_PACKED_UNALIGNED)
+                            m[j] = ld_row16(pkts + (size_t)pid[j] * stride + 15 + 16 * (vl ? l : 0));
+                        else
+                            m[j] = sw_ld(pk + (vl ? l + 1 : 1));
                         h[j] = *pk;
                     }
                 }
@@ -2978,7 +3002,16 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
 #pragma unroll
                 for (int j = 0; j < kP; ++j) {
                     if (in[j] && !ackr[j]) {
-                        m[j] = s_stage[wb][j][g * cpr + (vl ? l + 1 : 1)];
+                        if constexpr (INA_PACKED_UNALIGNED) {
+                            // the lane's bytes 15 + 16 l .. 30 + 16 l (group_packet's packed-row
+                            // form): chunk l's last byte, then chunk l + 1's first fifteen
+                            const u32x4s c0 = s_stage[wb][j][g * cpr + (vl ? l : 0)];
+                            const u32x4s c1 = s_stage[wb][j][g * cpr + (vl ? l + 1 : 1)];
+                            m[j] = u32x4s{__builtin_amdgcn_alignbyte(c1.x, c0.w, 3), __builtin_amdgcn_alignbyte(c1.y, c1.x, 3),
+                                          __builtin_amdgcn_alignbyte(c1.z, c1.y, 3), __builtin_amdgcn_alignbyte(c1.w, c1.z, 3)};
+                        } else {
+                            m[j] = s_stage[wb][j][g * cpr + (vl ? l + 1 : 1)];
+                        }
                         h[j] = s_stage[wb][j][g * cpr];
                     }
                 }
