@@ -2443,14 +2443,17 @@ __device__ __forceinline__ void run_segment_narrow(const ina_switch_state_t& st,
         __builtin_nontemporal_store(reg, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
 }
 
-// packets' loads in flight per lane group (the VGPRs buy occupancy): 2 for packed rows, 1 for
-// split rows.  Interleaved A/Bs at NGA-32 C3 size (profiles/r04/lab/slot_inflight_ab_v32_*.log):
+// packets' loads in flight per lane group (the VGPRs buy occupancy): 1 for packed and for split
+// rows.  Interleaved A/Bs at NGA-32 C3 size (profiles/r04/lab/slot_inflight_ab_v32_*.log):
 // 2 against 4 -- worker-major split 274.6 -> 260.7 us, round-robin packed 390.8 -> 374.7,
 // shuffled 757.9 -> 734.8, the rest equal (8 spills: 2-3x slower); 1 against 2 -- split rows
 // worker-major 258.6 -> 220.8, round-robin 285.9 -> 252.1, shuffled 646 -> 642, packed rows
 // 4-7 % slower (3: no better than 2)
+// (round 5: packed rows read as one unaligned 16-byte access per lane, no LDS exchange -- 1 in
+// flight at 8 waves per SIMD: round-robin 337.2 -> 329.5 us, jitter 64 398.4 -> 365.5 us,
+// worker-major and shuffled equal; 2 at 8 waves spills, profiles/r05/lab/packed_inflight_waves_ab_v32.log)
 #ifndef INA_SWITCH_SLOT_INFLIGHT
-#define INA_SWITCH_SLOT_INFLIGHT 2
+#define INA_SWITCH_SLOT_INFLIGHT 1
 #endif
 #ifndef INA_PACKED_UNALIGNED
 #define INA_PACKED_UNALIGNED 1
@@ -3144,7 +3147,10 @@ __device__ __forceinline__ size_t switch_block_index() {
 #define INA_SWITCH_WAVES_PS_NS 8      // NGA-32 packet path: switch + PS 329.3 -> 297.6 us, step 636.9 -> 608.9 (r05y)
 #endif
 template <bool kPs, bool kNarrow, bool kSplit>
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? ((kNarrow && kSplit) ? INA_SWITCH_WAVES_PS_NS : INA_SWITCH_WAVES) : (kNarrow && kSplit) ? INA_SWITCH_WAVES_RUN_NS : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
+#ifndef INA_SWITCH_WAVES_RUN_NP
+#define INA_SWITCH_WAVES_RUN_NP 8     // narrow packed rows (with 1 packet in flight, see kSlotInFlight)
+#endif
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? ((kNarrow && kSplit) ? INA_SWITCH_WAVES_PS_NS : INA_SWITCH_WAVES) : (kNarrow && kSplit) ? INA_SWITCH_WAVES_RUN_NS : kNarrow ? INA_SWITCH_WAVES_RUN_NP : INA_SWITCH_WAVES_RUN, 8))) void k_switch_run2(ina_switch_state_t st,
                                                           uint8_t* __restrict__ pkts,
                                                           uint8_t* __restrict__ pay, size_t npk,
                                                           size_t stride,
