@@ -974,8 +974,7 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
                                                                uint32_t num_slots, uint32_t kmask,
                                                                const uint32_t* __restrict__ unsorted,
                                                                const LocUnit* __restrict__ units, uint32_t gsize,
-                                                               uint32_t* __restrict__ ids, uint2* __restrict__ tab,
-                                                               uint8_t* __restrict__ actions) {
+                                                               uint32_t* __restrict__ ids, uint2* __restrict__ tab) {
     constexpr int kThr = kLlWaves * 64;
     constexpr int DPT = kLlBins / kThr;                           // consecutive slots a thread scans
     __shared__ uint32_t cw[kLlWaves / 2][kLlBins];                // per-wave counts, then cursors
@@ -989,13 +988,7 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
     const uint32_t kmin = unsorted[kLocKmin], nunits = unsorted[kLocUnits];
     for (uint32_t u = (uint32_t)switch_block_index(); u < nunits; u += gridDim.x) {
         const LocUnit w = units[u];
-        if (w.hi <= w.lo) {                                       // no slot (block-uniform): only
-            const uint32_t Pu = u * kLocU * gsize;                // its positions' drops
-            const uint32_t P1 = (uint32_t)min((size_t)Pu + (size_t)kLocU * gsize, npk);
-            for (uint32_t p = Pu + threadIdx.x; p < P1; p += kLlWaves * 64)
-                if ((keys[p] & kmask) < num_slots) actions[p] = INA_ACT_DROP;
-            continue;
-        }
+        if (w.hi <= w.lo) continue;                               // no slot (block-uniform)
         LOC_STAMP(0);
         // positions fit 32 bits (npk <= 2^31 - 1)
         const uint32_t P0 = w.g_lo * gsize, Pu = u * kLocU * gsize;
@@ -1031,10 +1024,6 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
                     const uint32_t p = r0 + (uint32_t)(r * 64 + lane);
                     lds_count_half(crow, slot - q, slot < num_slots && slot - q < qn, sh);
                     before += (p < Pu && p < b1 && (slot < w.lo || slot >= num_slots)) ? 1u : 0u;
-                    // the unit's own positions: every packet of this switch starts as a drop, so
-                    // the run stores only the other actions (1 in W) -- scattered byte stores
-                    // by list order cost 29 us at NGA-32 C3 size, these are by position
-                    if (q == w.lo && p >= Pu && p < b1 && slot < num_slots) actions[p] = INA_ACT_DROP;
                 }
             }
             if (q == w.lo) {
@@ -1324,11 +1313,13 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         // bit 31 carries "PS ack" through the sort (no digit reads it)
         k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
         v[r] = (uint32_t)p;
-        if (kMode != 2 && p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
-        // a batch this pass sorts: every packet of this switch starts as a drop, by position, so
-        // the narrow run stores only the other actions (1 in W) -- scattered byte stores in
-        // sorted order wrote back a line each (shuffled NGA-32 run kernel: 440 MB written, r05e)
-        if (kMode == 2 && p < npk && mine) actions[p] = INA_ACT_DROP;
+        if (kMode == 0 && p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
+        // the detection pass stores EVERY packet's action byte by position: foreign packets
+        // forwarded, this switch's starting as drops -- so a sorted or near-sorted run stores only
+        // the other actions (1 in W): scattered byte stores in slot / list order wrote back a line
+        // each (shuffled NGA-32 run kernel: 440 MB written, r05e); the in-order and run-table
+        // paths store every action anyway
+        if (kMode == 1 && p < npk) actions[p] = mine ? INA_ACT_DROP : INA_ACT_FWD_OTHER;
         if constexpr (kMode != 1) {
             if constexpr (kHalf) lds_count_half(base[wv >> 1], (key >> lb) & (nb - 1), p < npk, (wv & 1) * 16);
             else lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
@@ -1968,7 +1959,8 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
                                             size_t stride, uint8_t* __restrict__ pay,
                                             uint8_t* __restrict__ actions, const PsFuse& ps,
                                             uint32_t slot, bool ack_led, size_t q_begin, size_t q_end,
-                                            PidFn&& pid_batch) {
+                                            PidFn&& pid_batch, bool drop_written = false) {
+    // (drop_written: the detection pass stored every packet's drop by position)
     constexpr bool kActBatch = INA_SWITCH_ACT_BATCH;
     const int lane = threadIdx.x & 63;
     const int V = st.V;
@@ -2164,10 +2156,10 @@ __device__ __forceinline__ void run_segment(const ina_switch_state_t& st, uint8_
                 }
             }
             if constexpr (kActBatch) act_v = lane == b ? (uint32_t)act : act_v;
-            else if (lane == 0) actions[pid[b]] = act;
+            else if (lane == 0 && !(drop_written && act == INA_ACT_DROP)) actions[pid[b]] = act;
         }
-        if constexpr (kActBatch)
-            if (lane < nb) actions[mypid] = (uint8_t)act_v;   // one store for the batch
+        if constexpr (kActBatch)                      // one store for the batch
+            if (lane < nb && !(drop_written && act_v == INA_ACT_DROP)) actions[mypid] = (uint8_t)act_v;
     }
     if (lane == 0) {
         st.count[slot] = (uint8_t)cnt;
@@ -2598,7 +2590,7 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
             }
         }
     }
-    // (drop_written: the near-sorted path's lists kernel stored the drops by position)
+    // (drop_written: the detection pass stored the drops by position)
     if (l == 0 && !(drop_written && act == INA_ACT_DROP)) actions[pid] = act;
 }
 
@@ -2905,7 +2897,7 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                             pos + (ack_led ? 1 : 0), end, pids);
         else
             run_segment<kPs, kLat, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led,
-                                           pos + (ack_led ? 1 : 0), end, pids);
+                                           pos + (ack_led ? 1 : 0), end, pids, drop_written);
         }
     }
 }
@@ -2925,7 +2917,7 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                                                   uint8_t* __restrict__ actions, const PsFuse& ps,
                                                   uint32_t R, uint32_t rpos, uint32_t rlen, uint32_t rslot,
                                                   bool rack, uint32_t lo, uint32_t hi, size_t wave,
-                                                  size_t nwaves) {
+                                                  size_t nwaves, bool drop_written = false) {
     constexpr int kP = kSlotInFlight<kSplit>;
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, l = lane & 7;
@@ -3026,7 +3018,7 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                 if (!in[j]) continue;
                 touched = true;
                 group_packet<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, pid[j], m[j], h[j], ackr[j],
-                                          cnt, frag, reg, have_reg);
+                                          cnt, frag, reg, have_reg, drop_written);
             }
         }
         if (touched && l == 0) {
@@ -3049,7 +3041,7 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
                                                  uint8_t* __restrict__ actions,
                                                  uint32_t kmask, const PsFuse& ps,
                                                  const uint32_t* __restrict__ runs, size_t wave,
-                                                 size_t nwaves) {
+                                                 size_t nwaves, bool drop_written = false) {
     const int lane = threadIdx.x & 63;
     const uint32_t NS = st.num_slots;
     const uint32_t R = __builtin_amdgcn_readfirstlane(runs[0]);
@@ -3079,7 +3071,7 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
 #if INA_SWITCH_NARROW_SLOTS
     if constexpr (kNarrow) {
         runs_slots_narrow<kPs, kSplit>(st, pkts, stride, pay, actions, ps, R, rpos, rlen, rslot, rack, lo, hi,
-                                       wave, nwaves);
+                                       wave, nwaves, drop_written);
         return;
     }
 #endif
@@ -3117,7 +3109,8 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
         if constexpr (kNarrow)
             run_segment_narrow<kPs, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led, 0, nseg, pids);
         else
-            run_segment<kPs, false, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led, 0, nseg, pids);
+            run_segment<kPs, false, kSplit>(st, pkts, stride, pay, actions, ps, slot, ack_led, 0, nseg, pids,
+                                            drop_written);
     }
 }
 
@@ -3165,7 +3158,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                           const uint32_t* __restrict__ loc_ids,
                                                           const uint2* __restrict__ loc_tab, int drop_prefill) {
     const size_t wave = switch_block_index() * (kSwBlock / 64) + wave_in_block();
-    bool sorted_batch = false;                            // (drop_prefill: its digit pass stored the drops)
+    // (drop_prefill: the detection pass stored every packet's drop, so no path stores drops again)
     const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
     // (unsorted[1]: the epoch of the sort that filled the scratch, written by its chunk pass,
     // so a run queued apart from its sort needs no host-side state)
@@ -3187,17 +3180,16 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
         } else if (unsorted[2] == ep) {
             // a batch of dense ascending runs: the bucket pass wrote the run table, not a sort
             switch_runs_body<kPs, kNarrow, kSplit>(st, pkts, stride, pay, actions, kmask, ps,
-                                                   unsorted + (kCtlRuns - kCtlEpochs), wave, nwaves);
+                                                   unsorted + (kCtlRuns - kCtlEpochs), wave, nwaves,
+                                                   drop_prefill != 0);
             return;
-        } else {
-            sorted_batch = true;
         }
     }
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
     switch_run2_body<kPs, false, kNarrow, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps,
-                                                  wave, nwaves, drop_prefill != 0 && sorted_batch);
+                                                  wave, nwaves, drop_prefill != 0);
 }
 
 // batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
@@ -3492,7 +3484,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     const uint32_t* unsorted = nullptr;     // bucket sort: the run kernel may read A's output
     uint32_t epoch = 0;
     uint32_t loc_gsize = 0;                 // the near-sorted path's granule: 1/8 of a sort chunk
-    bool drop_prefill = false;              // the digit pass (mode 2) stores a sorted batch's drops
+    bool drop_prefill = false;              // the detection pass (mode 1) stores every packet's drop
     if (small && fast && npk <= (size_t)t.tiny_max) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
         if (!do_run) return INA_OK;
@@ -3613,7 +3605,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             // decision chose the path)
             hipLaunchKernelGGL(k_local_lists, dim3((unsigned)std::min<size_t>(sp.nch * kGranPerChunk / kLocU, 2048)),
                                dim3(kLlWaves * 64), 0, s, kc, npk, st->num_slots, ack_hint ? ~kAckBit : 0xFFFFFFFFu,
-                               ax.unsorted, ax.units, loc_gsize, k_out, ax.tab, actions);
+                               ax.unsorted, ax.units, loc_gsize, k_out, ax.tab);
         if (pre) {                                 // the in-order run reads the arrival-order keys
             kn = kc;
             vn = nullptr;

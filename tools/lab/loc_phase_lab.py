@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "distributed-training-ina_amd"))
 from ina_amd import _lib, ops  # noqa: E402
 
-_lib._lib = _lib.open_library(os.path.join(HERE, "libina_loctime.so"))
+_lib._lib = _lib.open_library(os.path.join(HERE, os.environ.get("LOCLIB", "libina_loctime.so")))
 lab = _lib._lib
 lab.ina_lab_loc_times.argtypes = [C.c_void_p]
 n, W, V, slots = 26_214_400, 8, 32, 1 << 20
@@ -82,6 +82,13 @@ for J in [int(x) for x in os.environ.get("J", "64,4096").split(",")]:
         res.setdefault("start_p10_p50_p90", []).append(0)
         if rep == 5:
             print("  start quantiles (us):", [round(float(np.quantile(st, q)), 1) for q in (0.1, 0.25, 0.5, 0.75, 0.9, 1.0)])
+            qs = (0.1, 0.5, 0.9, 0.99, 1.0)
+            for nm, x in (("block", b[:, 3] - b[:, 0]), ("count", b[:, 1] - b[:, 0]), ("place", b[:, 3] - b[:, 2]),
+                          ("end", b[:, 3] - b[:, 0].min())):
+                print(f"  {nm} quantiles (us) {qs}:", [round(float(np.quantile(x, q)) / 100, 1) for q in qs])
+            slow = np.argsort(b[:, 3] - b[:, 0])[-8:]
+            print("  slowest blocks' row index / start (us) / time (us):",
+                  [(int(i), round(float(b[i, 0] - b[:, 0].min()) / 100, 1), round(float(b[i, 3] - b[i, 0]) / 100, 1)) for i in slow])
     print(f"J={J} path={sw.batch_path(N)} (us, means over blocks):",
           {k: round(statistics.median(v), 2) for k, v in res.items()}, flush=True)
     del hdr, pay, desc, sw
