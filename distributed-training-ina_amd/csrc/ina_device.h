@@ -82,9 +82,18 @@ __device__ __forceinline__ void stream_store(T v, T* p) {
 // next launch's input (the switch, the sender), and write-through made the fused worker
 // pack 9 % slower in the packet path (54.7 -> 59.6 us per launch beside the switch,
 // profiles/r03/lab/path_store_lab.log).
+#ifndef INA_PACKET_STORE
+#define INA_PACKET_STORE 0            // 0 non-temporal, 1 write-through (stream_store), 2 default
+#endif
 template <typename T>
 __device__ __forceinline__ void packet_store(T v, T* p) {
+#if INA_PACKET_STORE == 1
+    stream_store(v, p);
+#elif INA_PACKET_STORE == 2
+    *p = v;
+#else
     __builtin_nontemporal_store(v, p);
+#endif
 }
 
 }  // namespace ina

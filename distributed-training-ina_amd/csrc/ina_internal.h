@@ -28,6 +28,7 @@ int set_bucket_tile(int v);   // ina_switch.hip
 int set_runs(int v);          // ina_switch.hip
 int set_pre_all(int v);       // ina_switch.hip
 int set_local(int v);         // ina_switch.hip
+int set_decide_delay(int v);  // ina_switch.hip
 int ew_grid_cap();            // ina_kernels.hip: grid cap of the elementwise kernels (tuning key 14)
 // checked builds (INA_STORE_CHECK, ina_device.h): each source's stream_store contract
 // violations since the last read, cleared by the read

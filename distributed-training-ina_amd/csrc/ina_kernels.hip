@@ -1943,7 +1943,7 @@ static int pack_nga_launch(const Src& src, bool src_aligned, size_t n, const ina
 
 extern "C" {
 
-const char* ina_version(void) { return "ina-mi355x 0.1 (gfx950)"; }
+const char* ina_version(void) { return "ina-mi355x 0.2 (gfx950)"; }
 const char* ina_last_error_string(void) { return g_err; }
 
 #ifndef INA_LAB_KEYS
@@ -1975,6 +1975,7 @@ int ina_set_tuning(int key, int value) {
         case 18: return set_runs(value);
         case 19: return set_pre_all(value);
         case 20: return set_local(value);
+        case 21: return set_decide_delay(value);
         default: return INA_EINVAL;
     }
 }

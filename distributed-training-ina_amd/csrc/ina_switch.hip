@@ -196,6 +196,31 @@ __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const ui
 //    are not this switch's (switch_check miss, ngaa.p4:27-37,184-186); fused with the
 //    first digit pass's chunk histogram.
 constexpr uint32_t kAckBit = 0x80000000u;
+
+// A batch's slot keys as the detection pass makes them (slot = index % num_slots, num_slots for
+// another switch's packets, bit 31 = PS ack when ack_hint): read from the detection pass's key
+// array, or -- narrow batches with descriptors, whose detection pass no longer writes that array
+// (round 6: 26 MB of stores in front of every NGA-32 C3 call) -- made again from the
+// descriptor, the same arithmetic (an index already below num_slots skips the division).
+#ifndef INA_KEYS_FROM_DESC
+#define INA_KEYS_FROM_DESC 1
+#endif
+struct KeySrc {
+    const uint32_t* keys;
+    const uint2* desc;
+    uint32_t num_slots;
+    int switch_id;
+    bool ack_hint;
+    __device__ __forceinline__ uint32_t operator()(size_t p) const {
+        if (!desc) return keys[p];
+        const uint2 d = desc[p];
+        const uint32_t idx = __builtin_bswap32((d.x >> 16) | (d.y << 16));
+        const bool mine = switch_id >= 0 && ((d.y >> 16) & 0xFFu) == (uint32_t)(uint8_t)switch_id;
+        if (!mine) return num_slots;
+        const uint32_t slot = idx < num_slots ? idx : idx % num_slots;
+        return slot | ((ack_hint && ((d.x >> 14) & 1u)) ? kAckBit : 0u);
+    }
+};
 template <int R, bool kDesc, int NW = kRsWaves>
 __global__ __launch_bounds__(NW * 64) void k_switch_keys(const uint8_t* __restrict__ pkts,
                                                           const uint2* __restrict__ desc,
@@ -308,6 +333,15 @@ int set_runs(int v) {
 static std::atomic<int> g_local{1};        // ina_set_tuning key 20: near-sorted batches skip the sort (0: off)
 int set_local(int v) {
     g_local = v ? 1 : 0;
+    return INA_OK;
+}
+// ina_set_tuning key 21 (tests): block 0 of the decision pass waits this many microseconds
+// before it decides, so every other block's bounded wait for the near-sorted verdict runs out
+// and it sorts its chunk anyway -- the shape of a block 0 dispatched late (0: off, the default)
+static std::atomic<int> g_decide_delay{0};
+int set_decide_delay(int v) {
+    if (v < 0 || v > 100000) return INA_EINVAL;
+    g_decide_delay = v;
     return INA_OK;
 }
 // ina_set_tuning key 19: the split chunk pass (detection, decision, then digits) for every key
@@ -584,12 +618,13 @@ int set_bucket_tile(int v) {
 // thread's sort and run changes nothing in that batch (the run used to re-read
 // key 19 and pick arrays the sort never wrote).
 struct SwitchTuning {
-    int small_sort, tiny_max, sort_mode, os_rounds, runs, local, pre_all, ack_fast, win, bucket_tile;
+    int small_sort, tiny_max, sort_mode, os_rounds, runs, local, pre_all, ack_fast, win, bucket_tile,
+        decide_delay;
 };
 static SwitchTuning switch_tuning() {
     return SwitchTuning{g_small_sort.load(), g_tiny_max.load(), g_sort_mode.load(), g_os_rounds.load(),
                         g_runs.load(),       g_local.load(),    g_pre_all.load(),   g_ack_fast.load(),
-                        g_switch_win.load(), g_bucket_tile.load()};
+                        g_switch_win.load(), g_bucket_tile.load(), g_decide_delay.load()};
 }
 
 // key fields of R rounds of 64 packets (all loads issued first): slot index, switch id and
@@ -778,6 +813,9 @@ constexpr int kGranPerChunk = kBkWaves / kGranWaves;          // 8 granules per 
 constexpr int kLocMaxGran = 8 * kBkThr;                       // the decision: <= 8 granules a thread
 constexpr uint32_t kLocBeta = 3;                              // the windows' scan <= 3 x the batch
 constexpr uint32_t kLocMaxWindow = 65535;                     // 16-bit cursors
+// how long a digit-pass block waits for block 0's near-sorted verdict before it sorts its chunk
+// anyway (constant 100 MHz clock: 50 us; block 0's decision takes ~8 us, r05)
+constexpr unsigned long long kLocPollTicks = 5000;
 #ifndef INA_LOC_U
 #define INA_LOC_U 4                                           // granules per unit (a half chunk)
 #endif
@@ -970,7 +1008,7 @@ __device__ __forceinline__ size_t switch_block_index();
 #ifndef INA_LL_WAVES_PER_EU
 #define INA_LL_WAVES_PER_EU 8
 #endif
-__global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(INA_LL_WAVES_PER_EU, 8))) void k_local_lists(const uint32_t* __restrict__ keys, size_t npk,
+__global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(INA_LL_WAVES_PER_EU, 8))) void k_local_lists(const KeySrc keys, size_t npk,
                                                                uint32_t num_slots, uint32_t kmask,
                                                                const uint32_t* __restrict__ unsorted,
                                                                const LocUnit* __restrict__ units, uint32_t gsize,
@@ -1001,7 +1039,7 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
 #pragma unroll
             for (int r = 0; r < kLlRounds; ++r) {
                 const uint32_t p = b0 + (uint32_t)(r * 64 + lane);
-                kk[r] = p < b1 ? keys[p] : num_slots;
+                kk[r] = p < b1 ? keys(p) : num_slots;
             }
         }
         uint32_t area = 0;
@@ -1015,7 +1053,7 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
 #pragma unroll
                     for (int r = 0; r < kLlRounds; ++r) {
                         const uint32_t p = r0 + (uint32_t)(r * 64 + lane);
-                        kk[r] = p < b1 ? keys[p] : num_slots;
+                        kk[r] = p < b1 ? keys(p) : num_slots;
                     }
                 }
 #pragma unroll
@@ -1084,7 +1122,7 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
 #pragma unroll
                     for (int r = 0; r < kLlRounds; ++r) {
                         const uint32_t p = r0 + (uint32_t)(r * 64 + lane);
-                        kk[r] = p < b1 ? keys[p] : num_slots;
+                        kk[r] = p < b1 ? keys(p) : num_slots;
                     }
                 }
 #pragma unroll
@@ -1208,8 +1246,12 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
 // kout, the descent flag, the breaks; no digits, a small LDS footprint), then 2 = the decision
 // (every block sums the break counts; dense runs: block 0 writes the run table) and, for a
 // batch neither in slot order nor dense runs, the digits + scatter.
+// lab builds only (timing what the detection pass's action stores cost; results then differ)
+#ifndef INA_LAB_DETECT_NOACT
+#define INA_LAB_DETECT_NOACT 0
+#endif
 template <int R, bool kDesc, int BINS, int kMode = 0>
-__global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restrict__ pkts,
+__global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_sort_chunks(const uint8_t* __restrict__ pkts,
                                                         const uint2* __restrict__ desc, size_t npk,
                                                         size_t stride, uint32_t num_slots, int switch_id,
                                                         uint8_t* __restrict__ actions, int hbits, int lb,
@@ -1219,7 +1261,8 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                                                         uint32_t* __restrict__ unsorted, uint32_t epoch,
                                                         uint32_t* __restrict__ brk_cnt,
                                                         uint2* __restrict__ brk_ent,
-                                                        uint32_t* __restrict__ gstat, LocUnit* __restrict__ units) {
+                                                        uint32_t* __restrict__ gstat, LocUnit* __restrict__ units,
+                                                        uint32_t decide_delay_ticks = 0) {
     // per-wave digit counts, then bases (2,048 bins: two waves' 16-bit halves per word)
     constexpr bool kHalf = BINS > kBkThr;
     __shared__ uint32_t base[kHalf ? kBkWaves / 2 : kBkWaves][BINS];
@@ -1257,12 +1300,25 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         // lists), no sort.  PM / SM live in the count array (the host takes the path only for G
         // <= half of it)
         // Block 0 decides and publishes the verdict (epoch-tagged, agent scope); the other blocks
-        // only poll it (block 0 is dispatched first and waits on nothing, so every poll ends)
+        // poll it for at most kLocPollTicks of the constant 100 MHz clock, then do the digits
+        // anyway.  No block's progress depends on when (or whether) block 0 is dispatched (ADVICE
+        // r05): a verdict that comes late only costs the digits' time, never the results -- on a
+        // near-sorted batch the digits land in k_out / v_out and the per-(digit, chunk) rows,
+        // which k_local_lists then overwrites (its ids) or nobody reads (the bucket pass and the
+        // run kernel follow the verdict's epoch, written before the verdict by block 0).  The
+        // verdict itself is the only word shared inside this launch; nothing block 0 writes is
+        // read by another block of it (the unit table and the control words are read by the
+        // NEXT launches).  Round 5's faulting lab kernel broke exactly these two
+        // rules.
         if (gstat) {
             __shared__ uint32_t s_loc;
             unsigned long long* verdict = reinterpret_cast<unsigned long long*>(unsorted + kLocVerdict);
             if (c == 0) {
                 DEC_STAMP(8191, 1);
+                if (decide_delay_ticks) {                 // (tests: key 21) a late block 0
+                    const unsigned long long t0 = wall_clock64();
+                    while (wall_clock64() - t0 < decide_delay_ticks) __builtin_amdgcn_s_sleep(64);
+                }
                 const bool loc = local_decide(gstat, gstat + G, G, (uint32_t)(kBkThr * R / kGranPerChunk), npk,
                                               unsorted, epoch, units, true, &base[0][0],
                                               &base[0][0] + sizeof(base) / 8, wtot, wbrk);
@@ -1274,9 +1330,18 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
                 DEC_STAMP(8191, 2);
             } else if (threadIdx.x == 0) {
                 unsigned long long v;
-                while (((v = __hip_atomic_load(verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) != epoch)
+                uint32_t loc = 0u;
+                const unsigned long long t0 = wall_clock64();
+                for (;;) {
+                    v = __hip_atomic_load(verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((v >> 1) == epoch) {
+                        loc = (uint32_t)(v & 1ull);
+                        break;
+                    }
+                    if (wall_clock64() - t0 > kLocPollTicks) break;      // no verdict yet: sort
                     __builtin_amdgcn_s_sleep(8);
-                s_loc = (uint32_t)(v & 1ull);
+                }
+                s_loc = loc;
                 if (c == nch - 1) DEC_STAMP(8190, 1);
             }
             __syncthreads();
@@ -1319,13 +1384,13 @@ __global__ __launch_bounds__(kBkThr) void k_sort_chunks(const uint8_t* __restric
         // the other actions (1 in W): scattered byte stores in slot / list order wrote back a line
         // each (shuffled NGA-32 run kernel: 440 MB written, r05e); the in-order and run-table
         // paths store every action anyway
-        if (kMode == 1 && p < npk) actions[p] = mine ? INA_ACT_DROP : INA_ACT_FWD_OTHER;
+        if (kMode == 1 && p < npk && !INA_LAB_DETECT_NOACT) actions[p] = mine ? INA_ACT_DROP : INA_ACT_FWD_OTHER;
         if constexpr (kMode != 1) {
             if constexpr (kHalf) lds_count_half(base[wv >> 1], (key >> lb) & (nb - 1), p < npk, (wv & 1) * 16);
             else lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
         }
         if constexpr (kMode == 1)
-            if (p < npk) kout[p] = k[r];              // arrival-order keys (the in-order run's)
+            if (p < npk && kout) kout[p] = k[r];   // arrival-order keys (the in-order run's; NULL: see KeySrc)
         // predecessor: lane l-1 of this round (DPP wave_shr:1), lane 0 the previous round's
         // lane 63 (or, in round 0, the key loaded above)
         const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp((int)prev, (int)key, 0x138, 0xF, 0xF, false);
@@ -2594,6 +2659,90 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
     if (l == 0 && !(drop_written && act == INA_ACT_DROP)) actions[pid] = act;
 }
 
+// ---- whole segments of 8 (round 6) ---------------------------------------------------------
+// The common narrow segment is one slot's W = 8 packets of one step: no PS ack, every frag id the
+// slot's (or, the slot free, the first packet's), count field 8 and the slot's count at 0.  Then
+// ngaa.p4:66-78 / processor.p4:14-24 reduce to: packet 0 overwrites the registers, packets 1..7
+// add, packet 7 completes the slot (count back to 0) and is forwarded with the sum, packets 0..6
+// are dropped.  The per-packet walk (group_packet) pays a dependent round trip and the state
+// machine's branches per packet; here a wave whose 8 lane groups each hold such a segment (or
+// none) reads every header row and the slots' count / frag in ONE round trip, checks the
+// conditions, then issues all 8 payload loads per lane at once and adds them in registers.  Any
+// other segment in the wave -> false, and the caller walks the wave's segments packet by packet
+// (the rows it reads then come from L2).  Lane l of group g: pidl = the id of packet l of group
+// g's segment, ackl its PS-ack hint (sort key bit 31); has = the group holds a segment.
+#ifndef INA_SWITCH_SEG8
+#define INA_SWITCH_SEG8 1
+#endif
+#ifndef INA_SEG8_FLIGHT
+#define INA_SEG8_FLIGHT 4
+#endif
+constexpr int kSeg8Flight = INA_SEG8_FLIGHT;
+static_assert(8 % kSeg8Flight == 0, "whole rounds of payload loads");
+template <bool kSplit>
+__device__ __forceinline__ bool seg8_fast(const ina_switch_state_t& st, uint8_t* __restrict__ pkts, size_t stride,
+                                          uint8_t* __restrict__ pay, uint8_t* __restrict__ actions, bool has,
+                                          uint32_t slot, uint32_t pidl, bool ackl, bool drop_written) {
+    const int lane = threadIdx.x & 63, l = lane & 7, g0 = lane & ~7;
+    const int V = st.V, L = V >> 2;
+    const bool vl = l < L;
+    u32x4s h = {0u, 0u, 0u, 0u};
+    uint32_t cnt = 0u, frag = 0u;
+    if (has) {
+        h = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pidl * (kSplit ? 16 : stride));
+        cnt = st.count[slot];
+        frag = st.frag[slot];
+    }
+    const uint32_t fin = __builtin_bswap32((h.z >> 24) | (h.w << 8));
+    const uint32_t F = frag ? frag : (uint32_t)__shfl((int)fin, g0);
+    const bool ok = !has || (!ackl && ((h.y >> 14) & 1u) == 0u && fin == F && (h.y & 0xFFu) == 8u && cnt == 0u);
+    if (__ballot(!ok)) return false;
+    // the payload loads in flight together: kSeg8Flight at a time (the VGPRs they hold)
+    constexpr int kF = kSeg8Flight;
+    u32x4s run = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k0 = 0; k0 < 8; k0 += kF) {
+    u32x4s m[kF];
+#pragma unroll
+    for (int j = 0; j < kF; ++j) {
+        const uint32_t pk = (uint32_t)__shfl((int)pidl, g0 + k0 + j);
+        m[j] = u32x4s{0u, 0u, 0u, 0u};
+        if (has && vl) {
+            if constexpr (kSplit)
+                m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pk * (size_t)(4 * V)) + l);
+            else
+                m[j] = ld_row16(pkts + (size_t)pk * stride + 15 + 16 * l);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kF; ++j) {
+        const int k = k0 + j;
+        const u32x4s v{__builtin_bswap32(m[j].x), __builtin_bswap32(m[j].y), __builtin_bswap32(m[j].z),
+                       __builtin_bswap32(m[j].w)};
+        run = k == 0 ? v : run + v;
+        // out_value -> the packet (processor.p4:22): the completing packet 7, and with
+        // write_dropped the dropped ones' running sums too (the id moved with every lane active:
+        // lanes past V/4 sit out the store, and a moved value from an inactive lane is undefined)
+        const uint32_t pk = (uint32_t)__shfl((int)pidl, g0 + k);
+        if (has && vl && (k == 7 || st.write_dropped)) {
+            const u32x4s e{__builtin_bswap32(run.x), __builtin_bswap32(run.y), __builtin_bswap32(run.z),
+                           __builtin_bswap32(run.w)};
+            if constexpr (kSplit) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pk * (size_t)(4 * V)) + l);
+            else st_row16(pkts + (size_t)pk * stride + 15 + 16 * l, e);
+        }
+    }
+    }
+    if (has) {
+        if (vl) __builtin_nontemporal_store(run, reinterpret_cast<u32x4s*>(st.regs + (size_t)slot * V + 4 * l));
+        if (l == 0) {
+            st.count[slot] = 0u;                                  // 8 adds of count 8: back to 0
+            st.frag[slot] = F;
+        }
+        if (l == 7 || !drop_written) actions[pidl] = l == 7 ? INA_ACT_FWD_AGG : INA_ACT_DROP;
+    }
+    return true;
+}
+
 // Narrow packets (V <= 32) in sorted order (the bucket sort's arrays, or a batch already in
 // slot order read in place), segment-parallel: each wave takes windows of `win` sorted
 // positions, and its 8 lane groups take the segments that START in the window, 8 at a time
@@ -2603,8 +2752,7 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
 template <bool kPs, bool kSplit>
 __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st, uint8_t* __restrict__ pkts,
                                                     uint8_t* __restrict__ pay, size_t npk, size_t stride,
-                                                    const uint32_t* __restrict__ keys,
-                                                    const uint32_t* __restrict__ ids,
+                                                    const KeySrc keys, const uint32_t* __restrict__ ids,
                                                     uint8_t* __restrict__ actions, uint32_t win, uint32_t kmask,
                                                     const PsFuse& ps, size_t wave, size_t nwaves,
                                                     bool drop_written = false) {
@@ -2620,10 +2768,10 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
     const int wb = (int)threadIdx.x & ~63;
     for (size_t w0 = wave * win; w0 < npk; w0 += nwaves * win) {
         const size_t i = w0 + (size_t)lane;
-        const uint32_t kr = i < npk ? keys[i] : NS;
+        const uint32_t kr = i < npk ? keys(i) : NS;
         const uint32_t ki = kr & kmask;                   // slot (bit 31: PS-ack hint)
         const uint32_t idw = i < npk ? (ids ? ids[i] : (uint32_t)i) : 0u;
-        const uint32_t kp = (i > 0 && i <= npk) ? (keys[i - 1] & kmask) : 0xFFFFFFFFu;
+        const uint32_t kp = (i > 0 && i <= npk) ? (keys(i - 1) & kmask) : 0xFFFFFFFFu;
         const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
         __builtin_amdgcn_wave_barrier();
         s_wid[threadIdx.x] = idw;
@@ -2647,7 +2795,7 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                     size_t j0 = w0 + 64;
                     for (;;) {
                         const size_t j = j0 + (size_t)lane;
-                        const bool diff = j >= npk || (keys[j] & kmask) != slot_b;
+                        const bool diff = j >= npk || (keys(j) & kmask) != slot_b;
                         const unsigned long long mm = __ballot(diff);
                         if (mm) { end = j0 + (size_t)__builtin_ctzll(mm); break; }
                         j0 += 64;
@@ -2662,6 +2810,28 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                 }
             }
             const bool has = hlen != 0;
+#if INA_SWITCH_SEG8
+            if constexpr (!kPs && kSplit) {
+                // every segment of these heads 8 packets long: the whole-segment path
+                if (maxlen == 8u && !__ballot(has && hlen != 8u)) {
+                    const uint32_t q = hst + (uint32_t)l;
+                    uint32_t pidl = 0u;
+                    bool ackl = false;
+                    if (has) {
+                        if (q < 64u) {
+                            pidl = s_wid[wb + (int)q];
+                            ackl = s_wack[wb + (int)q] != 0u;
+                        } else {
+                            const size_t qa = w0 + (size_t)q;
+                            pidl = ids ? ids[qa] : (uint32_t)qa;
+                            ackl = (keys(qa) & ~kmask) != 0u;
+                        }
+                    }
+                    if (seg8_fast<kSplit>(st, pkts, stride, pay, actions, has, hslot, pidl, ackl, drop_written))
+                        continue;
+                }
+            }
+#endif
             uint32_t cnt = 0, frag = 0;
             if (has) {
                 cnt = st.count[hslot];
@@ -2688,7 +2858,7 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                         } else {
                             const size_t qa = w0 + (size_t)q;
                             pid[j] = ids ? ids[qa] : (uint32_t)qa;
-                            acq[j] = (keys[qa] & ~kmask) != 0u;
+                            acq[j] = (keys(qa) & ~kmask) != 0u;
                         }
                     }
                     if (in[j] && !acq[j]) {
@@ -2762,6 +2932,17 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
         }
         const uint32_t slot = kmin + (uint32_t)s8 + (uint32_t)g;
         const bool has = hlen != 0;
+#if INA_SWITCH_SEG8
+        if constexpr (!kPs && kSplit) {
+            // every list of these 8 slots 8 packets long: the whole-segment path
+            if (maxlen == 8u && !__ballot(has && hlen != 8u) &&
+                seg8_fast<kSplit>(st, pkts, stride, pay, actions, has, slot, idl & ~kAckBit, (idl & kAckBit) != 0u,
+                                  true)) {
+                id_nx = (uint32_t)l < e_nx.y ? ids[e_nx.x + (uint32_t)l] : 0u;   // the next step's first ids
+                continue;
+            }
+        }
+#endif
         uint32_t cnt = 0, frag = 0;
         if (has) {
             cnt = st.count[slot];
@@ -2821,10 +3002,13 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                                  const uint32_t* __restrict__ ids,
                                                  uint8_t* __restrict__ actions, uint32_t win,
                                                  uint32_t kmask, const PsFuse& ps, size_t wave,
-                                                 size_t nwaves, bool drop_written = false) {
+                                                 size_t nwaves, bool drop_written = false,
+                                                 const uint2* __restrict__ kdesc = nullptr) {
 #if INA_SWITCH_NARROW_SLOTS
     if constexpr (kNarrow) {
-        window_slots_narrow<kPs, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps, wave,
+        // (kdesc: a batch in slot order whose keys come from its descriptors, see KeySrc)
+        const KeySrc ks{keys, kdesc, st.num_slots, st.switch_id, kmask != 0xFFFFFFFFu};
+        window_slots_narrow<kPs, kSplit>(st, pkts, pay, npk, stride, ks, ids, actions, win, kmask, ps, wave,
                                          nwaves, drop_written);
         return;
     }
@@ -2941,6 +3125,21 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
     for (size_t s8 = s_begin; s8 < s_end; s8 += 8) {
         const uint32_t slot = (uint32_t)(s8 + (size_t)g);
         const bool sv = s8 + (size_t)g < s_end;
+#if INA_SWITCH_SEG8
+        if constexpr (!kPs && kSplit) {
+            // 8 runs, each holding every slot of this group once: the whole-segment path (lane l
+            // of a group: run l's packet of the group's slot, in run order = arrival order)
+            if (R == 8u) {
+                const uint32_t rsl = (uint32_t)__shfl((int)rslot, l), rll = (uint32_t)__shfl((int)rlen, l),
+                               rpl = (uint32_t)__shfl((int)rpos, l);
+                const bool ackl = __shfl((int)rack_u, l) != 0;
+                const uint32_t off = slot - rsl;
+                if (!__ballot(sv && off >= rll) &&
+                    seg8_fast<kSplit>(st, pkts, stride, pay, actions, sv, slot, rpl + off, ackl, drop_written))
+                    continue;
+            }
+        }
+#endif
         uint32_t cnt = 0, frag = 0;
         if (sv) {
             cnt = st.count[slot];
@@ -2971,15 +3170,14 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
                         h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
                     }
                 } else {
-                    // the stretch of run r holding group gg's row: rows base + gg
-                    const uint32_t base_row = rp + (uint32_t)s8 - rs;
+                    // the stretch of run r holding group gg's row: rows rp + (slot - rs)
                     const uint32_t sg0 = (uint32_t)s8 + (uint32_t)gg0, sg1 = (uint32_t)s8 + (uint32_t)gg1;
                     const bool ok0 = !ackr[j] && gg0 < 8 && sg0 < s_end && sg0 - rs < rl;
                     const bool ok1 = !ackr[j] && has1 && sg1 < s_end && sg1 - rs < rl;
                     if (ok0)
-                        m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)(base_row + (uint32_t)gg0) * stride) + cc0);
+                        m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)(rp + (sg0 - rs)) * stride) + cc0);
                     if (ok1)
-                        h[j] = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)(base_row + (uint32_t)gg1) * stride) + cc1);
+                        h[j] = sw_ld(reinterpret_cast<const u32x4s*>(pkts + (size_t)(rp + (sg1 - rs)) * stride) + cc1);
                 }
             }
             if constexpr (!kSplit) {
@@ -3156,7 +3354,8 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                           const uint32_t* __restrict__ ids_a,
                                                           const uint32_t* __restrict__ unsorted,
                                                           const uint32_t* __restrict__ loc_ids,
-                                                          const uint2* __restrict__ loc_tab, int drop_prefill) {
+                                                          const uint2* __restrict__ loc_tab, int drop_prefill,
+                                                          const uint2* __restrict__ kdesc) {
     const size_t wave = switch_block_index() * (kSwBlock / 64) + wave_in_block();
     // (drop_prefill: the detection pass stored every packet's drop, so no path stores drops again)
     const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
@@ -3170,6 +3369,13 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
                                                 unsorted[kLocKmin], unsorted[kLocSlots], wave, nwaves);
             return;
         }
+        if (unsorted[2] == ep) {
+            // a batch of dense ascending runs: the decision wrote the run table, not a sort
+            switch_runs_body<kPs, kNarrow, kSplit>(st, pkts, stride, pay, actions, kmask, ps,
+                                                   unsorted + (kCtlRuns - kCtlEpochs), wave, nwaves,
+                                                   drop_prefill != 0);
+            return;
+        }
         if (unsorted[0] != ep) {
             // a batch already in slot order: the chunk sort's own output is the sorted order
             // (after the split chunk pass of wide keys: the arrival-order keys, ids_a NULL --
@@ -3177,19 +3383,17 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
             keys = keys_a;
             ids = ids_a;
             if (!ids_a) nforeign = nullptr;
-        } else if (unsorted[2] == ep) {
-            // a batch of dense ascending runs: the bucket pass wrote the run table, not a sort
-            switch_runs_body<kPs, kNarrow, kSplit>(st, pkts, stride, pay, actions, kmask, ps,
-                                                   unsorted + (kCtlRuns - kCtlEpochs), wave, nwaves,
-                                                   drop_prefill != 0);
-            return;
+        } else {
+            kdesc = nullptr;                                // only an in-order batch reads them
         }
+    } else {
+        kdesc = nullptr;
     }
     // bucket sort: the foreign packets' bucket was left unsorted at the END of the arrays;
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
     switch_run2_body<kPs, false, kNarrow, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps,
-                                                  wave, nwaves, drop_prefill != 0);
+                                                  wave, nwaves, drop_prefill != 0, kdesc);
 }
 
 // batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
@@ -3321,15 +3525,20 @@ static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
 }
 
 // The sorts queued alone (phase 1), by scratch: the switch keys they ran under and the batch
-// they sorted.  The run over that scratch (phase 2) takes its keys from here, and refuses a
-// scratch no sort of this batch filled; a sort + run call (phase 0) over the scratch drops its
-// record, since it overwrites what that sort left.
+// they sorted -- its shape, its rows, its actions (the detection pass stored every packet's drop
+// / foreign action there, and the run stores only the others) and the switch id its keys were
+// made for.  The run over that scratch (phase 2) takes its keys from here, refuses a scratch no
+// sort of exactly this batch filled, and consumes the record.  Every sort or sort + run call
+// drops the scratch's record before it launches anything (it overwrites what an earlier sort
+// left), and a sort alone records only once all its launches succeeded.
 struct SortRecord {
     SwitchTuning t;
     size_t npk, stride;
     uint32_t num_slots;
     int V;
     bool split;
+    const void *rows, *pay, *actions;
+    int switch_id;
 };
 static std::mutex g_sorts_mu;
 static std::unordered_map<const void*, SortRecord> g_sorts;
@@ -3349,7 +3558,8 @@ static bool sort_record_find(const void* scratch, const SortRecord& want, Switch
     if (it == g_sorts.end()) return false;
     const SortRecord& r = it->second;
     if (r.npk != want.npk || r.stride != want.stride || r.num_slots != want.num_slots || r.V != want.V ||
-        r.split != want.split)
+        r.split != want.split || r.rows != want.rows || r.pay != want.pay || r.actions != want.actions ||
+        r.switch_id != want.switch_id)
         return false;
     *t = r.t;
     return true;
@@ -3444,16 +3654,26 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         return set_error(INA_EINVAL, "descriptors must be 8-byte aligned%s", "");
     // the switch keys of this batch: read once here, or (a run alone) its sort's record
     SwitchTuning t;
-    {
-        const SortRecord rec{SwitchTuning{}, npk, stride, st->num_slots, st->V, split};
-        if (phase == 2) {
-            if (!sort_record_find(scratch, rec, &t))
-                return set_error(INA_EINVAL, "run alone: no sort of this batch was queued into this scratch%s", "");
-        } else {
-            t = switch_tuning();
-            sort_record_set(scratch, phase == 1, SortRecord{t, npk, stride, st->num_slots, st->V, split});
-        }
+    SortRecord rec{SwitchTuning{}, npk, stride, st->num_slots, st->V, split, pkts, pay, actions, st->switch_id};
+    if (phase == 2) {
+        if (!sort_record_find(scratch, rec, &t))
+            return set_error(INA_EINVAL,
+                             "run alone: no sort of this batch (rows, actions, shape, switch id) was queued into "
+                             "this scratch%s", "");
+    } else {
+        t = switch_tuning();
+        rec.t = t;
+        sort_record_set(scratch, false, rec);                  // this call overwrites the scratch
     }
+    // a sort alone records its batch once every launch succeeded; a run alone consumes the record
+    auto sorted_ok = [&]() {
+        if (phase == 1) sort_record_set(scratch, true, rec);
+        return INA_OK;
+    };
+    auto run_ok = [&]() {
+        if (phase == 2) sort_record_set(scratch, false, rec);
+        return INA_OK;
+    };
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     uint8_t* base = reinterpret_cast<uint8_t*>(align_up((uintptr_t)scratch, 256));
     size_t arr = align_up(npk * 4, 256);
@@ -3485,9 +3705,10 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     uint32_t epoch = 0;
     uint32_t loc_gsize = 0;                 // the near-sorted path's granule: 1/8 of a sort chunk
     bool drop_prefill = false;              // the detection pass (mode 1) stores every packet's drop
+    bool keys_from_desc = false;            // narrow + descriptors, one call: no arrival-order key array
     if (small && fast && npk <= (size_t)t.tiny_max) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
-        if (!do_run) return INA_OK;
+        if (!do_run) return sorted_ok();
         uint32_t win = (uint32_t)INA_SWITCH_WIN_SMALL;
         if (const int wv = t.win) win = (uint32_t)wv;
         const bool narrow = (uint64_t)st->num_slots + 1 <= (1u << 20);
@@ -3503,9 +3724,9 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
 #undef INA_TINY
         if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch tiny launch%s", "");
         *fused_out = ps.on != 0;
-        return INA_OK;
+        return run_ok();
     } else if (small) {
-        if (!do_run) return INA_OK;                         // this sort reads the packets
+        if (!do_run) return sorted_ok();                         // this sort reads the packets
         if ((uint64_t)st->num_slots + 1 <= (1u << 20))
             hipLaunchKernelGGL((k_switch_sort_small<uint32_t, 12>), dim3(1), dim3(kSmallBlock), 0, s, pkts,
                                (uint32_t)npk, stride, st->num_slots, st->switch_id, actions, kc, vc);
@@ -3536,6 +3757,12 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // chunk pass split in two (detection, then decision + digits), so structured batches skip the digits
         const bool pre = (sp.wide || t.pre_all) && fast;
         drop_prefill = pre;
+        // the detection pass's arrival-order keys are read only by the in-order narrow run and the
+        // near-sorted lists; with descriptors both make them again from the descriptors (KeySrc)
+        // -- the 4-byte store per packet (26 MB at NGA-32 C3 size) leaves the pass in front of
+        // every call.  A sort queued alone still writes them (its run may come without the
+        // descriptors).
+        keys_from_desc = INA_KEYS_FROM_DESC && pre && desc && phase == 0 && st->V <= kNarrowMaxV;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
@@ -3543,8 +3770,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
 #define INA_A_DETECT(RR)                                                                              \
             hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true, 64, 1> : &k_sort_chunks<RR, false, 64, 1>),      \
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
-                               st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kc, vc, ah, \
-                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units)
+                               st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, keys_from_desc ? nullptr : kc, vc, ah, \
+                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u)
             if (ri == 3) INA_A_DETECT(kR3 / 4);
             else if (ri == 2) INA_A_DETECT(kR2 / 4);
             else if (ri == 1) INA_A_DETECT(kR1 / 4);
@@ -3556,7 +3783,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                         : (desc ? &k_sort_chunks<RR, true, kRsBins, 2> : &k_sort_chunks<RR, false, kRsBins, 2>)), \
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
-                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units)
+                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, \
+                               (uint32_t)t.decide_delay * 100u)
             if (ri == 3) INA_A_SORT(kR3 / 4);
             else if (ri == 2) INA_A_SORT(kR2 / 4);
             else if (ri == 1) INA_A_SORT(kR1 / 4);
@@ -3568,7 +3796,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                     : (desc ? &k_sort_chunks<RR, true, kRsBins> : &k_sort_chunks<RR, false, kRsBins>)), \
                            dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                            st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah,  \
-                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units)
+                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u)
         if (ri == 3) INA_A_LAUNCH(kR3 / 4);
         else if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
@@ -3604,7 +3832,9 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             // the near-sorted path's per-slot lists into the idle k_out (exits at once unless the
             // decision chose the path)
             hipLaunchKernelGGL(k_local_lists, dim3((unsigned)std::min<size_t>(sp.nch * kGranPerChunk / kLocU, 2048)),
-                               dim3(kLlWaves * 64), 0, s, kc, npk, st->num_slots, ack_hint ? ~kAckBit : 0xFFFFFFFFu,
+                               dim3(kLlWaves * 64), 0, s,
+                               KeySrc{kc, keys_from_desc ? dsc : nullptr, st->num_slots, st->switch_id, ack_hint},
+                               npk, st->num_slots, ack_hint ? ~kAckBit : 0xFFFFFFFFu,
                                ax.unsorted, ax.units, loc_gsize, k_out, ax.tab);
         if (pre) {                                 // the in-order run reads the arrival-order keys
             kn = kc;
@@ -3658,7 +3888,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             }
         }
     }
-    if (!do_run) return INA_OK;
+    if (!do_run) return sorted_ok();
     if (fast) {
         // a wave runs the segments that start in its window of `win` sorted positions: a
         // segment is a chain of dependent round trips, so small windows (more waves) win
@@ -3681,7 +3911,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                    : (narrow ? &k_switch_run2<false, true, false> : &k_switch_run2<false, false, false>));
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, pay, npk, stride, kc, vc, actions,
                            win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted, k_out, ax.tab,
-                           drop_prefill ? 1 : 0);
+                           drop_prefill ? 1 : 0, keys_from_desc ? reinterpret_cast<const uint2*>(desc) : nullptr);
         *fused_out = ps.on != 0;
     } else {
         unsigned gw = (unsigned)((npk + (kSwBlock / 64) - 1) / (kSwBlock / 64));
@@ -3689,7 +3919,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                            vc, actions);
     }
     if (hipGetLastError() != hipSuccess) return set_error(INA_EHIP, "switch run launch%s", "");
-    return INA_OK;
+    return run_ok();
 }
 
 static int switch_apply_impl(const ina_switch_state_t* st, uint8_t* pkts, size_t npk, size_t stride,

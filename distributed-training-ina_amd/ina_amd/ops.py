@@ -970,7 +970,7 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
                ew_blocks: int | None = None, switch_tiny_max: int | None = None,
                host_zero_copy: bool | None = None, switch_bucket_tile: int | None = None,
                switch_runs: bool | None = None, switch_pre_all: bool | None = None,
-               switch_local: bool | None = None):
+               switch_local: bool | None = None, switch_decide_delay_us: int | None = None):
     """Launch-geometry knobs (results never change, only speed): max_blocks caps the
     grid of the elementwise kernels, reduce_blocks that of the sum-reduce (0 = the
     measured 64*W rule), stream_blocks the chunk-loop kernels, combine_blocks the fp32
@@ -997,7 +997,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
     default; False always sorts); switch_pre_all splits the sort's first pass into detection,
     decision and digits for every key width (True, the default; False: keys of 19-22 bits only);
     switch_local lets near-sorted batches (V <= 32, local disorder) run from per-slot lists
-    without a sort (True, the default); unroll is the sum-reduce's 16-byte chunks per worker
+    without a sort (True, the default); switch_decide_delay_us (tests) delays the near-sorted
+    decision so the digit pass's bounded wait for it runs out (0, the default); unroll is the sum-reduce's 16-byte chunks per worker
     per thread.  Each switch batch reads the switch keys once (a run() follows what its sort()
     recorded).  stream_blocks, combine_blocks, combine_ina_blocks, ew_blocks and switch_window
     are grid-cap sweeps that only lab builds of the library accept (make EXTRA=-DINA_LAB_KEYS=1);
@@ -1039,6 +1040,8 @@ def set_tuning(max_blocks: int | None = None, unroll: int | None = None,
         check(lib.ina_set_tuning(19, int(bool(switch_pre_all))), "set_tuning")
     if switch_local is not None:
         check(lib.ina_set_tuning(20, int(bool(switch_local))), "set_tuning")
+    if switch_decide_delay_us is not None:
+        check(lib.ina_set_tuning(21, int(switch_decide_delay_us)), "set_tuning")
     if max_blocks is not None:
         check(lib.ina_set_tuning(0, int(max_blocks)), "set_tuning")
     if unroll is not None:

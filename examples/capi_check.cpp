@@ -211,9 +211,22 @@ int main() {
         HK(hipMemcpy(act3.data(), d_act, act3.size(), hipMemcpyDeviceToHost));
         if (act3 != act) ++bad;
         for (size_t i = 0; i < n; ++i) bad += std::memcmp(&out[i], &f[i], 4) != 0;
-        // a run with no sort of its batch in the scratch is refused
+        // a run with no sort of its batch in the scratch is refused: the run above consumed the
+        // sort; a fresh sort, then runs that name another batch length, another actions buffer
+        // (the sort stored the drops in d_act) or another switch id are refused too
         const ina_switch_batch_t other{d_stream, nullptr, (size_t)W * npk - 1, stride, nullptr, d_act, d_scratch};
+        if (ina_switch(&st, &tb, nullptr, INA_SWITCH_RUN, s) != INA_EINVAL) ++bad;
+        CK(ina_switch(&st, &tb, nullptr, INA_SWITCH_SORT, s));
         if (ina_switch(&st, &other, nullptr, INA_SWITCH_RUN, s) != INA_EINVAL) ++bad;
+        uint8_t* d_act2;
+        HK(hipMalloc(&d_act2, (size_t)W * npk));
+        const ina_switch_batch_t other_act{d_stream, nullptr, (size_t)W * npk, stride, nullptr, d_act2, d_scratch};
+        if (ina_switch(&st, &other_act, nullptr, INA_SWITCH_RUN, s) != INA_EINVAL) ++bad;
+        ina_switch_state_t st2 = st;
+        st2.switch_id = st.switch_id + 1;
+        if (ina_switch(&st2, &tb, nullptr, INA_SWITCH_RUN, s) != INA_EINVAL) ++bad;
+        HK(hipStreamSynchronize(s));
+        HK(hipFree(d_act2));
         HK(hipFree(d_desc));
     }
     // the error path: a bad argument returns a code, sets a message, never exits

@@ -59,6 +59,10 @@ extern "C" {
 
 typedef void* ina_stream_t; /* hipStream_t */
 
+/* "ina-mi355x 0.2 (gfx950)".  0.2 broke the 0.1 ABI: the switch is the one struct-taking call
+ * ina_switch (+ ina_switch_process); 0.1's ina_switch_process_desc / _apply / _apply_desc /
+ * _apply_ackdesc / _split / _apply_split, ina_switch_sort_desc and ina_switch_run_sorted* are
+ * gone ("ABI 0.2"). */
 const char* ina_version(void);
 const char* ina_last_error_string(void);
 
@@ -81,7 +85,10 @@ const char* ina_last_error_string(void);
  * sort's first pass split into detection + decision + digits for every key width (1, default:
  * structured batches then skip the digits) or only for keys of 19-22 bits (0), 20 near-sorted
  * batches (V <= 32, local disorder) skip the sort and run from per-slot lists (1, default; 0 =
- * sort).  (Keys 4, 5, 6, 10 and 14, grid-cap sweeps, exist in lab builds only.)
+ * sort), 21 (tests) microseconds the near-sorted decision waits before deciding, 0..100000
+ * (0, default): the other blocks' bounded wait for it then runs out and they sort their chunks
+ * anyway -- results unchanged.  (Keys 4, 5, 6, 10 and 14, grid-cap sweeps, exist in lab builds
+ * only.)
  * Returns INA_EINVAL for an unknown key or value.                                 */
 int ina_set_tuning(int key, int value);
 
@@ -340,8 +347,11 @@ typedef struct ina_switch_ps {
  * alone: ina_nga_make_descriptors); rows must already be the batch's final address.
  * INA_SWITCH_RUN then runs the batch over that scratch (the caller orders the two: same stream
  * or an event) under the switch tuning keys the sort recorded -- ina_set_tuning between them,
- * from any thread, changes nothing in this batch.  A run over a scratch that no sort of this
- * batch (npkts, stride, layout, V, num_slots) filled is refused (INA_EINVAL).  (Batches the
+ * from any thread, changes nothing in this batch.  The run must name the SAME batch: rows, pay,
+ * actions (the sort already stored every dropped and foreign packet's action byte there; the run
+ * stores only the others), npkts, stride, V, num_slots and switch_id.  A run over a scratch that
+ * no sort of that batch filled is refused (INA_EINVAL), and a run consumes its sort's record (a
+ * second run needs a second sort).  A sort that fails leaves no record.  (Batches the
  * small-batch paths take, which sort from the headers, are sorted inside the run.) */
 #define INA_SWITCH_ALL 0
 #define INA_SWITCH_SORT 1

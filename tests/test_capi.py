@@ -200,6 +200,8 @@ def test_set_tuning_rejects_unknown_keys_and_values():
     for lab_key in (4, 5, 6, 10, 14):                           # grid-cap sweeps: lab builds only
         assert lib.ina_set_tuning(lab_key, 1) == _lib.INA_EINVAL
     assert lib.ina_set_tuning(11, 1) == _lib.INA_OK
+    assert lib.ina_set_tuning(21, -1) == _lib.INA_EINVAL       # decision delay: 0..100000 us
+    assert lib.ina_set_tuning(21, 0) == _lib.INA_OK
     assert lib.ina_set_tuning(12, 4) == _lib.INA_EINVAL        # sort: 0 auto, 3 digit passes
     assert lib.ina_set_tuning(12, 1) == _lib.INA_EINVAL        # one-sweep: moved to tools/lab
     assert lib.ina_set_tuning(12, 2) == _lib.INA_EINVAL

@@ -150,14 +150,16 @@ def test_jitter_small_V(V):
     check_vs_oracle(o, V, batches, 1 << 17, {"local"})
 
 
-def test_unit_and_subwindow_edges():
-    """Units of 512 slots and sub-windows of 8,192 positions: slots at unit edges whose
-    packets straddle sub-windows (wide jitter, few slots per unit), a slot with 600 packets
-    (one slot's list longer than a wave), and a pool of 1,000 slots (one-digit keys)."""
+def test_unit_and_window_edges():
+    """Unit and window edges: units of 4 granules whose windows reach far back (24 senders,
+    jitter 3,000: a unit's packets come from many granules before its own), a slot with 600
+    packets (one slot's list longer than a wave), and a pool of 1,000 slots (one-digit keys).
+    These cases may exceed the scan budget, so either path is accepted; the path itself is
+    asserted in test_multi_pass_lists and the jitter tests."""
     o = ops()
     V, stride = 32, o.nga_stride(32)
     rng = np.random.default_rng(3)
-    # 24 senders, 2,048 slots: a unit holds 12,288 packets, so every unit spans two sub-windows
+    # 24 senders, 2,048 slots: jitter 3,000 spreads a slot's packets over many granules
     a = [rr_batch(rng, V, 24, 2048, 1, 1 << 20, stride, 3000) for _ in range(2)]
     check_vs_oracle(o, V, a, 1 << 20, {"local", "sorted"})
     # one heavy slot: 600 packets of slot 77 spread through a jittered batch
@@ -175,6 +177,45 @@ def test_unit_and_subwindow_edges():
     check_vs_oracle(o, V, [mixed], 1 << 17, {"local", "sorted"})
     c = [rr_batch(rng, V, 8, 1000, 1, 1000, stride, 40) for _ in range(2)]
     check_vs_oracle(o, V, c, 1000, {"local"})
+
+
+@pytest.mark.parametrize("W,npk", [(2, 600_000), (1, 400_000)])
+def test_multi_pass_lists(W, npk):
+    """a unit whose slot range is wider than one LDS pass (kLlBins = 1,024 slots)
+    builds its lists in several passes (k_local_lists' q loop: the area's count taken on the
+    first pass only, the area advanced by each pass's packets).  600,000 packets take 4,096-packet
+    chunks (granules of 512 packets, units of 2,048) and 400,000 take 2,048-packet chunks (units
+    of 1,024): two senders, or one, then give units of 1,024 +- the jitter slots, so about half
+    of them take two passes.  Jitter 64 keeps the scan within budget (one sender over 2,048-packet
+    units would need three passes a unit and sort), so the near-sorted path is asserted, packet
+    for packet against the oracle."""
+    o = ops()
+    V, per = 32, npk // W
+    rng = np.random.default_rng(91 + W)
+    stride = o.nga_stride(V)
+    batches = [rr_batch(rng, V, W, per, 1 + 5 * b, 1 << 20, stride, 64, collide=0.001, degree_mix=0.001)
+               for b in range(2)]
+    check_vs_oracle(o, V, batches, 1 << 20, {"local"}, split=W == 2, write_dropped=W == 1)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_late_decision_block(split):
+    """Verdict r05 item 4: the digit pass's blocks wait for block 0's near-sorted verdict only
+    for a bounded time (kLocPollTicks, 50 us), so no block's progress depends on when block 0 is
+    dispatched.  Key 21 holds block 0 back 300 us: every other block's wait runs out and it
+    sorts its chunk; block 0 then still chooses the near-sorted path, whose lists overwrite what
+    those digits wrote.  The results must be the oracle's, packet for packet, and the path
+    'local'; a sort-only / run pair and a whole call agree."""
+    o = ops()
+    V, W, per, num_slots = 32, 8, 40_000, 1 << 20
+    rng = np.random.default_rng(123 + split)
+    stride = o.nga_stride(V)
+    batches = [rr_batch(rng, V, W, per, 1 + 3 * b, num_slots, stride, 64) for b in range(2)]
+    o.set_tuning(switch_decide_delay_us=300)
+    try:
+        check_vs_oracle(o, V, batches, num_slots, {"local"}, split=split, write_dropped=not split)
+    finally:
+        o.set_tuning(switch_decide_delay_us=0)
 
 
 def test_wide_disorder_takes_the_sort():

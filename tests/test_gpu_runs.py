@@ -603,3 +603,83 @@ def test_numpy_integer_seq0_broadcasts():
     p1 = o.quantize_pack_nga_multi(xs, 16, 32, [1, 2, 3], 3, 1, np.uint32(9))
     p2 = o.quantize_pack_nga_multi(xs, 16, 32, [1, 2, 3], 3, 1, 9)
     assert all(torch.equal(x, y) for x, y in zip(p1, p2))
+
+
+
+def _check_split_vs_oracle(o, V, batches, want_paths, write_dropped):
+    """Split rows through a fresh device switch and the oracle (state carried): actions, the
+    rewritten datagram bytes (all rows, or the forwarded ones without write_dropped) and the
+    registers after every batch, and the path each batch took."""
+    stride = batches[0].shape[1]
+    sw = o.Switch(V, num_slots=POOL, switch_id=1, device=DEV, write_dropped=write_dropped)
+    ref = orc.Switch(V, num_slots=POOL, switch_id=1)
+    for i, stream in enumerate(batches):
+        want_pk, want_act = ref.run(stream, stride=stride)
+        d = dev(stream)
+        desc = o.nga_descriptors(d)
+        hdr = torch.zeros((d.shape[0], 16), dtype=torch.uint8, device=DEV)
+        hdr[:, :15] = d[:, :15]
+        pay = d[:, 15:15 + 4 * V].contiguous()
+        act = sw.process_split(hdr, pay, desc=desc)
+        d[:, :15] = hdr[:, :15]
+        d[:, 15:15 + 4 * V] = pay
+        assert np.array_equal(host(act), want_act), i
+        got = host(d)
+        rows = slice(None) if write_dropped else want_act != orc.ACT_DROP
+        assert np.array_equal(got[rows], want_pk[rows]), i
+        assert sw.batch_path(len(stream)) in want_paths, (i, sw.batch_path(len(stream)))
+        cnt, frag, regs = ref.registers()
+        assert np.array_equal(host(sw.count), cnt), i
+        assert np.array_equal(host(sw.frag).view(np.uint32), frag), i
+        assert np.array_equal(host(sw.regs).view(np.uint32), regs), i
+
+
+@pytest.mark.parametrize("write_dropped", [False, True])
+@pytest.mark.parametrize("order", ["worker_major", "round_robin", "jitter", "shuffled"])
+@pytest.mark.parametrize("case", ["clean", "collide", "count_open", "ack_inside", "degree4", "small_V"])
+def test_whole_segments_vs_oracle(case, order, write_dropped):
+    """Round 6 (seg8_fast): split-row narrow batches whose slots hold exactly 8 packets of
+    degree 8 take the whole-segment path in every run path -- the run table (worker-major), the
+    in-order windows (round-robin), the near-sorted lists (jitter 64) and the sorted windows
+    (shuffled).  Any other segment in a wave sends that wave back to the packet-by-packet walk:
+    a frag-id collision, a slot whose count is not 0 when the batch arrives (its first 4 packets
+    came in the previous batch), a PS ack among the 8, degree 4 (two completions per segment).
+    V = 8 leaves 6 of a group's 8 lanes without payload.  Bit-exact against the P4 restatement
+    with registers after every batch, with and without write_dropped."""
+    o = ops()
+    V = 8 if case == "small_V" else 32
+    W, per = 8, 2000
+    rng = np.random.default_rng(1000 * len(case) + 10 * len(order) + int(write_dropped))
+    stride = o.nga_stride(V)
+    collide = 0.01 if case == "collide" else 0.0
+
+    def arrive(b, k):
+        n = len(b)
+        if order == "worker_major":
+            return b
+        rr = b.reshape(k, n // k, stride).transpose(1, 0, 2).reshape(n, stride)
+        if order == "round_robin":
+            return rr.copy()
+        if order == "jitter":
+            return rr[np.argsort(np.arange(n) + rng.integers(0, 64, n), kind="stable")].copy()
+        return rr[rng.permutation(n)].copy()
+
+    batches = []
+    for bi in range(2):
+        if case == "count_open" and bi == 0:
+            specs = [(5, per // 2, w) for w in range(4)]           # half the slots: 4 of 8 packets
+        else:
+            specs = [(5, per, w) for w in range(W)]
+        k = len(specs)
+        b = runs_batch(rng, V, specs, W, stride, collide=collide, degree_mix=0.0)
+        if case == "degree4":
+            b[:, 4] = 4
+        if case == "ack_inside":
+            for i in rng.choice(len(b), 20, replace=False):    # (<= 48 run breaks: still a run table)
+                b[i, 5] |= orc.FLAG_ACK                            # a PS ack among a slot's packets
+        batches.append(arrive(b, k))
+    want = {"worker_major": ("runs",), "round_robin": ("in_order",), "jitter": ("local",),
+            "shuffled": ("sorted", "local")}[order]
+    if case == "count_open" and order == "worker_major":
+        want = ("runs",)
+    _check_split_vs_oracle(o, V, batches, want, write_dropped)

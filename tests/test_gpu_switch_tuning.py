@@ -99,3 +99,30 @@ def test_run_without_its_sort_is_refused():
     sw.run(pk, act)                                # the real pair still runs
     torch.cuda.synchronize()
     assert int((act == 1).sum()) == npk // 2
+
+
+def test_run_must_name_the_sorted_batch():
+    """the sort stores every dropped and foreign packet's action byte, so a run that
+    names another actions buffer (or other rows, or another switch id) would leave those bytes
+    unwritten -- the library refuses it; a run consumes its sort, so a second run is refused."""
+    from ina_amd import _lib, ops
+    import ctypes as C
+    pk, ds, V, slots = _batch("jitter", W=2, npw=4_000)
+    sw = ops.Switch(V, num_slots=slots, switch_id=1, device=DEV)
+    act = sw.sort(pk, ds)
+    npk, stride = pk.shape
+    lib = _lib.load()
+    cs = torch.cuda.current_stream().cuda_stream
+    other_act = torch.empty_like(act)
+    other_pk = pk.clone()
+    for rows, a in ((pk, other_act), (other_pk, act)):
+        b = _lib.SwitchBatch(rows.data_ptr(), None, npk, stride, None, a.data_ptr(), sw._scratch.data_ptr())
+        assert lib.ina_switch(C.byref(sw._state), C.byref(b), None, _lib.INA_SWITCH_RUN, cs) == _lib.INA_EINVAL
+    st2 = _lib.SwitchState.from_buffer_copy(sw._state)
+    st2.switch_id = 2
+    b = _lib.SwitchBatch(pk.data_ptr(), None, npk, stride, None, act.data_ptr(), sw._scratch.data_ptr())
+    assert lib.ina_switch(C.byref(st2), C.byref(b), None, _lib.INA_SWITCH_RUN, cs) == _lib.INA_EINVAL
+    assert lib.ina_switch(C.byref(sw._state), C.byref(b), None, _lib.INA_SWITCH_RUN, cs) == 0
+    assert lib.ina_switch(C.byref(sw._state), C.byref(b), None, _lib.INA_SWITCH_RUN, cs) == _lib.INA_EINVAL
+    torch.cuda.synchronize()
+    assert int((act == 1).sum()) == npk // 2

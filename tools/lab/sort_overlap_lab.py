@@ -1,9 +1,10 @@
 """Lab: the packet path's steady-state step with the switch's slot sort taken out of the
 critical path.  The sort reads only descriptors, and descriptors follow from the header
 fields, so the sort can be queued before the worker packs: (a) one call per step as in
-bench.py (packs write the descriptors, then ina_switch_process_apply_desc); (b) the same
-stream, sort first (ina_nga_make_descriptors + ack descriptors + ina_switch_sort_desc, then
-the packs, then ina_switch_run_sorted_apply); (c) as (b) with the sort on a second stream
+bench.py (packs write the descriptors, then ina_switch with the PS step, INA_SWITCH_ALL); (b)
+the same stream, sort first (ina_nga_make_descriptors + ack descriptors + ina_switch
+INA_SWITCH_SORT, then the packs, then ina_switch INA_SWITCH_RUN with the PS step); (c) as (b)
+with the sort on a second stream
 beside the packs.  Alternated; every variant must leave the same update and actions.
 Config-3 sizes (8 x 26,214,400 fp32, V = 256, 2^17 slots)."""
 import os
