@@ -2679,10 +2679,15 @@ __device__ __forceinline__ void group_packet(const ina_switch_state_t& st, uint8
 #endif
 constexpr int kSeg8Flight = INA_SEG8_FLIGHT;
 static_assert(8 % kSeg8Flight == 0, "whole rounds of payload loads");
-template <bool kSplit>
+// kPs: the completing packet's sum goes straight into the PS update and its ack row (as
+// group_packet does).  ack_pid != ~0u (group-uniform): a PS ack leads the segment (the steady
+// state: step t's ack in front of step t+1's packets) -- it clears the slot's frag register
+// (fragcheck.p4:26-31), so the first packet's frag id is the slot's, and it is forwarded as is.
+template <bool kPs, bool kSplit>
 __device__ __forceinline__ bool seg8_fast(const ina_switch_state_t& st, uint8_t* __restrict__ pkts, size_t stride,
-                                          uint8_t* __restrict__ pay, uint8_t* __restrict__ actions, bool has,
-                                          uint32_t slot, uint32_t pidl, bool ackl, bool drop_written) {
+                                          uint8_t* __restrict__ pay, uint8_t* __restrict__ actions,
+                                          const PsFuse& ps, bool has, uint32_t slot, uint32_t pidl, bool ackl,
+                                          bool drop_written, uint32_t ack_pid = ~0u) {
     const int lane = threadIdx.x & 63, l = lane & 7, g0 = lane & ~7;
     const int V = st.V, L = V >> 2;
     const bool vl = l < L;
@@ -2691,12 +2696,15 @@ __device__ __forceinline__ bool seg8_fast(const ina_switch_state_t& st, uint8_t*
     if (has) {
         h = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pidl * (kSplit ? 16 : stride));
         cnt = st.count[slot];
-        frag = st.frag[slot];
+        if (ack_pid == ~0u) frag = st.frag[slot];
     }
     const uint32_t fin = __builtin_bswap32((h.z >> 24) | (h.w << 8));
     const uint32_t F = frag ? frag : (uint32_t)__shfl((int)fin, g0);
     const bool ok = !has || (!ackl && ((h.y >> 14) & 1u) == 0u && fin == F && (h.y & 0xFFu) == 8u && cnt == 0u);
     if (__ballot(!ok)) return false;
+    // the PS step (launch.py:46-50): this slot's update row, when the PS takes it
+    const uint32_t ps_slot = F - ps.seq0;
+    const bool consumed = kPs && has && ps_slot < ps.nslots;
     // the payload loads in flight together: kSeg8Flight at a time (the VGPRs they hold)
     constexpr int kF = kSeg8Flight;
     u32x4s run = {0u, 0u, 0u, 0u};
@@ -2720,11 +2728,12 @@ __device__ __forceinline__ bool seg8_fast(const ina_switch_state_t& st, uint8_t*
         const u32x4s v{__builtin_bswap32(m[j].x), __builtin_bswap32(m[j].y), __builtin_bswap32(m[j].z),
                        __builtin_bswap32(m[j].w)};
         run = k == 0 ? v : run + v;
-        // out_value -> the packet (processor.p4:22): the completing packet 7, and with
-        // write_dropped the dropped ones' running sums too (the id moved with every lane active:
-        // lanes past V/4 sit out the store, and a moved value from an inactive lane is undefined)
+        // out_value -> the packet (processor.p4:22): the completing packet 7 (unless the PS
+        // consumed it), and with write_dropped the dropped ones' running sums too (the id moved
+        // with every lane active: lanes past V/4 sit out the store, and a moved value from an
+        // inactive lane is undefined)
         const uint32_t pk = (uint32_t)__shfl((int)pidl, g0 + k);
-        if (has && vl && (k == 7 || st.write_dropped)) {
+        if (has && vl && (k == 7 ? (!consumed || ps.keep_fwd) : st.write_dropped)) {
             const u32x4s e{__builtin_bswap32(run.x), __builtin_bswap32(run.y), __builtin_bswap32(run.z),
                            __builtin_bswap32(run.w)};
             if constexpr (kSplit) sw_st(e, reinterpret_cast<u32x4s*>(pay + (size_t)pk * (size_t)(4 * V)) + l);
@@ -2737,8 +2746,35 @@ __device__ __forceinline__ bool seg8_fast(const ina_switch_state_t& st, uint8_t*
         if (l == 0) {
             st.count[slot] = 0u;                                  // 8 adds of count 8: back to 0
             st.frag[slot] = F;
+            if (ack_pid != ~0u) actions[ack_pid] = INA_ACT_FWD_ACK;
         }
         if (l == 7 || !drop_written) actions[pidl] = l == 7 ? INA_ACT_FWD_AGG : INA_ACT_DROP;
+        if constexpr (kPs) {
+            if (consumed) {                                       // launch.py:46-50 with the switch's sum
+                const size_t e0 = (size_t)ps_slot * (size_t)V + 4 * (size_t)l;
+                if (vl && e0 + 4 <= ps.n) {
+                    const f32x4s lc = *reinterpret_cast<const f32x4s*>(ps.local + e0);
+                    f32x4s o;
+                    o.x = __fadd_rn(lc.x, __fmul_rn(__fmul_rn((float)(int32_t)run.x, ps.inv), ps.ws));
+                    o.y = __fadd_rn(lc.y, __fmul_rn(__fmul_rn((float)(int32_t)run.y, ps.inv), ps.ws));
+                    o.z = __fadd_rn(lc.z, __fmul_rn(__fmul_rn((float)(int32_t)run.z, ps.inv), ps.ws));
+                    o.w = __fadd_rn(lc.w, __fmul_rn(__fmul_rn((float)(int32_t)run.w, ps.inv), ps.ws));
+                    __builtin_nontemporal_store(o, reinterpret_cast<f32x4s*>(ps.out + e0));
+                } else if (vl) {
+                    const uint32_t rv[4] = {run.x, run.y, run.z, run.w};
+                    for (int t = 0; t < 4 && e0 + t < ps.n; ++t)
+                        ps.out[e0 + t] = __fadd_rn(ps.local[e0 + t],
+                                                   __fmul_rn(__fmul_rn((float)(int32_t)rv[t], ps.inv), ps.ws));
+                }
+                if (l == 7 && ps.acks) {                          // the PS ack (fragcheck.p4:26-31): packet 7's header
+                    static_assert(kSplit || !kPs, "packed rows' ack rows also carry value 0's first byte");
+                    u32x4s hd = h;
+                    hd.y = (hd.y & ~0xFF00u) | ((uint32_t)INA_FLAG_ACK << 8);
+                    *reinterpret_cast<u32x4s*>(ps.acks + (size_t)ps_slot * ps.ack_stride) = hd;
+                    if (ps.ack_desc) ps.ack_desc[ps_slot] = uint2{hd.y, hd.z};
+                }
+            }
+        }
     }
     return true;
 }
@@ -2811,7 +2847,7 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
             }
             const bool has = hlen != 0;
 #if INA_SWITCH_SEG8
-            if constexpr (!kPs && kSplit) {
+            if constexpr (kSplit && !kPs) {
                 // every segment of these heads 8 packets long: the whole-segment path
                 if (maxlen == 8u && !__ballot(has && hlen != 8u)) {
                     const uint32_t q = hst + (uint32_t)l;
@@ -2827,7 +2863,7 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                             ackl = (keys(qa) & ~kmask) != 0u;
                         }
                     }
-                    if (seg8_fast<kSplit>(st, pkts, stride, pay, actions, has, hslot, pidl, ackl, drop_written))
+                    if (seg8_fast<kPs, kSplit>(st, pkts, stride, pay, actions, ps, has, hslot, pidl, ackl, drop_written))
                         continue;
                 }
             }
@@ -2933,11 +2969,11 @@ __device__ __forceinline__ void lists_slots_narrow(const ina_switch_state_t& st,
         const uint32_t slot = kmin + (uint32_t)s8 + (uint32_t)g;
         const bool has = hlen != 0;
 #if INA_SWITCH_SEG8
-        if constexpr (!kPs && kSplit) {
+        if constexpr (kSplit && !kPs) {
             // every list of these 8 slots 8 packets long: the whole-segment path
             if (maxlen == 8u && !__ballot(has && hlen != 8u) &&
-                seg8_fast<kSplit>(st, pkts, stride, pay, actions, has, slot, idl & ~kAckBit, (idl & kAckBit) != 0u,
-                                  true)) {
+                seg8_fast<kPs, kSplit>(st, pkts, stride, pay, actions, ps, has, slot, idl & ~kAckBit,
+                                       (idl & kAckBit) != 0u, true)) {
                 id_nx = (uint32_t)l < e_nx.y ? ids[e_nx.x + (uint32_t)l] : 0u;   // the next step's first ids
                 continue;
             }
@@ -3126,16 +3162,24 @@ __device__ __forceinline__ void runs_slots_narrow(const ina_switch_state_t& st, 
         const uint32_t slot = (uint32_t)(s8 + (size_t)g);
         const bool sv = s8 + (size_t)g < s_end;
 #if INA_SWITCH_SEG8
-        if constexpr (!kPs && kSplit) {
-            // 8 runs, each holding every slot of this group once: the whole-segment path (lane l
-            // of a group: run l's packet of the group's slot, in run order = arrival order)
-            if (R == 8u) {
-                const uint32_t rsl = (uint32_t)__shfl((int)rslot, l), rll = (uint32_t)__shfl((int)rlen, l),
-                               rpl = (uint32_t)__shfl((int)rpos, l);
-                const bool ackl = __shfl((int)rack_u, l) != 0;
+        if constexpr (kSplit) {
+            // 8 runs, each holding every slot of this group once -- or a run of PS acks and then
+            // 8 such runs (the packet path's steady state): the whole-segment path (lane l of a
+            // group: run l's (l + 1's) packet of the group's slot, in run order = arrival order)
+            const uint32_t a = R == 9u ? 1u : 0u;         // a leading run of acks
+            if (R - a == 8u && (a == 0u || (__builtin_amdgcn_readfirstlane(rack_u) != 0u &&
+                                            __builtin_amdgcn_readlane(rack_u, 1) == 0u))) {
+                const uint32_t rsl = (uint32_t)__shfl((int)rslot, l + (int)a), rll = (uint32_t)__shfl((int)rlen, l + (int)a),
+                               rpl = (uint32_t)__shfl((int)rpos, l + (int)a);
+                const bool ackl = __shfl((int)rack_u, l + (int)a) != 0;
                 const uint32_t off = slot - rsl;
-                if (!__ballot(sv && off >= rll) &&
-                    seg8_fast<kSplit>(st, pkts, stride, pay, actions, sv, slot, rpl + off, ackl, drop_written))
+                // the ack run's packet of this slot (a: every slot of the wave must have one)
+                const uint32_t r0s = __builtin_amdgcn_readfirstlane(rslot), r0l = __builtin_amdgcn_readfirstlane(rlen),
+                               r0p = __builtin_amdgcn_readfirstlane(rpos);
+                const uint32_t aoff = slot - r0s;
+                if (!__ballot(sv && (off >= rll || (a && aoff >= r0l))) &&
+                    seg8_fast<kPs, kSplit>(st, pkts, stride, pay, actions, ps, sv, slot, rpl + off, ackl, drop_written,
+                                           a ? r0p + aoff : ~0u))
                     continue;
             }
         }
