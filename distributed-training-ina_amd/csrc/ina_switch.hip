@@ -199,20 +199,26 @@ constexpr uint32_t kAckBit = 0x80000000u;
 
 // A batch's slot keys as the detection pass makes them (slot = index % num_slots, num_slots for
 // another switch's packets, bit 31 = PS ack when ack_hint): read from the detection pass's key
-// array, or -- narrow batches with descriptors, whose detection pass no longer writes that array
-// (round 6: 26 MB of stores in front of every NGA-32 C3 call) -- made again from the
-// descriptor, the same arithmetic (an index already below num_slots skips the division).
+// array, or -- narrow batches with descriptors (round 6) -- made again from the descriptor, the
+// same arithmetic (an index already below num_slots skips the division).  There the detection
+// pass stores a wave's keys only when the wave found a descent (a wave of a batch in slot order
+// or of a dense run stores none: 26 MB of stores left the pass in front of every NGA-32 C3 call)
+// and tags the wave's entry of `flags` with the call's epoch; a reader takes the array where the
+// tag matches and the descriptor elsewhere (the in-order run: always the descriptor).
 #ifndef INA_KEYS_FROM_DESC
 #define INA_KEYS_FROM_DESC 1
 #endif
+constexpr uint32_t kKeysSpanMax = 65535;      // slots a storing detection wave may span
 struct KeySrc {
     const uint32_t* keys;
     const uint2* desc;
     uint32_t num_slots;
     int switch_id;
     bool ack_hint;
+    const uint32_t* flags = nullptr;   // per detection wave (64 R positions, 2^kb_shift): the epoch if stored
+    uint32_t epoch = 0, kb_shift = 0;
     __device__ __forceinline__ uint32_t operator()(size_t p) const {
-        if (!desc) return keys[p];
+        if (!desc || (flags && flags[p >> kb_shift] == epoch)) return keys[p];
         const uint2 d = desc[p];
         const uint32_t idx = __builtin_bswap32((d.x >> 16) | (d.y << 16));
         const bool mine = switch_id >= 0 && ((d.y >> 16) & 0xFFu) == (uint32_t)(uint8_t)switch_id;
@@ -1008,7 +1014,7 @@ __device__ __forceinline__ size_t switch_block_index();
 #ifndef INA_LL_WAVES_PER_EU
 #define INA_LL_WAVES_PER_EU 8
 #endif
-__global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(INA_LL_WAVES_PER_EU, 8))) void k_local_lists(const KeySrc keys, size_t npk,
+__global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(INA_LL_WAVES_PER_EU, 8))) void k_local_lists(const KeySrc keys_in, size_t npk,
                                                                uint32_t num_slots, uint32_t kmask,
                                                                const uint32_t* __restrict__ unsorted,
                                                                const LocUnit* __restrict__ units, uint32_t gsize,
@@ -1019,6 +1025,8 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
     __shared__ uint32_t s_ws[kLlWaves];
     const uint32_t ep = unsorted[1];
     if (unsorted[kLocEpoch] != ep) return;                        // not this path's batch
+    KeySrc kall = keys_in;
+    kall.epoch = ep;                                              // this call's stored waves
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const int sh = (wv & 1) * 16;
     uint32_t* crow = cw[wv >> 1];
@@ -1034,6 +1042,17 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
         const uint32_t per = ((P1 - P0 + kLlWaves * 64 - 1) / (kLlWaves * 64)) * 64;
         const uint32_t b0 = min(P0 + (uint32_t)wv * per, P1), b1 = min(b0 + per, P1);
         const bool held = per <= 64u * kLlRounds;                 // the keys stay in registers
+        // one source for the whole window: the stored keys when every detection wave of the
+        // window stored its own (a near-sorted batch: each has a descent), else the descriptors
+        // (the same values) -- no per-key tag test between a load and the next
+        KeySrc keys = kall;
+        if (kall.desc && kall.flags) {
+            bool miss = false;
+            for (uint32_t f = (P0 >> kall.kb_shift) + (uint32_t)lane; f <= ((P1 - 1u) >> kall.kb_shift); f += 64u)
+                miss |= kall.flags[f] != ep;
+            if (__ballot(miss)) keys.flags = nullptr;             // the descriptors throughout
+            else keys.desc = nullptr;                             // the stored keys throughout
+        }
         uint32_t kk[kLlRounds];
         if (held) {
 #pragma unroll
@@ -1262,7 +1281,8 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                                                         uint32_t* __restrict__ brk_cnt,
                                                         uint2* __restrict__ brk_ent,
                                                         uint32_t* __restrict__ gstat, LocUnit* __restrict__ units,
-                                                        uint32_t decide_delay_ticks = 0) {
+                                                        uint32_t decide_delay_ticks = 0,
+                                                        uint32_t* __restrict__ kflags = nullptr) {
     // per-wave digit counts, then bases (2,048 bins: two waves' 16-bit halves per word)
     constexpr bool kHalf = BINS > kBkThr;
     __shared__ uint32_t base[kHalf ? kBkWaves / 2 : kBkWaves][BINS];
@@ -1390,7 +1410,7 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             else lds_count(base[wv], (key >> lb) & (nb - 1), p < npk);
         }
         if constexpr (kMode == 1)
-            if (p < npk && kout) kout[p] = k[r];   // arrival-order keys (the in-order run's; NULL: see KeySrc)
+            if (p < npk && !kflags) kout[p] = k[r];   // arrival-order keys (kflags: after the loop, see KeySrc)
         // predecessor: lane l-1 of this round (DPP wave_shr:1), lane 0 the previous round's
         // lane 63 (or, in round 0, the key loaded above)
         const uint32_t pk = (uint32_t)__builtin_amdgcn_update_dpp((int)prev, (int)key, 0x138, 0xF, 0xF, false);
@@ -1420,6 +1440,16 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         if (lane == 0) {
             wgmn[wv] = kmn;
             wgmx[wv] = kmx;
+        }
+        // (kflags) only a wave the near-sorted lists may read stores its keys: one with a descent
+        // (a wave in slot order is read from the descriptors) whose slots span at most
+        // kKeysSpanMax (a shuffled batch's waves span the pool and take the sort, which reads the
+        // descriptors itself)
+        if (kflags && __ballot(down) && kmx >= kmn && kmx - kmn <= kKeysSpanMax) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (i0 + (size_t)r * 64 < npk) kout[i0 + (size_t)r * 64] = k[r];
+            if (lane == 0) kflags[c * kBkWaves + wv] = epoch;
         }
     }
     __syncthreads();
@@ -3530,6 +3560,7 @@ struct SortAux {
     uint32_t* gstat;              // near-sorted path: granule key bounds, gmin[G] then gmax[G]
     LocUnit* units;               // near-sorted path: per unit (>= 2 granules) its slot range and window
     uint2* tab;                   // near-sorted path: per slot (first list entry, length)
+    uint32_t* kflags;             // per detection wave: the epoch of the call whose keys it stored
 };
 
 static size_t sort_nch_cap(size_t npk) {
@@ -3547,7 +3578,8 @@ static size_t sort_temp_bytes(size_t npk, uint32_t num_slots) {
     const size_t nc = sort_nch_cap(npk);
     return 2 * hist + align_up((size_t)kRsBins * 4, 256) + 1024 + align_up(nc * 4, 256) +
            align_up(nc * (size_t)kRunsMax * 8, 256) + align_up(2 * nc * kGranPerChunk * 4, 256) +
-           align_up(nc * (kGranPerChunk / 2) * sizeof(LocUnit), 256) + (size_t)num_slots * 8;
+           align_up(nc * (kGranPerChunk / 2) * sizeof(LocUnit), 256) + align_up((size_t)num_slots * 8, 256) +
+           nc * kBkWaves * 4;
 }
 
 static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
@@ -3565,6 +3597,7 @@ static SortAux sort_aux(uint8_t* aux, size_t npk, uint32_t num_slots) {
     a.gstat = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.brk_ent) + align_up(nc * (size_t)kRunsMax * 8, 256));
     a.units = reinterpret_cast<LocUnit*>(reinterpret_cast<uint8_t*>(a.gstat) + align_up(2 * nc * kGranPerChunk * 4, 256));
     a.tab = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(a.units) + align_up(nc * (kGranPerChunk / 2) * sizeof(LocUnit), 256));
+    a.kflags = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.tab) + align_up((size_t)num_slots * 8, 256));
     return a;
 }
 
@@ -3802,10 +3835,10 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         const bool pre = (sp.wide || t.pre_all) && fast;
         drop_prefill = pre;
         // the detection pass's arrival-order keys are read only by the in-order narrow run and the
-        // near-sorted lists; with descriptors both make them again from the descriptors (KeySrc)
-        // -- the 4-byte store per packet (26 MB at NGA-32 C3 size) leaves the pass in front of
-        // every call.  A sort queued alone still writes them (its run may come without the
-        // descriptors).
+        // near-sorted lists; with descriptors the pass stores only the waves that found a descent
+        // (a batch in slot order or of dense runs: none of its 26 MB at NGA-32 C3 size), the lists
+        // read those and make the rest from the descriptors, the in-order run makes all (KeySrc).
+        // A sort queued alone still writes every key (its run may come without the descriptors).
         keys_from_desc = INA_KEYS_FROM_DESC && pre && desc && phase == 0 && st->V <= kNarrowMaxV;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
@@ -3814,8 +3847,9 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
 #define INA_A_DETECT(RR)                                                                              \
             hipLaunchKernelGGL((desc ? &k_sort_chunks<RR, true, 64, 1> : &k_sort_chunks<RR, false, 64, 1>),      \
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
-                               st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, keys_from_desc ? nullptr : kc, vc, ah, \
-                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u)
+                               st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kc, vc, ah, \
+                               ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u, \
+                               keys_from_desc ? ax.kflags : nullptr)
             if (ri == 3) INA_A_DETECT(kR3 / 4);
             else if (ri == 2) INA_A_DETECT(kR2 / 4);
             else if (ri == 1) INA_A_DETECT(kR1 / 4);
@@ -3828,7 +3862,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
                                ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, \
-                               (uint32_t)t.decide_delay * 100u)
+                               (uint32_t)t.decide_delay * 100u, nullptr)
             if (ri == 3) INA_A_SORT(kR3 / 4);
             else if (ri == 2) INA_A_SORT(kR2 / 4);
             else if (ri == 1) INA_A_SORT(kR1 / 4);
@@ -3840,7 +3874,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                     : (desc ? &k_sort_chunks<RR, true, kRsBins> : &k_sort_chunks<RR, false, kRsBins>)), \
                            dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                            st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah,  \
-                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u)
+                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u, nullptr)
         if (ri == 3) INA_A_LAUNCH(kR3 / 4);
         else if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
@@ -3877,7 +3911,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
             // decision chose the path)
             hipLaunchKernelGGL(k_local_lists, dim3((unsigned)std::min<size_t>(sp.nch * kGranPerChunk / kLocU, 2048)),
                                dim3(kLlWaves * 64), 0, s,
-                               KeySrc{kc, keys_from_desc ? dsc : nullptr, st->num_slots, st->switch_id, ack_hint},
+                               KeySrc{kc, keys_from_desc ? dsc : nullptr, st->num_slots, st->switch_id, ack_hint,
+                                      ax.kflags, 0u, 6u + (uint32_t)__builtin_ctz((unsigned)(sp.rounds / 4))},
                                npk, st->num_slots, ack_hint ? ~kAckBit : 0xFFFFFFFFu,
                                ax.unsorted, ax.units, loc_gsize, k_out, ax.tab);
         if (pre) {                                 // the in-order run reads the arrival-order keys
