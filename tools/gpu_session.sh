@@ -52,7 +52,9 @@ for st in $STAGES; do
       timeout -k 10 900 python -u -m pytest tests/test_gpu_bench_contract.py -m gpu -v -rf --timeout 600 --timeout-method thread > "$OUT/contract.log" 2>&1
       rc=$?; tail -8 "$OUT/contract.log"; ok_or_fail contract $rc ;;
     bench)
-      timeout -k 10 400 python bench.py --steps 50 --warmup 10 > "$OUT/bench.json" 2> "$OUT/bench.err"
+      # the driver's own command (BENCH_rNN.json), so the session's line and the driver's are the
+      # same measurement
+      timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
       rc=$?; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -ne 0 ] && fatal bench $rc ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
