@@ -196,6 +196,16 @@ __device__ __forceinline__ void rs_tile_scatter(const uint32_t (&k)[R], const ui
 //    are not this switch's (switch_check miss, ngaa.p4:27-37,184-186); fused with the
 //    first digit pass's chunk histogram.
 constexpr uint32_t kAckBit = 0x80000000u;
+// Bit 30 of a sorted key (round 6): a PLAIN packet, one whose header fields the run can make
+// from its slot -- this switch's, flags byte 0, index == slot (< num_slots), count field == C and
+// frag id == index + B, with B and C the call's constants (header row 0's frag id - index and
+// count).  Senders that number fragments in sequence and index slots by them
+// (DataManager.py:116-134: index = (seq + i) mod pool, frag id = seq + i) make every packet of a
+// pass over the pool plain.  The digit pass of a shuffled narrow split-row batch reads the
+// header rows in arrival order (coalesced) and sets the bit; the sorted run then reads no header
+// row for a plain packet -- each such read was a random 16-byte gather costing a whole line.
+// No digit covers the bit; the run masks it out of the slot.
+constexpr uint32_t kPlainBit = 0x40000000u;
 
 // A batch's slot keys as the detection pass makes them (slot = index % num_slots, num_slots for
 // another switch's packets, bit 31 = PS ack when ack_hint): read from the detection pass's key
@@ -205,6 +215,9 @@ constexpr uint32_t kAckBit = 0x80000000u;
 // or of a dense run stores none: 26 MB of stores left the pass in front of every NGA-32 C3 call)
 // and tags the wave's entry of `flags` with the call's epoch; a reader takes the array where the
 // tag matches and the descriptor elsewhere (the in-order run: always the descriptor).
+#ifndef INA_SWITCH_PLAIN
+#define INA_SWITCH_PLAIN 1
+#endif
 #ifndef INA_KEYS_FROM_DESC
 #define INA_KEYS_FROM_DESC 1
 #endif
@@ -736,6 +749,8 @@ constexpr int kRunsStart = 1, kRunsKey = 2 + kRunsMax;
 constexpr int kCtlLocal = kCtlRuns + kRunsKey + kRunsMax;
 constexpr int kLocEpoch = kCtlLocal - kCtlEpochs;     // offsets from the epochs (`unsorted`)
 constexpr int kLocKmin = kLocEpoch + 1, kLocSlots = kLocEpoch + 2, kLocUnits = kLocEpoch + 3;
+// the sorted narrow run's plain-packet constants (see kPlainBit): frag id - index, count field
+constexpr int kPlainB = kLocEpoch + 4, kPlainC = kLocEpoch + 5;
 constexpr int kLocVerdict = kLocEpoch + 6;            // 2 words: the decision, (epoch << 1) | local
 static_assert((kCtlEpochs + kLocVerdict) % 2 == 0, "the verdict is 8-byte aligned in the control block");
 constexpr int kCtlWords = kCtlLocal + 8;
@@ -1282,7 +1297,8 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                                                         uint2* __restrict__ brk_ent,
                                                         uint32_t* __restrict__ gstat, LocUnit* __restrict__ units,
                                                         uint32_t decide_delay_ticks = 0,
-                                                        uint32_t* __restrict__ kflags = nullptr) {
+                                                        uint32_t* __restrict__ kflags = nullptr,
+                                                        const uint32_t* __restrict__ plain_hdr = nullptr) {
     // per-wave digit counts, then bases (2,048 bins: two waves' 16-bit halves per word)
     constexpr bool kHalf = BINS > kBkThr;
     __shared__ uint32_t base[kHalf ? kBkWaves / 2 : kBkWaves][BINS];
@@ -1373,7 +1389,36 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         for (uint32_t d = lane; d < nb; d += 64) base[kHalf ? wv >> 1 : wv][d] = 0;
     const size_t i0 = c * (size_t)(kBkThr * R) + (size_t)wv * (64 * R) + (size_t)lane;
     uint32_t idx[R], sid[R], ack[R], k[R], v[R];
-    load_key_fields<R, kDesc>(pkts, desc, npk, stride, i0, idx, sid, ack);
+    uint32_t plainm = 0u;                                     // bit r: round r's packet is plain
+    if (kMode == 2 && plain_hdr) {
+        // (split header rows, 16 B each) the key fields and the plain test from one row read
+        const uint32_t w01 = plain_hdr[1], w02 = plain_hdr[2], w03 = plain_hdr[3];
+        const uint32_t C0 = w01 & 0xFFu;
+        const uint32_t B0 = __builtin_bswap32((w02 >> 24) | (w03 << 8)) - __builtin_bswap32((w01 >> 16) | (w02 << 16));
+        if (c == 0 && threadIdx.x == 0) {
+            unsorted[kPlainB] = B0;
+            unsorted[kPlainC] = C0;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t p = i0 + (size_t)r * 64;
+            uint32_t w1 = 0, w2 = 0, w3 = 0;
+            if (p < npk) {
+                const uint32_t* pk = plain_hdr + p * 4;
+                w1 = pk[1];
+                w2 = pk[2];
+                w3 = pk[3];
+            }
+            idx[r] = __builtin_bswap32((w1 >> 16) | (w2 << 16));
+            sid[r] = (w2 >> 16) & 0xFFu;
+            ack[r] = (w1 >> 14) & 1u;
+            const uint32_t fr = __builtin_bswap32((w2 >> 24) | (w3 << 8));
+            const bool pl = (w1 & 0xFFFFu) == C0 && idx[r] < num_slots && fr - idx[r] == B0;
+            plainm |= pl ? 1u << r : 0u;
+        }
+    } else {
+        load_key_fields<R, kDesc>(pkts, desc, npk, stride, i0, idx, sid, ack);
+    }
     // the key before the wave's first item (the previous wave's or chunk's last): every lane
     // loads the same entry
     uint32_t pidx[1], psid[1], pack[1];
@@ -1396,7 +1441,7 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             kmx = max(kmx, key);
         }
         // bit 31 carries "PS ack" through the sort (no digit reads it)
-        k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u);
+        k[r] = key | ((ack_hint && mine && ack[r]) ? kAckBit : 0u) | ((mine && ((plainm >> r) & 1u)) ? kPlainBit : 0u);
         v[r] = (uint32_t)p;
         if (kMode == 0 && p < npk && !mine) actions[p] = INA_ACT_FWD_OTHER;   // switch_check miss, ngaa.p4:184-186
         // the detection pass stores EVERY packet's action byte by position: foreign packets
@@ -2717,20 +2762,24 @@ template <bool kPs, bool kSplit>
 __device__ __forceinline__ bool seg8_fast(const ina_switch_state_t& st, uint8_t* __restrict__ pkts, size_t stride,
                                           uint8_t* __restrict__ pay, uint8_t* __restrict__ actions,
                                           const PsFuse& ps, bool has, uint32_t slot, uint32_t pidl, bool ackl,
-                                          bool drop_written, uint32_t ack_pid = ~0u) {
+                                          bool drop_written, uint32_t ack_pid = ~0u, bool plainl = false,
+                                          uint32_t plB = 0u, uint32_t plC = 0u) {
     const int lane = threadIdx.x & 63, l = lane & 7, g0 = lane & ~7;
     const int V = st.V, L = V >> 2;
     const bool vl = l < L;
     u32x4s h = {0u, 0u, 0u, 0u};
     uint32_t cnt = 0u, frag = 0u;
+    // a plain packet (kPlainBit, sorted window path without the PS step): no header row read
+    const bool pl = !kPs && plainl;
     if (has) {
-        h = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pidl * (kSplit ? 16 : stride));
+        if (!pl) h = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pidl * (kSplit ? 16 : stride));
         cnt = st.count[slot];
         if (ack_pid == ~0u) frag = st.frag[slot];
     }
-    const uint32_t fin = __builtin_bswap32((h.z >> 24) | (h.w << 8));
+    const uint32_t fin = pl ? slot + plB : __builtin_bswap32((h.z >> 24) | (h.w << 8));
     const uint32_t F = frag ? frag : (uint32_t)__shfl((int)fin, g0);
-    const bool ok = !has || (!ackl && ((h.y >> 14) & 1u) == 0u && fin == F && (h.y & 0xFFu) == 8u && cnt == 0u);
+    const bool hok = pl ? plC == 8u : (!ackl && ((h.y >> 14) & 1u) == 0u && (h.y & 0xFFu) == 8u);
+    const bool ok = !has || (hok && fin == F && cnt == 0u);
     if (__ballot(!ok)) return false;
     // the PS step (launch.py:46-50): this slot's update row, when the PS takes it
     const uint32_t ps_slot = F - ps.seq0;
@@ -2821,13 +2870,17 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                                                     const KeySrc keys, const uint32_t* __restrict__ ids,
                                                     uint8_t* __restrict__ actions, uint32_t win, uint32_t kmask,
                                                     const PsFuse& ps, size_t wave, size_t nwaves,
-                                                    bool drop_written = false) {
+                                                    bool drop_written = false, uint32_t plB = 0u,
+                                                    uint32_t plC = 0u) {
     constexpr int kP = kSlotInFlight<kSplit>;
+    // plain packets (kPlainBit: set only for split rows without the PS step) read no header row
+    constexpr bool kPlain = kSplit && !kPs;
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, l = lane & 7;
     const int V = st.V, L = V >> 2;
     const bool vl = l < L;
     const uint32_t NS = st.num_slots;
+    const uint32_t xm = ~kmask;                           // the hint bits: PS ack, plain
     // the window's packet ids and ack hints, for the lane groups to pick from (through LDS,
     // written by every lane of the wave: see group_packet on DPP / permutes and EXEC)
     __shared__ uint32_t s_wid[kSwBlock], s_wack[kSwBlock];
@@ -2841,7 +2894,8 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
         const bool head = (uint32_t)lane < win && i < npk && ki < NS && (i == 0 || kp != ki);
         __builtin_amdgcn_wave_barrier();
         s_wid[threadIdx.x] = idw;
-        s_wack[threadIdx.x] = (kr & ~kmask) != 0u ? 1u : 0u;   // a PS ack by its key (with the hint)
+        // bit 0: a PS ack by its key (with the hint); bit 1: a plain packet
+        s_wack[threadIdx.x] = ((kr & xm & kAckBit) ? 1u : 0u) | ((kr & xm & kPlainBit) ? 2u : 0u);
         __builtin_amdgcn_wave_barrier();
         unsigned long long hm = __ballot(head);
         while (hm) {
@@ -2881,19 +2935,20 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                 // every segment of these heads 8 packets long: the whole-segment path
                 if (maxlen == 8u && !__ballot(has && hlen != 8u)) {
                     const uint32_t q = hst + (uint32_t)l;
-                    uint32_t pidl = 0u;
-                    bool ackl = false;
+                    uint32_t pidl = 0u, hint = 0u;
                     if (has) {
                         if (q < 64u) {
                             pidl = s_wid[wb + (int)q];
-                            ackl = s_wack[wb + (int)q] != 0u;
+                            hint = s_wack[wb + (int)q];
                         } else {
                             const size_t qa = w0 + (size_t)q;
                             pidl = ids ? ids[qa] : (uint32_t)qa;
-                            ackl = (keys(qa) & ~kmask) != 0u;
+                            const uint32_t kq = keys(qa) & xm;
+                            hint = ((kq & kAckBit) ? 1u : 0u) | ((kq & kPlainBit) ? 2u : 0u);
                         }
                     }
-                    if (seg8_fast<kPs, kSplit>(st, pkts, stride, pay, actions, ps, has, hslot, pidl, ackl, drop_written))
+                    if (seg8_fast<kPs, kSplit>(st, pkts, stride, pay, actions, ps, has, hslot, pidl, (hint & 1u) != 0u,
+                                               drop_written, ~0u, (hint & 2u) != 0u, plB, plC))
                         continue;
                 }
             }
@@ -2914,24 +2969,36 @@ __device__ __forceinline__ void window_slots_narrow(const ina_switch_state_t& st
                     const uint32_t k = k0 + (uint32_t)j;
                     const uint32_t q = hst + k;           // window-relative position
                     in[j] = has && k < hlen;
-                    // id and ack hint: the window's (LDS), past the window from memory
+                    // id and hints: the window's (LDS), past the window from memory
                     pid[j] = 0u;
-                    acq[j] = false;
+                    uint32_t hint = 0u;
                     if (in[j]) {
                         if (q < 64u) {
                             pid[j] = s_wid[wb + (int)q];
-                            acq[j] = s_wack[wb + (int)q] != 0u;
+                            hint = s_wack[wb + (int)q];
                         } else {
                             const size_t qa = w0 + (size_t)q;
                             pid[j] = ids ? ids[qa] : (uint32_t)qa;
-                            acq[j] = (keys(qa) & ~kmask) != 0u;
+                            const uint32_t kq = keys(qa) & xm;
+                            hint = ((kq & kAckBit) ? 1u : 0u) | ((kq & kPlainBit) ? 2u : 0u);
                         }
                     }
+                    acq[j] = (hint & 1u) != 0u;
                     if (in[j] && !acq[j]) {
                         if constexpr (kSplit) {
                             m[j] = sw_ld(reinterpret_cast<const u32x4s*>(pay + (size_t)pid[j] * (size_t)(4 * V)) +
                                          (vl ? l : 0));
-                            h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+                            if (kPlain && (hint & 2u)) {
+                                // the header fields group_packet reads, made from the slot: words 1-3
+                                // of the row (count, flags 0, index = slot, switch id, frag id, pad 0)
+                                const uint32_t fr = hslot + plB;
+                                h[j] = u32x4s{0u, plC | (__builtin_bswap32(hslot) & 0xFFFFu) << 16,
+                                              (__builtin_bswap32(hslot) >> 16) | ((uint32_t)(uint8_t)st.switch_id << 16) |
+                                                  (fr & 0xFF000000u),
+                                              (__builtin_bswap32(fr) >> 8)};
+                            } else {
+                                h[j] = *reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * 16);
+                            }
                         } else {
                             const u32x4s* pk = reinterpret_cast<const u32x4s*>(pkts + (size_t)pid[j] * stride);
                             if constexpr (INA_PACKED_UNALIGNED)
@@ -3069,13 +3136,14 @@ __device__ __forceinline__ void switch_run2_body(const ina_switch_state_t& st, u
                                                  uint8_t* __restrict__ actions, uint32_t win,
                                                  uint32_t kmask, const PsFuse& ps, size_t wave,
                                                  size_t nwaves, bool drop_written = false,
-                                                 const uint2* __restrict__ kdesc = nullptr) {
+                                                 const uint2* __restrict__ kdesc = nullptr,
+                                                 uint32_t plB = 0u, uint32_t plC = 0u) {
 #if INA_SWITCH_NARROW_SLOTS
     if constexpr (kNarrow) {
         // (kdesc: a batch in slot order whose keys come from its descriptors, see KeySrc)
         const KeySrc ks{keys, kdesc, st.num_slots, st.switch_id, kmask != 0xFFFFFFFFu};
         window_slots_narrow<kPs, kSplit>(st, pkts, pay, npk, stride, ks, ids, actions, win, kmask, ps, wave,
-                                         nwaves, drop_written);
+                                         nwaves, drop_written, plB, plC);
         return;
     }
 #endif
@@ -3324,7 +3392,7 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
         rlen = runs[kRunsStart + lane + 1] - rpos;
         const uint32_t rk = runs[kRunsKey + lane];
         rslot = rk & kmask;
-        rack = (rk & ~kmask) != 0u;
+        rack = (rk & ~kmask & kAckBit) != 0u;
         if (rslot >= NS) rlen = 0;                    // foreign packets: A set their action
     }
     // the slots the runs cover: [lo, hi)
@@ -3435,6 +3503,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
     const size_t nwaves = ((size_t)gridDim.x * kSwBlock) >> 6;
     // (unsorted[1]: the epoch of the sort that filled the scratch, written by its chunk pass,
     // so a run queued apart from its sort needs no host-side state)
+    uint32_t plB = 0u, plC = 0u;                            // (sorted keys with kPlainBit)
     if (unsorted) {
         const uint32_t ep = unsorted[1];
         if (unsorted[kLocEpoch] == ep) {                   // a near-sorted batch: its per-slot lists
@@ -3459,6 +3528,10 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
             if (!ids_a) nforeign = nullptr;
         } else {
             kdesc = nullptr;                                // only an in-order batch reads them
+            if constexpr (kNarrow && kSplit && !kPs) {
+                plB = unsorted[kPlainB];
+                plC = unsorted[kPlainC];
+            }
         }
     } else {
         kdesc = nullptr;
@@ -3467,7 +3540,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
     // the run kernel never processes foreign packets, so it stops before them
     if (nforeign) npk -= *nforeign;
     switch_run2_body<kPs, false, kNarrow, kSplit>(st, pkts, pay, npk, stride, keys, ids, actions, win, kmask, ps,
-                                                  wave, nwaves, drop_prefill != 0, kdesc);
+                                                  wave, nwaves, drop_prefill != 0, kdesc, plB, plC);
 }
 
 // batches of at most INA_SWITCH_TINY_MAX packets (latency, not bandwidth): ONE launch of
@@ -3783,6 +3856,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
     uint32_t loc_gsize = 0;                 // the near-sorted path's granule: 1/8 of a sort chunk
     bool drop_prefill = false;              // the detection pass (mode 1) stores every packet's drop
     bool keys_from_desc = false;            // narrow + descriptors, one call: no arrival-order key array
+    bool plain = false;                     // the digit pass marks plain packets (kPlainBit)
     if (small && fast && npk <= (size_t)t.tiny_max) {
         // sort and run in ONE launch of one workgroup (k_switch_tiny)
         if (!do_run) return sorted_ok();
@@ -3840,6 +3914,12 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         // read those and make the rest from the descriptors, the in-order run makes all (KeySrc).
         // A sort queued alone still writes every key (its run may come without the descriptors).
         keys_from_desc = INA_KEYS_FROM_DESC && pre && desc && phase == 0 && st->V <= kNarrowMaxV;
+        // plain packets (kPlainBit): the digit pass of a narrow split-row batch reads its header rows
+        // and marks them, so the sorted run reads no header row for them.  One call only (a sort
+        // queued alone reads nothing but the descriptors), no PS step, and the ack hint on (both
+        // hint bits outside the digits, masked out of the slot by the run)
+        plain = INA_SWITCH_PLAIN && pre && split && phase == 0 && !ps.on && ack_hint && st->V <= kNarrowMaxV &&
+                sp.passes * sp.bits <= 30 && st->num_slots < kPlainBit;
         if (do_sort) {
         epoch = g_sort_epoch.fetch_add(1u) + 1u;
         if (epoch == 0u) epoch = g_sort_epoch.fetch_add(1u) + 1u;
@@ -3849,7 +3929,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kc, vc, ah, \
                                ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u, \
-                               keys_from_desc ? ax.kflags : nullptr)
+                               keys_from_desc ? ax.kflags : nullptr, nullptr)
             if (ri == 3) INA_A_DETECT(kR3 / 4);
             else if (ri == 2) INA_A_DETECT(kR2 / 4);
             else if (ri == 1) INA_A_DETECT(kR1 / 4);
@@ -3862,7 +3942,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                                st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah, \
                                ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, \
-                               (uint32_t)t.decide_delay * 100u, nullptr)
+                               (uint32_t)t.decide_delay * 100u, nullptr,                                  \
+                               plain ? reinterpret_cast<const uint32_t*>(pkts) : nullptr)
             if (ri == 3) INA_A_SORT(kR3 / 4);
             else if (ri == 2) INA_A_SORT(kR2 / 4);
             else if (ri == 1) INA_A_SORT(kR1 / 4);
@@ -3874,7 +3955,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                                     : (desc ? &k_sort_chunks<RR, true, kRsBins> : &k_sort_chunks<RR, false, kRsBins>)), \
                            dim3(gc), dim3(kBkThr), 0, s, pkts, dsc, npk, stride, st->num_slots,       \
                            st->switch_id, actions, sp.hbits, lb, ax.hist, ax.rst, sp.nch, kn, vn, ah,  \
-                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u, nullptr)
+                           ax.unsorted, epoch, runs_on ? ax.brk_cnt : nullptr, ax.brk_ent, loc ? ax.gstat : nullptr, ax.units, 0u, nullptr, \
+                           nullptr)
         if (ri == 3) INA_A_LAUNCH(kR3 / 4);
         else if (ri == 2) INA_A_LAUNCH(kR2 / 4);
         else if (ri == 1) INA_A_LAUNCH(kR1 / 4);
@@ -3989,7 +4071,8 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
                           : (ps.on ? (narrow ? &k_switch_run2<true, true, false> : &k_switch_run2<true, false, false>)
                                    : (narrow ? &k_switch_run2<false, true, false> : &k_switch_run2<false, false, false>));
         hipLaunchKernelGGL(run, dim3(gr), dim3(kSwBlock), 0, s, *st, pkts, pay, npk, stride, kc, vc, actions,
-                           win, ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn, unsorted, k_out, ax.tab,
+                           win, plain ? ~(kAckBit | kPlainBit) : ack_hint ? ~kAckBit : 0xFFFFFFFFu, ps, nforeign, kn, vn,
+                           unsorted, k_out, ax.tab,
                            drop_prefill ? 1 : 0, keys_from_desc ? reinterpret_cast<const uint2*>(desc) : nullptr);
         *fused_out = ps.on != 0;
     } else {

@@ -606,13 +606,13 @@ def test_numpy_integer_seq0_broadcasts():
 
 
 
-def _check_split_vs_oracle(o, V, batches, want_paths, write_dropped):
+def _check_split_vs_oracle(o, V, batches, want_paths, write_dropped, num_slots=POOL):
     """Split rows through a fresh device switch and the oracle (state carried): actions, the
     rewritten datagram bytes (all rows, or the forwarded ones without write_dropped) and the
     registers after every batch, and the path each batch took."""
     stride = batches[0].shape[1]
-    sw = o.Switch(V, num_slots=POOL, switch_id=1, device=DEV, write_dropped=write_dropped)
-    ref = orc.Switch(V, num_slots=POOL, switch_id=1)
+    sw = o.Switch(V, num_slots=num_slots, switch_id=1, device=DEV, write_dropped=write_dropped)
+    ref = orc.Switch(V, num_slots=num_slots, switch_id=1)
     for i, stream in enumerate(batches):
         want_pk, want_act = ref.run(stream, stride=stride)
         d = dev(stream)
@@ -683,3 +683,49 @@ def test_whole_segments_vs_oracle(case, order, write_dropped):
     if case == "count_open" and order == "worker_major":
         want = ("runs",)
     _check_split_vs_oracle(o, V, batches, want, write_dropped)
+
+
+@pytest.mark.parametrize("write_dropped", [False, True])
+@pytest.mark.parametrize("case", ["base", "base_b", "row0_foreign", "index_high", "flags", "refrag",
+                                  "wrap", "degree4"])
+def test_plain_packets_vs_oracle(case, write_dropped):
+    """Round 6 (kPlainBit): the digit pass of a shuffled narrow split-row batch marks each packet
+    whose header fields follow from its slot -- flags 0, index == slot, count == C, frag id ==
+    index + B, with B and C taken from header row 0 -- and the sorted run makes those fields
+    instead of gathering the header row.  Cases: B = 0 and B = 3 x pool; row 0 another switch's
+    packet with its own frag id (B and C from it: few packets plain); 10 % of the rows with index
+    + pool (same slot, not plain); 5 % with the resend flag; a second batch whose frag ids are
+    one pool further on (every plain packet collides with the slot's stored frag id: the
+    collision rewrite writes the made header word); a pool of 2^10 slots that the batch wraps
+    (B holds for one pass of the pool only); degree 4 (plain with C = 4: not whole segments).
+    Bit-exact against the P4 restatement, registers after every batch."""
+    o = ops()
+    V, W, per = 32, 8, 2000
+    num_slots = (1 << 10) if case == "wrap" else POOL
+    rng = np.random.default_rng(7000 + 10 * len(case) + int(write_dropped))
+    stride = o.nga_stride(V)
+    seq0 = 3 * num_slots + 5 if case == "base_b" else 5
+    batches = []
+    for bi in range(2):
+        s0 = seq0 + (num_slots if case == "refrag" and bi == 1 else 0)
+        specs = [(s0, per, w) for w in range(W)]
+        b = runs_batch(rng, V, specs, W, stride, num_slots=num_slots, collide=0.0, degree_mix=0.0)
+        if case == "degree4":
+            b[:, 4] = 4
+        if case == "index_high":
+            for i in np.flatnonzero(rng.random(len(b)) < 0.1):
+                ix = int.from_bytes(b[i, 6:10].tobytes(), "big") + num_slots
+                b[i, 6:10] = np.frombuffer(ix.to_bytes(4, "big"), np.uint8)
+        if case == "flags":
+            b[rng.random(len(b)) < 0.05, 5] |= orc.FLAG_RESEND
+        b = b[rng.permutation(len(b))].copy()
+        if case == "row0_foreign":
+            f = runs_batch(rng, V, [(999999, 1, "foreign")], W, stride, num_slots=num_slots,
+                           collide=0.0, degree_mix=0.0)
+            b = np.concatenate([f, b])
+        batches.append(b)
+    o.set_tuning(switch_local=False)          # small shuffled batches may take the lists instead
+    try:
+        _check_split_vs_oracle(o, V, batches, ("sorted",), write_dropped, num_slots=num_slots)
+    finally:
+        o.set_tuning(switch_local=True)
