@@ -1204,14 +1204,16 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
 // chunk blocks or three bucket blocks (1,024 bins) share a CU instead of one.
 // rs_tile_scatter over the packed counts: each wave's offset of digit d inside the digit's
 // run in this chunk (16-bit halves), the run's first output position in gst[d]
-template <int R, int BINS, bool kStage = false>
+// kPosOnly: no stores -- each item's place minus sbase into spos_out (~0u: none), for a caller
+// that stages the output itself
+template <int R, int BINS, bool kStage = false, bool kPosOnly = false>
 __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], const uint32_t (&v)[R],
                                                      size_t i0, size_t n, int shift, int bits,
                                                      uint32_t (*base)[BINS], const uint32_t* gst,
                                                      uint32_t* __restrict__ kout,
                                                      uint32_t* __restrict__ vout, int rw = R,
                                                      uint32_t* sk = nullptr, uint32_t* sv = nullptr,
-                                                     uint32_t sbase = 0u) {
+                                                     uint32_t sbase = 0u, uint32_t* spos_out = nullptr) {
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     const int sh = (wv & 1) * 16;
     uint32_t* row = base[wv >> 1];
@@ -1245,7 +1247,9 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
         const uint32_t b0 = (row[d] >> sh) & 0xFFFFu;
         if (valid) {
             const uint32_t pos = gst[d] + b0 + rank;
-            if constexpr (kStage) {                   // the chunk's output staged in LDS
+            if constexpr (kPosOnly) {
+                spos[r] = pos - sbase;
+            } else if constexpr (kStage) {            // the chunk's output staged in LDS
 #if INA_SORT_STAGE_ALIAS
                 spos[r] = pos - sbase;
 #else
@@ -1258,6 +1262,11 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
             }
             if (rank == 0) atomicAdd(&row[d], (uint32_t)__builtin_popcountll(pm) << sh);
         }
+    }
+    if constexpr (kPosOnly) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) spos_out[r] = spos[r];
+        return;
     }
 #if INA_SORT_STAGE_ALIAS
     if constexpr (kStage) {
@@ -1281,6 +1290,24 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
 // (every block sums the break counts; dense runs: block 0 writes the run table) and, for a
 // batch neither in slot order nor dense runs, the digits + scatter.
 // lab builds only (timing what the detection pass's action stores cost; results then differ)
+// The digit pass writes each chunk's (digit, chunk) run lengths and starts as COLUMNS (word c of
+// row d): neighbouring chunks write neighbouring words, so a line of them is written by 32 chunk
+// blocks.  Dispatched round-robin over the XCDs, those blocks sat on 8 L2s and each wrote the line
+// back partly: 182 MB written against 59 MB of data at NGA-32 C3 size.  With neighbouring chunks
+// on one XCD (switch_block_index) the line fills in one L2: 69 MB, shuffled split 436 -> 426 us
+// (profiles/r06/lab/sort_stage_xcd_ab_v32.log)
+#ifndef INA_CHUNK_XCD
+#define INA_CHUNK_XCD 1
+#endif
+// A one-tile bucket's sorted keys and values leave through LDS as two contiguous runs instead of
+// scattered 4-byte stores: the bucket pass wrote 214 MB for 52 MB of keys and values, now 52 MB;
+// shuffled split 436 -> 404 us, with the chunk mapping 393 us (same log; NGA-256 neutral)
+#ifndef INA_BUCKET_STAGE
+#define INA_BUCKET_STAGE 1
+#endif
+#ifndef INA_BUCKET_XCD
+#define INA_BUCKET_XCD 0
+#endif
 #ifndef INA_LAB_DETECT_NOACT
 #define INA_LAB_DETECT_NOACT 0
 #endif
@@ -1307,7 +1334,8 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     __shared__ uint32_t wbrk[kBkWaves];               // per-wave break counts
     __shared__ uint32_t wgmn[kBkWaves], wgmx[kBkWaves];   // per-wave slot-key bounds (near-sorted path)
     const int lane = threadIdx.x & 63, wv = wave_in_block();
-    const size_t c = blockIdx.x;
+    // (INA_CHUNK_XCD: neighbouring chunks on one XCD, so the (digit, chunk) columns they write share its L2)
+    const size_t c = INA_CHUNK_XCD && kMode == 2 ? switch_block_index() : blockIdx.x;
     // gstat (near-sorted path on): granule bounds, gmin[G] then gmax[G], G = 8 granules a chunk
     const uint32_t G = (uint32_t)nch * (uint32_t)kGranPerChunk;
     if constexpr (kMode == 2) {
@@ -1644,7 +1672,8 @@ __global__ __launch_bounds__(kBkThr, BINS <= 1024 ? 2 * kBkThr / 256 : kBkThr / 
     __shared__ uint32_t gst[BINS];                    // bucket digit counts, then output positions
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
-    const uint32_t b = blockIdx.x;
+    // (INA_BUCKET_XCD: neighbouring buckets on one XCD: their runs in a chunk share lines, read through one L2)
+    const uint32_t b = INA_BUCKET_XCD ? (uint32_t)switch_block_index() : blockIdx.x;
     // keys already in slot order: A's output is the sorted order and the register-resident
     // run kernel reads it there (sorted_copy = 0), so only the foreign bucket's size is needed
     const bool in_order = unsorted[0] != epoch;
@@ -1830,9 +1859,35 @@ __global__ __launch_bounds__(kBkThr, BINS <= 1024 ? 2 * kBkThr / 256 : kBkThr / 
         }
         __syncthreads();
         BK_STAMP(3);
-        // (staging a one-tile bucket's output in LDS to leave as one contiguous run measured
-        // no faster: 244.5 -> 244.1 us worker-major, 228.3 -> 229.9 round-robin,
-        // profiles/r03/lab/bucket_stage_lab.log)
+        // (staging a one-tile bucket's output in LDS: round 3 measured it neutral at NGA-256,
+        // profiles/r03/lab/bucket_stage_lab.log; at NGA-32 it cuts the pass's writes 4x, see
+        // INA_BUCKET_STAGE)
+#if INA_BUCKET_STAGE
+        if constexpr (kHalf) {
+            if (ntile == 1) {
+                // a one-tile bucket leaves as two contiguous runs: keys, then values, each staged in
+                // the count array once every wave has read its offsets (8 x BINS words >= a tile)
+                static_assert((kBkWaves / 2) * BINS >= (int)kTile, "a tile fits the count array");
+                uint32_t sp[R];
+                rs_tile_scatter_half<R, BINS, false, true>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw,
+                                                           nullptr, nullptr, s0, sp);
+                uint32_t* stg = &base[0][0];
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (sp[r] != 0xFFFFFFFFu) stg[sp[r]] = k[r];
+                __syncthreads();
+                for (uint32_t i = threadIdx.x; i < cnt; i += kBkThr) kout[s0 + i] = stg[i];
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (sp[r] != 0xFFFFFFFFu) stg[sp[r]] = v[r];
+                __syncthreads();
+                for (uint32_t i = threadIdx.x; i < cnt; i += kBkThr) vout[s0 + i] = stg[i];
+                return;
+            }
+        }
+#endif
         if constexpr (kHalf) rs_tile_scatter_half<R, BINS>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
         else rs_tile_scatter<R, kBkWaves, BINS>(k, v, i0, t_end, 0, lbits, base, gst, kout, vout, rw);
         __syncthreads();
