@@ -1308,6 +1308,15 @@ __device__ __forceinline__ void rs_tile_scatter_half(const uint32_t (&k)[R], con
 #ifndef INA_BUCKET_XCD
 #define INA_BUCKET_XCD 0
 #endif
+// Groups of 8 neighbouring buckets on one XCD: a bucket's run in a digit-pass chunk is ~6 items,
+// so the runs of neighbouring buckets share lines, and round-robin dispatch read each line into
+// up to eight L2s (218 MB read for ~60 MB at NGA-32 C3 size, shuffled).  Groups of 8: 79 MB, the
+// shuffled split call 386 -> 378 us, packed 554 / 515 -> 538 / 506 us, NGA-256 -2 us.  All 128 of
+// an XCD's buckets in one run (INA_BUCKET_XCD) reads 62 MB but costs 7 us: its in-flight blocks
+// then share too few lines (profiles/r06/lab/bucket_group_ab_v32.log, bucket_xcd_ab_v32.log)
+#ifndef INA_BUCKET_GROUP
+#define INA_BUCKET_GROUP 8
+#endif
 #ifndef INA_LAB_DETECT_NOACT
 #define INA_LAB_DETECT_NOACT 0
 #endif
@@ -1673,7 +1682,18 @@ __global__ __launch_bounds__(kBkThr, BINS <= 1024 ? 2 * kBkThr / 256 : kBkThr / 
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     // (INA_BUCKET_XCD: neighbouring buckets on one XCD: their runs in a chunk share lines, read through one L2)
-    const uint32_t b = INA_BUCKET_XCD ? (uint32_t)switch_block_index() : blockIdx.x;
+    uint32_t b = INA_BUCKET_XCD ? (uint32_t)switch_block_index() : blockIdx.x;
+#if INA_BUCKET_GROUP > 1
+    {   // groups of INA_BUCKET_GROUP neighbouring buckets on one XCD (blocks go to the XCDs
+        // round-robin); the grid's tail past whole groups of 8 x G keeps its own index
+        constexpr uint32_t G = INA_BUCKET_GROUP;
+        const uint32_t p = blockIdx.x, full = (gridDim.x / (8u * G)) * (8u * G);
+        if (p < full) {
+            const uint32_t x = p & 7u, i = p >> 3;
+            b = (i / G) * (8u * G) + x * G + (i % G);
+        }
+    }
+#endif
     // keys already in slot order: A's output is the sorted order and the register-resident
     // run kernel reads it there (sorted_copy = 0), so only the foreign bucket's size is needed
     const bool in_order = unsorted[0] != epoch;
