@@ -841,7 +841,10 @@ constexpr unsigned long long kLocPollTicks = 5000;
 #define INA_LOC_U 4                                           // granules per unit (a half chunk)
 #endif
 constexpr uint32_t kLocU = INA_LOC_U;
-constexpr int kLlWaves = 4;                                   // waves per unit in the list build
+#ifndef INA_LL_WAVES
+#define INA_LL_WAVES 4
+#endif
+constexpr int kLlWaves = INA_LL_WAVES;                        // waves per unit in the list build
 constexpr int kLlBins = 1024;                                 // slots one LDS pass counts
 constexpr int kLlBits = 10;
 #ifndef INA_LL_ROUNDS
@@ -2094,14 +2097,13 @@ static_assert(INA_SWITCH_WIN_SMALL >= 1 && INA_SWITCH_WIN_SMALL <= 64 && INA_SWI
 #ifndef INA_SWITCH_ACT_BATCH
 #define INA_SWITCH_ACT_BATCH 1
 #endif
-// forwarded packets: written once per call, never read back by it (lab knobs: sc1, nt)
-#ifndef INA_SWITCH_STORE_SC1
-#define INA_SWITCH_STORE_SC1 0
-#endif
+// forwarded packets: written once per call, never read back by it (lab knob: nt).  Not
+// stream_store: its buffer resource starts at the wave's first active lane, and the lists and
+// sorted paths scatter a wave's rows below it too -- a write-through build of sw_st lost those
+// stores (jitter 64 and shuffled differed from the default build; it was also no faster on the
+// structured orders: profiles/r06/lab/switch_store_sc1_ab.log)
 __device__ __forceinline__ void sw_st(u32x4s v, u32x4s* p) {
-#if INA_SWITCH_STORE_SC1
-    stream_store(v, p);
-#elif INA_SWITCH_FWD_NT
+#if INA_SWITCH_FWD_NT
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
