@@ -222,6 +222,14 @@ constexpr uint32_t kPlainBit = 0x40000000u;
 #define INA_KEYS_FROM_DESC 1
 #endif
 constexpr uint32_t kKeysSpanMax = 65535;      // slots a storing detection wave may span
+// ... and must span more than this: a wave of small local disorder leaves its keys to the
+// descriptors, which the lists then read instead.  NGA-32 C3 split (profiles/r06/lab/
+// keys_span_min_ab_v32.log): jitter 64 289-290 -> 285 us, jitter 512 296 -> 292, jitter 4096
+// unchanged at 128 (its waves span 193-256 slots; a minimum of 256 lost it 13 us)
+#ifndef INA_KEYS_SPAN_MIN
+#define INA_KEYS_SPAN_MIN 128
+#endif
+constexpr uint32_t kKeysSpanMin = INA_KEYS_SPAN_MIN;
 struct KeySrc {
     const uint32_t* keys;
     const uint2* desc;
@@ -1530,7 +1538,7 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         // (a wave in slot order is read from the descriptors) whose slots span at most
         // kKeysSpanMax (a shuffled batch's waves span the pool and take the sort, which reads the
         // descriptors itself)
-        if (kflags && __ballot(down) && kmx >= kmn && kmx - kmn <= kKeysSpanMax) {
+        if (kflags && __ballot(down) && kmx >= kmn && kmx - kmn <= kKeysSpanMax && kmx - kmn > kKeysSpanMin) {
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (i0 + (size_t)r * 64 < npk) kout[i0 + (size_t)r * 64] = k[r];
