@@ -1037,6 +1037,7 @@ __device__ __forceinline__ bool local_decide(const uint32_t* __restrict__ gmin, 
 // lanes of the same slot (a stable counting sort).  ids[e] = packet | PS-ack bit 31 (by its sort
 // key).
 __device__ __forceinline__ size_t switch_block_index();
+__device__ __forceinline__ size_t xcd_block_index();
 #ifndef INA_LL_WAVES_PER_EU
 #define INA_LL_WAVES_PER_EU 8
 #endif
@@ -1058,7 +1059,7 @@ __global__ __launch_bounds__(kLlWaves * 64) __attribute__((amdgpu_waves_per_eu(I
     uint32_t* crow = cw[wv >> 1];
     const unsigned long long below = (1ull << lane) - 1ull;
     const uint32_t kmin = unsorted[kLocKmin], nunits = unsorted[kLocUnits];
-    for (uint32_t u = (uint32_t)switch_block_index(); u < nunits; u += gridDim.x) {
+    for (uint32_t u = (uint32_t)xcd_block_index(); u < nunits; u += gridDim.x) {
         const LocUnit w = units[u];
         if (w.hi <= w.lo) continue;                               // no slot (block-uniform)
         LOC_STAMP(0);
@@ -1355,7 +1356,7 @@ __global__ __launch_bounds__(kBkThr) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     __shared__ uint32_t wgmn[kBkWaves], wgmx[kBkWaves];   // per-wave slot-key bounds (near-sorted path)
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     // (INA_CHUNK_XCD: neighbouring chunks on one XCD, so the (digit, chunk) columns they write share its L2)
-    const size_t c = INA_CHUNK_XCD && kMode == 2 ? switch_block_index() : blockIdx.x;
+    const size_t c = INA_CHUNK_XCD && kMode == 2 ? xcd_block_index() : blockIdx.x;
     // gstat (near-sorted path on): granule bounds, gmin[G] then gmax[G], G = 8 granules a chunk
     const uint32_t G = (uint32_t)nch * (uint32_t)kGranPerChunk;
     if constexpr (kMode == 2) {
@@ -1693,7 +1694,7 @@ __global__ __launch_bounds__(kBkThr, BINS <= 1024 ? 2 * kBkThr / 256 : kBkThr / 
     __shared__ uint32_t red[kBkWaves], red2[kBkWaves];
     const int lane = threadIdx.x & 63, wv = wave_in_block();
     // (INA_BUCKET_XCD: neighbouring buckets on one XCD: their runs in a chunk share lines, read through one L2)
-    uint32_t b = INA_BUCKET_XCD ? (uint32_t)switch_block_index() : blockIdx.x;
+    uint32_t b = INA_BUCKET_XCD ? (uint32_t)xcd_block_index() : blockIdx.x;
 #if INA_BUCKET_GROUP > 1
     {   // groups of INA_BUCKET_GROUP neighbouring buckets on one XCD (blocks go to the XCDs
         // round-robin); the grid's tail past whole groups of 8 x G keeps its own index
@@ -3539,18 +3540,28 @@ __device__ __forceinline__ void switch_runs_body(const ina_switch_state_t& st, u
     }
 }
 
-// XCD-aware window map: blocks b and b + 8 share an XCD (and its L2), so logical block
-// (b % 8) * G/8 + b / 8 gives each XCD one contiguous run of sorted positions -- a slot's
-// neighbours, whose rows share their boundary 128-byte lines, are then gathered through
-// the same L2 (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"; speed only)
+// XCD-contiguous block map: blocks b and b + 8 share an XCD (and its L2), so logical block
+// (b % 8) * G/8 + b / 8 gives each XCD one contiguous run of the logical index
+// (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"; speed only).  The digit pass's
+// chunks and the near-sorted lists' units use it (their neighbours share lines and windows);
+// the run kernel's windows and slot ranges do NOT since round 6 (INA_SWITCH_XCD = 0): each XCD
+// then streams from every part of the batch instead of one eighth of it, and every order ran
+// faster -- NGA-32 split worker-major 207.8 -> 202.5 us, round-robin 232.8 -> 228.0, jitter 64
+// 286.4 -> 281.5, shuffled 384.5 -> 374.8, packed worker-major 259.3 -> 236.2; NGA-256 packed
+// 4-7 us, split worker-major 195.3 -> 180.0; the NGA-256 packet path's switch + PS 219.4 ->
+// 204.1 us (profiles/r06/lab/run_block_map_ab.log).  The near-sorted lists keep the map, in
+// their build and in the run's walk of them: plain, jitter 4096 lost 15-16 us.
 #ifndef INA_SWITCH_XCD
-#define INA_SWITCH_XCD 1
+#define INA_SWITCH_XCD 0
 #endif
-__device__ __forceinline__ size_t switch_block_index() {
-#if INA_SWITCH_XCD
+__device__ __forceinline__ size_t xcd_block_index() {
     const uint32_t G = gridDim.x, b = blockIdx.x, x = b & 7u;
     const uint32_t per = G >> 3, rem = G & 7u;
     return (size_t)x * per + (x < rem ? x : rem) + (b >> 3);
+}
+__device__ __forceinline__ size_t switch_block_index() {
+#if INA_SWITCH_XCD
+    return xcd_block_index();
 #else
     return blockIdx.x;
 #endif
@@ -3593,8 +3604,12 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(kPs ? 
         const uint32_t ep = unsorted[1];
         if (unsorted[kLocEpoch] == ep) {                   // a near-sorted batch: its per-slot lists
             if constexpr (kNarrow)
+                // (the lists' slots XCD-contiguous: neighbouring slots' lists point into the same
+                // arrival windows, whose rows then come through one L2 -- the plain map cost
+                // jitter 4096 16 us)
                 lists_slots_narrow<kPs, kSplit>(st, pkts, stride, pay, actions, ps, loc_ids, loc_tab,
-                                                unsorted[kLocKmin], unsorted[kLocSlots], wave, nwaves);
+                                                unsorted[kLocKmin], unsorted[kLocSlots],
+                                                xcd_block_index() * (kSwBlock / 64) + wave_in_block(), nwaves);
             return;
         }
         if (unsorted[2] == ep) {
