@@ -2061,6 +2061,10 @@ constexpr int kB = INA_SWITCH_BATCH;         // packets of a segment loaded at o
 #ifndef INA_SWITCH_WIN_SMALL
 #define INA_SWITCH_WIN_SMALL 8
 #endif
+#ifndef INA_SWITCH_WIN_NARROW
+#define INA_SWITCH_WIN_NARROW 64
+#endif
+static_assert(INA_SWITCH_WIN_NARROW >= 1 && INA_SWITCH_WIN_NARROW <= 64, "a narrow window's heads are one wave's lanes");
 #ifndef INA_SWITCH_WIN_LARGE
 #define INA_SWITCH_WIN_LARGE 16
 #endif
@@ -4162,7 +4166,7 @@ static int switch_process_impl(const ina_switch_state_t* st, uint8_t* pkts, size
         uint32_t win = npk <= 65536 ? (uint32_t)INA_SWITCH_WIN_SMALL : (uint32_t)INA_SWITCH_WIN_LARGE;
         // a narrow wave moves a whole segment per batch: a window of 64 sorted positions
         // (about 8 segments) keeps the grid at npk / 256 workgroups
-        if (narrow && (INA_SWITCH_NARROW_SLOTS || npk > 65536)) win = 64;   // 8 lane groups: ~8 segments
+        if (narrow && (INA_SWITCH_NARROW_SLOTS || npk > 65536)) win = INA_SWITCH_WIN_NARROW;   // 8 lane groups: ~8 segments
         if (const int wv = t.win) win = (uint32_t)wv;
         const size_t per_block = (size_t)win * (kSwBlock / 64);
         unsigned gr = (unsigned)std::min<size_t>((npk + per_block - 1) / per_block, INA_SWITCH_GRID);
