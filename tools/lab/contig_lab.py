@@ -2,7 +2,8 @@
 """Placement lab (experiment only): the NGA-32 C3 round-robin split-row switch call with its
 header rows, payload rows and slot registers in torch's default allocations, against the same
 arrays in physically contiguous allocations (hipExtMallocWithFlags(hipDeviceMallocContiguous)),
-wrapped as torch tensors through __cuda_array_interface__.  Each kind is allocated afresh REPS
+wrapped as torch tensors through __cuda_array_interface__ (KINDS: torch, contiguous = all three,
+rows = header + payload rows only, regs = slot registers only).  Each kind is allocated afresh REPS
 times, alternating, with a large allocation freed in between to change the allocator's history;
 HIP events around K back-to-back calls, median of ROUNDS.  Env: K, ROUNDS, REPS, ORDER (rr,
 wm), V (32 or 256)."""
@@ -80,21 +81,26 @@ def timed(fn):
     return a.elapsed_time(b) * 1e3 / K
 
 
-res = {"torch": [], "contiguous": []}
+KINDS = os.environ.get("KINDS", "torch,contiguous").split(",")   # + rows (hdr + pay only), regs (regs only)
+res = {k: [] for k in KINDS}
 for rep in range(REPS):
-    for kind in ("torch", "contiguous"):
+    for kind in KINDS:
         churn = torch.empty((8 + 4 * rep) << 30, dtype=torch.uint8, device=dev)   # allocator history
         del churn
         keep = []
-        if kind == "torch":
-            hdr = torch.empty((N, 16), dtype=torch.uint8, device=dev)
-            pay = torch.empty((N, 4 * V), dtype=torch.uint8, device=dev)
-            regs = torch.zeros((slots, V), dtype=torch.int32, device=dev)
-        else:
+        rows_c = kind in ("contiguous", "rows")
+        regs_c = kind in ("contiguous", "regs")
+        if rows_c:
             hdr = contiguous(N * 16, keep).view(N, 16)
             pay = contiguous(N * 4 * V, keep).view(N, 4 * V)
+        else:
+            hdr = torch.empty((N, 16), dtype=torch.uint8, device=dev)
+            pay = torch.empty((N, 4 * V), dtype=torch.uint8, device=dev)
+        if regs_c:
             regs = contiguous(slots * V * 4, keep).view(torch.int32).view(slots, V)
             regs.zero_()
+        else:
+            regs = torch.zeros((slots, V), dtype=torch.int32, device=dev)
         hdr.copy_(hdr0)
         pay.copy_(pay0)
         sw = ops.Switch(V, num_slots=slots, switch_id=1, device=dev)
